@@ -1,0 +1,17 @@
+"""llm_training_amd — an MI355X-native (gfx950, ROCm) LLM training framework.
+
+Same capabilities and YAML surface as cchou0519/LLM-Training (``llm-training fit --config cfg.yaml``),
+re-designed for CDNA4: hand-written HIP kernels for the hot ops, a flat-buffer ZeRO engine and
+tensor/sequence parallelism over RCCL/xGMI, one process per GPU.
+"""
+import logging
+
+__version__ = "0.1.0"
+
+logger = logging.getLogger("llm_training")
+if not logger.handlers:
+    _h = logging.StreamHandler()
+    _h.setFormatter(logging.Formatter("[%(asctime)s] [%(levelname)s] %(message)s", "%Y-%m-%d %H:%M:%S"))
+    logger.addHandler(_h)
+    logger.setLevel(logging.INFO)
+    logger.propagate = False

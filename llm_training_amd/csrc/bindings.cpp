@@ -1,0 +1,350 @@
+// Torch operator registrations for the gfx950 kernels (namespace `llmt`, loaded with
+// torch.ops.load_library). Every op runs on torch's current HIP stream, validates shapes on the host
+// before launching (a mis-shaped launch can fault the GPU), and raises if a launch fails.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <torch/library.h>
+
+#include <hip/hip_runtime.h>
+
+#include <tuple>
+#include <vector>
+
+extern "C" {
+hipError_t llmt_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* res_out, float* rstd,
+                            int T, int H, float eps, hipStream_t stream);
+int llmt_rmsnorm_bwd_nblocks(int T);
+hipError_t llmt_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres,
+                            void* dx, float* dw_part, void* dw, int dw_is_fp32, int accumulate, int T, int H,
+                            hipStream_t stream);
+hipError_t llmt_swiglu_fwd(const void* gu, void* c, int64_t T, int I, hipStream_t stream);
+hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu, int64_t T, int I, hipStream_t stream);
+hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const float* cos_t, const float* sin_t, int64_t T,
+                     int nheads, int D, int64_t stride_t, int stride_h, int inverse, hipStream_t stream);
+hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const int64_t* labels,
+                              int64_t vocab_start, int64_t ignore_index, const float* lse_in, float* lse_out,
+                              float* tgt_out, float* loss_out, const float* coef_row, const float* coef_scalar,
+                              int write_grad, hipStream_t stream);
+hipError_t llmt_adamw(float* p, float* m, float* v, const void* g, int grad_is_fp32, void* pout, int64_t n,
+                      float lr, float b1, float b2, float eps, float wd, int64_t step, const float* gscale,
+                      hipStream_t stream);
+hipError_t llmt_sumsq(const void* x, int is_fp32, int64_t n, float* out, hipStream_t stream);
+hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* seg,
+                               int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss, int64_t q_sh,
+                               int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh,
+                               int64_t o_sb, int64_t o_ss, int64_t o_sh, float scale, int causal, int window,
+                               hipStream_t stream);
+hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                               const float* lse, float* delta, const int* seg, void* dq, void* dk, void* dv,
+                               float* work, int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss,
+                               int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss,
+                               int64_t v_sh, int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss,
+                               int64_t dq_sh, int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb,
+                               int64_t dv_ss, int64_t dv_sh, float scale, int causal, int window,
+                               hipStream_t stream);
+}
+
+namespace {
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+inline void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "llmt kernel '", what, "' failed: ", hipGetErrorString(e));
+}
+
+inline void check_bf16_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+
+inline void check_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+}
+
+// ---------------------------------------------------------------- RMSNorm
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                                           const at::Tensor& w, double eps) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "weight");
+  check_rows(x, "x");
+  const int64_t H = x.size(-1);
+  TORCH_CHECK(w.numel() == H && w.is_contiguous(), "weight shape mismatch");
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "rmsnorm: hidden size must be a multiple of 8 and <= 8192");
+  const int64_t T = x.numel() / H;
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({T}, x.options().dtype(at::kFloat));
+  at::Tensor res_out;
+  const void* rp = nullptr;
+  void* rop = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_bf16_cuda(*res, "residual");
+    check_rows(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch");
+    res_out = at::empty_like(x);
+    rp = res->data_ptr();
+    rop = res_out.data_ptr();
+  }
+  check(llmt_rmsnorm_fwd(x.data_ptr(), rp, w.data_ptr(), y.data_ptr(), rop, rstd.data_ptr<float>(), (int)T, (int)H,
+                         (float)eps, cur_stream()),
+        "rmsnorm_fwd");
+  return {y, res_out.defined() ? res_out : at::Tensor(), rstd};
+}
+
+// dw_out: if given (bf16 or fp32, numel H) the weight gradient is written (accumulate=false) or added
+// (accumulate=true) into it in place; otherwise a new fp32 tensor is returned.
+std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                               const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                                               const c10::optional<at::Tensor>& dw_out, bool accumulate,
+                                               bool compute_dw) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(x, "x");
+  check_rows(dy, "dy");
+  check_rows(x, "x");
+  const int64_t H = x.size(-1);
+  const int64_t T = x.numel() / H;
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
+  TORCH_CHECK(rstd.numel() == T && rstd.scalar_type() == at::kFloat, "rstd mismatch");
+  auto dx = at::empty_like(x);
+  const void* drp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    check_bf16_cuda(*dres, "dres");
+    check_rows(*dres, "dres");
+    TORCH_CHECK(dres->sizes() == x.sizes(), "dres shape mismatch");
+    drp = dres->data_ptr();
+  }
+  at::Tensor dw;
+  void* dwp = nullptr;
+  int dw_fp32 = 1;
+  if (compute_dw) {
+    if (dw_out.has_value() && dw_out->defined()) {
+      dw = *dw_out;
+      TORCH_CHECK(dw.numel() == H && dw.is_contiguous() && dw.is_cuda(), "dw_out mismatch");
+      TORCH_CHECK(dw.scalar_type() == at::kFloat || dw.scalar_type() == at::kBFloat16, "dw_out dtype");
+      dw_fp32 = dw.scalar_type() == at::kFloat;
+    } else {
+      dw = at::empty({H}, x.options().dtype(at::kFloat));
+      accumulate = false;
+    }
+    dwp = dw.data_ptr();
+  }
+  const int nblk = llmt_rmsnorm_bwd_nblocks((int)T);
+  auto part = at::empty({compute_dw ? (int64_t)nblk * H : H}, x.options().dtype(at::kFloat));
+  check(llmt_rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), drp, dx.data_ptr(),
+                         part.data_ptr<float>(), dwp, dw_fp32, accumulate ? 1 : 0, (int)T, (int)H, cur_stream()),
+        "rmsnorm_bwd");
+  return {dx, dw};
+}
+
+// ---------------------------------------------------------------- SwiGLU
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  check_bf16_cuda(gu, "gate_up");
+  check_rows(gu, "gate_up");
+  const int64_t I2 = gu.size(-1);
+  TORCH_CHECK(I2 % 16 == 0, "swiglu: intermediate size must be a multiple of 8");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I2 / 2;
+  auto c = at::empty(sizes, gu.options());
+  check(llmt_swiglu_fwd(gu.data_ptr(), c.data_ptr(), gu.numel() / I2, (int)(I2 / 2), cur_stream()), "swiglu_fwd");
+  return c;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dc) {
+  check_bf16_cuda(gu, "gate_up");
+  check_bf16_cuda(dc, "grad");
+  check_rows(gu, "gate_up");
+  check_rows(dc, "grad");
+  const int64_t I2 = gu.size(-1);
+  TORCH_CHECK(dc.numel() * 2 == gu.numel() && dc.size(-1) * 2 == I2, "swiglu_bwd shape mismatch");
+  auto dgu = at::empty_like(gu);
+  check(llmt_swiglu_bwd(gu.data_ptr(), dc.data_ptr(), dgu.data_ptr(), gu.numel() / I2, (int)(I2 / 2), cur_stream()),
+        "swiglu_bwd");
+  return dgu;
+}
+
+// ---------------------------------------------------------------- RoPE (in place)
+// qkv: [..., T, nh_total, D] with unit stride on D; rotates the first `nheads` heads.
+void rope_(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t, int64_t nheads,
+           bool inverse) {
+  check_bf16_cuda(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() >= 3, "rope: qkv must be [T, H, D]");
+  const int64_t D = qkv.size(-1);
+  TORCH_CHECK(qkv.stride(-1) == 1, "rope: head dim must be contiguous");
+  TORCH_CHECK(D % 16 == 0, "rope: head dim must be a multiple of 16");
+  TORCH_CHECK(nheads <= qkv.size(-2), "rope: nheads out of range");
+  // flatten all leading dims into T (they must be uniformly strided)
+  const int64_t T = qkv.numel() / (qkv.size(-1) * qkv.size(-2));
+  const int64_t stride_t = qkv.stride(-3);
+  for (int d = 0; d < qkv.dim() - 3; ++d)
+    TORCH_CHECK(qkv.stride(d) == qkv.stride(d + 1) * qkv.size(d + 1), "rope: leading dims not flattenable");
+  TORCH_CHECK(pos.numel() == T && pos.is_contiguous() && pos.is_cuda(), "rope: positions must be [T] contiguous");
+  TORCH_CHECK(pos.scalar_type() == at::kLong || pos.scalar_type() == at::kInt, "rope: positions must be int");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.size(-1) * 2 == D,
+              "rope: cos/sin tables must be fp32 [max_pos, D/2]");
+  check(llmt_rope(qkv.data_ptr(), pos.data_ptr(), pos.scalar_type() == at::kLong, cos_t.data_ptr<float>(),
+                  sin_t.data_ptr<float>(), T, (int)nheads, (int)D, stride_t, (int)qkv.stride(-2), inverse ? 1 : 0,
+                  cur_stream()),
+        "rope");
+}
+
+// ---------------------------------------------------------------- cross entropy
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_(at::Tensor logits, const at::Tensor& labels,
+                                                             int64_t vocab_start, int64_t ignore_index,
+                                                             const c10::optional<at::Tensor>& lse_in,
+                                                             const c10::optional<at::Tensor>& coef_row,
+                                                             const c10::optional<at::Tensor>& coef_scalar,
+                                                             bool write_grad) {
+  check_bf16_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] with unit column stride");
+  const int64_t N = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(labels.numel() == N && labels.scalar_type() == at::kLong && labels.is_contiguous(), "labels mismatch");
+  auto opts = logits.options().dtype(at::kFloat);
+  auto lse = at::empty({N}, opts), tgt = at::empty({N}, opts), loss = at::empty({N}, opts);
+  auto fptr = [&](const c10::optional<at::Tensor>& t, int64_t n) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == n && t->is_cuda(),
+                "cross_entropy: fp32 side input mismatch");
+    return t->data_ptr<float>();
+  };
+  check(llmt_cross_entropy(logits.data_ptr(), N, logits.stride(0), (int)V, labels.data_ptr<int64_t>(), vocab_start,
+                           ignore_index, fptr(lse_in, N), lse.data_ptr<float>(), tgt.data_ptr<float>(),
+                           loss.data_ptr<float>(), fptr(coef_row, N), fptr(coef_scalar, 1), write_grad ? 1 : 0,
+                           cur_stream()),
+        "cross_entropy");
+  return {lse, tgt, loss};
+}
+
+// ---------------------------------------------------------------- optimizer
+void adamw_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g, const c10::optional<at::Tensor>& pout,
+            double lr, double b1, double b2, double eps, double wd, int64_t step,
+            const c10::optional<at::Tensor>& gscale) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "adamw: master/m/v must be fp32");
+  TORCH_CHECK(p.is_contiguous() && m.is_contiguous() && v.is_contiguous() && g.is_contiguous(), "adamw: contiguous");
+  TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n, "adamw: size mismatch");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "adamw: grad dtype");
+  TORCH_CHECK(n % 4 == 0, "adamw: flat buffers must be padded to a multiple of 4");
+  void* po = nullptr;
+  if (pout.has_value() && pout->defined()) {
+    TORCH_CHECK(pout->numel() == n && pout->scalar_type() == at::kBFloat16 && pout->is_contiguous(), "adamw: pout");
+    po = pout->data_ptr();
+  }
+  const float* gs = nullptr;
+  if (gscale.has_value() && gscale->defined()) {
+    TORCH_CHECK(gscale->scalar_type() == at::kFloat && gscale->numel() == 1, "adamw: gscale");
+    gs = gscale->data_ptr<float>();
+  }
+  check(llmt_adamw(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr(),
+                   g.scalar_type() == at::kFloat, po, n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, step,
+                   gs, cur_stream()),
+        "adamw");
+}
+
+void sumsq_(const at::Tensor& x, at::Tensor out) {
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 4 == 0, "sumsq: contiguous, numel % 4 == 0");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "sumsq dtype");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "sumsq out");
+  check(llmt_sumsq(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), out.data_ptr<float>(), cur_stream()),
+        "sumsq");
+}
+
+// ---------------------------------------------------------------- flash attention
+// q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (any batch/seq/head strides, unit stride on D).
+// seg: optional int32 [B, S] segment ids (0 = padding): attention is restricted to equal ids.
+std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                  const c10::optional<at::Tensor>& seg, double scale, bool causal,
+                                                  int64_t window) {
+  check_bf16_cuda(q, "q");
+  check_bf16_cuda(k, "k");
+  check_bf16_cuda(v, "v");
+  TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "flash_attn: q/k/v must be [B, S, H, D]");
+  const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int64_t Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && k.size(1) == S && k.size(3) == D && v.sizes() == k.sizes(), "flash_attn: k/v shape");
+  TORCH_CHECK(Hq % Hkv == 0, "flash_attn: Hq must be a multiple of Hkv");
+  TORCH_CHECK(D == 64 || D == 96 || D == 128, "flash_attn: head dim must be 64, 96 or 128");
+  TORCH_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1, "flash_attn: unit stride on head dim");
+  // O keeps q's batch/sequence memory order (seq-major activations stay seq-major: no copies)
+  auto o = (q.stride(0) >= q.stride(1)) ? at::empty({B, S, Hq, D}, q.options())
+                                        : at::empty({S, B, Hq, D}, q.options()).transpose(0, 1);
+  auto lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  const int* sp = nullptr;
+  if (seg.has_value() && seg->defined()) {
+    TORCH_CHECK(seg->scalar_type() == at::kInt && seg->is_contiguous() && seg->numel() == B * S, "flash_attn: seg");
+    sp = seg->data_ptr<int>();
+  }
+  check(llmt_flash_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), sp, (int)B,
+                            (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(0), q.stride(1), q.stride(2), k.stride(0),
+                            k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1),
+                            o.stride(2), (float)scale, causal ? 1 : 0, (int)window, cur_stream()),
+        "flash_attn_fwd");
+  return {o, lse};
+}
+
+// dq/dk/dv are written into caller-provided tensors (so they can be views of one fused dQKV buffer).
+void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+                    const at::Tensor& dout, const at::Tensor& lse, const c10::optional<at::Tensor>& seg, at::Tensor dq,
+                    at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window) {
+  const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int64_t Hkv = k.size(2);
+  check_bf16_cuda(dout, "dout");
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes(), "flash_attn_bwd: o/dout shape");
+  TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "flash_attn_bwd: grads");
+  TORCH_CHECK(dout.stride(3) == 1 && o.stride(3) == 1 && dq.stride(3) == 1 && dk.stride(3) == 1 && dv.stride(3) == 1,
+              "flash_attn_bwd: unit stride on head dim");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == B * Hq * S, "flash_attn_bwd: lse");
+  const int* sp = nullptr;
+  if (seg.has_value() && seg->defined()) sp = seg->data_ptr<int>();
+  auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  TORCH_CHECK(dout.strides() == o.strides(), "flash_attn_bwd: dout must share O's layout");
+  at::Tensor work;  // fp32 per-q-head dK/dV partials, only needed for GQA
+  if (Hq != Hkv) work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
+  check(llmt_flash_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                            lse.data_ptr<float>(), delta.data_ptr<float>(), sp, dq.data_ptr(), dk.data_ptr(),
+                            dv.data_ptr(), work.defined() ? work.data_ptr<float>() : nullptr, (int)B, (int)S, (int)Hq, (int)Hkv, (int)D,
+                            q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0),
+                            v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
+                            dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0),
+                            dv.stride(1), dv.stride(2), (float)scale, causal ? 1 : 0, (int)window, cur_stream()),
+        "flash_attn_bwd");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(llmt, m) {
+  m.def("rmsnorm_fwd(Tensor x, Tensor? res, Tensor w, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def(
+      "rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres, Tensor(a!)? dw_out, bool accumulate, "
+      "bool compute_dw) -> (Tensor, Tensor)");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor gu, Tensor dc) -> Tensor");
+  m.def("rope_(Tensor(a!) qkv, Tensor pos, Tensor cos, Tensor sin, int nheads, bool inverse) -> ()");
+  m.def(
+      "cross_entropy_(Tensor(a!) logits, Tensor labels, int vocab_start, int ignore_index, Tensor? lse_in, "
+      "Tensor? coef_row, Tensor? coef_scalar, bool write_grad) -> (Tensor, Tensor, Tensor)");
+  m.def(
+      "adamw_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? pout, float lr, float b1, float b2, "
+      "float eps, float wd, int step, Tensor? gscale) -> ()");
+  m.def("sumsq_(Tensor x, Tensor(a!) out) -> ()");
+  m.def(
+      "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window) -> (Tensor, "
+      "Tensor)");
+  m.def(
+      "flash_attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor? seg, Tensor(a!) dq, "
+      "Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int window) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
+  m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("rope_", &rope_);
+  m.impl("cross_entropy_", &cross_entropy_);
+  m.impl("adamw_", &adamw_);
+  m.impl("sumsq_", &sumsq_);
+  m.impl("flash_attn_fwd", &flash_attn_fwd);
+  m.impl("flash_attn_bwd", &flash_attn_bwd);
+}

@@ -1,0 +1,138 @@
+// Cross-entropy / log-softmax statistics with in-place gradient for gfx950.
+//
+// Replaces the reference's LigerCrossEntropyFunction (grad-in-forward online softmax,
+// reference src/llm_training/ops/liger_kernel/cross_entropy_op.py:10-33) and the torch
+// loss_parallel / log_softmax().gather() paths of DPO/ORPO (reference
+// src/llm_training/lms/dpo/dpo.py:73-114, lms/orpo/orpo.py:61-93).
+//
+// One 256-thread workgroup per row of bf16 logits [N, V_local] (the row is streamed in 16-byte
+// vectors). Pass 1: per-thread online max / sum-exp, block-reduced -> lse. Pass 2 (optional):
+// overwrite the row with coef * (softmax - onehot(label)), i.e. the gradient of
+//   coef * (lse - logit[label])
+// w.r.t. the logits, so the logits buffer doubles as the dlogits buffer (no extra [N, V] tensor).
+//
+// Vocab-parallel (TP) use: `vocab_start` offsets the label into this rank's vocab shard; pass 1 is
+// run alone (write_grad=0) to produce the LOCAL lse and target logit, the caller combines lse across
+// ranks (one small RCCL all-gather/all-reduce), then pass 2 is run with lse_in = the global lse.
+#include "common.h"
+
+namespace llmt {
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int64_t ld, int V,
+                                                 const int64_t* __restrict__ labels, int64_t vocab_start,
+                                                 int64_t ignore_index, const float* __restrict__ lse_in,
+                                                 float* __restrict__ lse_out, float* __restrict__ tgt_out,
+                                                 float* __restrict__ loss_out, const float* __restrict__ coef_row,
+                                                 const float* __restrict__ coef_scalar, int write_grad) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  bf16* x = logits + row * ld;
+  const int64_t lab = labels[row];
+  const bool valid = lab != ignore_index;
+  const int64_t lloc = lab - vocab_start;
+  const bool local_hit = valid && lloc >= 0 && lloc < V;
+  const int tid = threadIdx.x;
+
+  float lse;
+  if (lse_in) {
+    lse = lse_in[row];
+  } else {
+    float m = -INFINITY, s = 0.f;
+    if constexpr (VEC) {
+      const bf16x8* xv = reinterpret_cast<const bf16x8*>(x);
+      const int V8 = V >> 3;
+      for (int j = tid; j < V8; j += 256) {
+        float f[8];
+        unpack8(xv[j], f);
+        float lm = f[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) lm = fmaxf(lm, f[i]);
+        if (lm > m) {
+          s *= __expf(m - lm);
+          m = lm;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += __expf(f[i] - m);
+      }
+      for (int j = (V8 << 3) + tid; j < V; j += 256) {
+        const float f = bf2f(x[j]);
+        if (f > m) {
+          s *= __expf(m - f);
+          m = f;
+        }
+        s += __expf(f - m);
+      }
+    } else {
+      for (int j = tid; j < V; j += 256) {
+        const float f = bf2f(x[j]);
+        if (f > m) {
+          s *= __expf(m - f);
+          m = f;
+        }
+        s += __expf(f - m);
+      }
+    }
+    const float gm = block_max<4>(m, red);
+    s = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
+    const float gs = block_sum<4>(s, red);
+    lse = gm + __logf(gs);
+  }
+  const float tgt = local_hit ? bf2f(x[lloc]) : 0.f;
+  if (tid == 0) {
+    if (lse_out) lse_out[row] = lse;
+    if (tgt_out) tgt_out[row] = tgt;
+    if (loss_out) loss_out[row] = valid ? (lse - tgt) : 0.f;
+  }
+  if (!write_grad) return;
+  __syncthreads();  // every thread has read x[lloc] before anyone overwrites it
+  float coef = valid ? 1.f : 0.f;
+  if (coef_row) coef *= coef_row[row];
+  if (coef_scalar) coef *= coef_scalar[0];
+  if constexpr (VEC) {
+    bf16x8* xv = reinterpret_cast<bf16x8*>(x);
+    const int V8 = V >> 3;
+    for (int j = tid; j < V8; j += 256) {
+      float f[8];
+      unpack8(xv[j], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float g = __expf(f[i] - lse);
+        if (local_hit && (int64_t)(j * 8 + i) == lloc) g -= 1.f;
+        f[i] = coef * g;
+      }
+      xv[j] = pack8(f);
+    }
+    for (int j = (V8 << 3) + tid; j < V; j += 256) {
+      float g = __expf(bf2f(x[j]) - lse);
+      if (local_hit && j == lloc) g -= 1.f;
+      x[j] = __float2bfloat16(coef * g);
+    }
+  } else {
+    for (int j = tid; j < V; j += 256) {
+      float g = __expf(bf2f(x[j]) - lse);
+      if (local_hit && j == lloc) g -= 1.f;
+      x[j] = __float2bfloat16(coef * g);
+    }
+  }
+}
+
+}  // namespace llmt
+
+using namespace llmt;
+
+extern "C" hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const int64_t* labels,
+                                         int64_t vocab_start, int64_t ignore_index, const float* lse_in,
+                                         float* lse_out, float* tgt_out, float* loss_out, const float* coef_row,
+                                         const float* coef_scalar, int write_grad, hipStream_t stream) {
+  if (N == 0) return hipSuccess;
+  const bool vec = (ld % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) & 15) == 0);
+  if (vec)
+    ce_kernel<true><<<(unsigned)N, 256, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index, lse_in,
+                                                     lse_out, tgt_out, loss_out, coef_row, coef_scalar, write_grad);
+  else
+    ce_kernel<false><<<(unsigned)N, 256, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index,
+                                                      lse_in, lse_out, tgt_out, loss_out, coef_row, coef_scalar,
+                                                      write_grad);
+  return hipGetLastError();
+}

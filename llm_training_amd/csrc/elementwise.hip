@@ -1,0 +1,135 @@
+// Fused elementwise kernels for gfx950: SwiGLU (SiLU·mul) and rotary position embedding.
+//
+// SwiGLU replaces the reference's LigerSiLUMulFunction (reference call sites
+// src/llm_training/ops/liger_kernel/swiglu_op.py:36-39 <- models/llama/llama_model.py:427). Our MLP
+// keeps gate and up projections in ONE fused GEMM whose output row is [gate(I) | up(I)], so the
+// kernel reads the fused [T, 2I] buffer directly (no torch.chunk views, no copies).
+//
+// RoPE replaces src/llm_training/ops/rope_op.py:10-20. It runs IN PLACE on the
+// fused QKV GEMM output [T, Hq+2Hkv, D] for the q and k heads, gathering cos/sin from a
+// precomputed fp32 table by position id (packed-sequence aware: any position layout works).
+// Backward is the same kernel with the rotation negated (rotate by -theta).
+#include "common.h"
+
+namespace llmt {
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// c[t, j] = silu(gu[t, j]) * gu[t, I + j]
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16x8* __restrict__ gu, bf16x8* __restrict__ c,
+                                                         int64_t n8, int I8) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n8; e += (int64_t)gridDim.x * 256) {
+    const int64_t t = e / I8;
+    const int j = (int)(e - t * I8);
+    float a[8], b[8], o[8];
+    unpack8(gu[t * 2 * I8 + j], a);
+    unpack8(gu[t * 2 * I8 + I8 + j], b);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = a[i] * sigmoidf_(a[i]) * b[i];
+    c[e] = pack8(o);
+  }
+}
+
+// d gate = dc * b * s * (1 + a * (1 - s)),  d up = dc * a * s
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16x8* __restrict__ gu, const bf16x8* __restrict__ dc,
+                                                         bf16x8* __restrict__ dgu, int64_t n8, int I8) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n8; e += (int64_t)gridDim.x * 256) {
+    const int64_t t = e / I8;
+    const int j = (int)(e - t * I8);
+    float a[8], b[8], g[8], da[8], db[8];
+    unpack8(gu[t * 2 * I8 + j], a);
+    unpack8(gu[t * 2 * I8 + I8 + j], b);
+    unpack8(dc[e], g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float s = sigmoidf_(a[i]);
+      const float silu = a[i] * s;
+      da[i] = g[i] * b[i] * s * (1.f + a[i] * (1.f - s));
+      db[i] = g[i] * silu;
+    }
+    dgu[t * 2 * I8 + j] = pack8(da);
+    dgu[t * 2 * I8 + I8 + j] = pack8(db);
+  }
+}
+
+// In-place rotary embedding (HF rotate_half convention): for i < D/2,
+//   y[i]       = x[i] * cos - x[i+D/2] * sin
+//   y[i+D/2]   = x[i+D/2] * cos + x[i] * sin
+// One thread owns 8 consecutive pairs of one (token, head). sign = -1 applies the inverse rotation.
+template <typename PosT>
+__global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const PosT* __restrict__ pos,
+                                                   const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                                                   int64_t T, int nheads, int D, int64_t stride_t, int stride_h,
+                                                   float sign) {
+  const int half = D >> 1;
+  const int groups = half >> 3;  // 8 pairs per thread
+  const int64_t total = T * nheads * groups;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int g = (int)(e % groups);
+    const int64_t th = e / groups;
+    const int h = (int)(th % nheads);
+    const int64_t t = th / nheads;
+    const int64_t p = (int64_t)pos[t];
+    bf16* base = qkv + t * stride_t + (int64_t)h * stride_h + g * 8;
+    bf16x8* lo = reinterpret_cast<bf16x8*>(base);
+    bf16x8* hi = reinterpret_cast<bf16x8*>(base + half);
+    const float4* cp = reinterpret_cast<const float4*>(cos_t + p * half + g * 8);
+    const float4* sp = reinterpret_cast<const float4*>(sin_t + p * half + g * 8);
+    float c[8], s[8];
+    *reinterpret_cast<float4*>(c) = cp[0];
+    *reinterpret_cast<float4*>(c + 4) = cp[1];
+    *reinterpret_cast<float4*>(s) = sp[0];
+    *reinterpret_cast<float4*>(s + 4) = sp[1];
+    float x1[8], x2[8], y1[8], y2[8];
+    unpack8(*lo, x1);
+    unpack8(*hi, x2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sn = sign * s[i];
+      y1[i] = x1[i] * c[i] - x2[i] * sn;
+      y2[i] = x2[i] * c[i] + x1[i] * sn;
+    }
+    *lo = pack8(y1);
+    *hi = pack8(y2);
+  }
+}
+
+}  // namespace llmt
+
+using namespace llmt;
+
+extern "C" hipError_t llmt_swiglu_fwd(const void* gu, void* c, int64_t T, int I, hipStream_t stream) {
+  if (I % 8) return hipErrorInvalidValue;
+  const int64_t n8 = T * (I / 8);
+  if (n8 == 0) return hipSuccess;
+  swiglu_fwd_kernel<<<stream_grid(n8, 256), 256, 0, stream>>>((const bf16x8*)gu, (bf16x8*)c, n8, I / 8);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu, int64_t T, int I,
+                                      hipStream_t stream) {
+  if (I % 8) return hipErrorInvalidValue;
+  const int64_t n8 = T * (I / 8);
+  if (n8 == 0) return hipSuccess;
+  swiglu_bwd_kernel<<<stream_grid(n8, 256), 256, 0, stream>>>((const bf16x8*)gu, (const bf16x8*)dc, (bf16x8*)dgu,
+                                                               n8, I / 8);
+  return hipGetLastError();
+}
+
+// qkv: bf16, element strides stride_t (token) / stride_h (head); pos: int32 (pos_is_64=0) or int64.
+extern "C" hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const float* cos_t, const float* sin_t,
+                                int64_t T, int nheads, int D, int64_t stride_t, int stride_h, int inverse,
+                                hipStream_t stream) {
+  if (D % 16) return hipErrorInvalidValue;
+  const int64_t total = T * nheads * (D / 16);
+  if (total == 0) return hipSuccess;
+  const int grid = stream_grid(total, 256);
+  const float sign = inverse ? -1.f : 1.f;
+  if (pos_is_64)
+    rope_kernel<int64_t><<<grid, 256, 0, stream>>>((bf16*)qkv, (const int64_t*)pos, cos_t, sin_t, T, nheads, D,
+                                                   stride_t, stride_h, sign);
+  else
+    rope_kernel<int32_t><<<grid, 256, 0, stream>>>((bf16*)qkv, (const int32_t*)pos, cos_t, sin_t, T, nheads, D,
+                                                   stride_t, stride_h, sign);
+  return hipGetLastError();
+}

@@ -1,0 +1,694 @@
+// Flash attention forward / backward for gfx950 (CDNA4) with MFMA 32x32x16 bf16.
+//
+// Replaces flash-attn 2 (CUDA) `flash_attn_func` / `flash_attn_varlen_func` (SURVEY K6/K7/K8;
+// reference call sites src/llm_training/ops/attention_op.py:538-654 <- models/llama/llama_model.py:570-663).
+// Instead of unpad -> varlen -> pad (attention_op.py:415-485) the kernels take the padded [B, S, H, D]
+// layout directly plus optional per-token segment ids (the reference's packed attention-mask contract,
+// SURVEY Q1): a key is visible to a query iff seg[q] == seg[k] (and k <= q when causal, and
+// k >= q - window when a sliding window is set). GQA is native (kv head = q head / (Hq/Hkv)).
+// q/k/v may be arbitrary strided views (e.g. slices of one fused QKV GEMM output) — no copies.
+//
+// Layout choices (all wave64, MFMA v_mfma_f32_32x32x16_bf16):
+//  * forward / dQ: "swapped" S^T = K·Q^T, so each lane owns ONE query (the MFMA column) and holds its
+//    scores for 16 keys in registers: softmax max / sum are lane-local plus one cross-half shuffle.
+//    The S^T accumulator is directly the B operand of O^T += V^T·P^T (accumulator-as-operand: registers
+//    8s..8s+7 = k-step s), and V^T comes from LDS via ds_read_b64_tr_b16 (hardware transpose read).
+//  * dK/dV: S = Q·K^T with the KEY on the lane; P and dS accumulators are directly the B operands of
+//    dV^T += dO^T·P and dK^T += Q^T·dS; dO^T / Q^T come from transposed LDS reads.
+//  * dQ is a separate query-parallel pass (recomputes S and dP) so the backward needs no atomics and
+//    is bitwise deterministic (the reference only offers determinism via FLASH_ATTENTION_DETERMINISTIC,
+//    attention_op.py:590-592).
+//  * LDS row pitches are chosen per read kind: (2D+16) bytes makes 16 consecutive rows hit distinct
+//    16-byte bank slots for ds_read_b128; 320/192 bytes put the 4 rows of a tr-read block in disjoint
+//    16-bank ranges.
+//  * K/V (or Q/dO) tiles are register-staged: the next tile's global loads are issued before the
+//    current tile's MFMAs and written to LDS after the barrier (async-stage split).
+//  * query blocks are scheduled heaviest-first (reverse order) so the causal triangle load-balances.
+#include "common.h"
+
+namespace llmt {
+
+typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
+typedef short s16v4 __attribute__((ext_vector_type(4)));
+typedef short s16v8 __attribute__((ext_vector_type(8)));
+typedef float f32v16 __attribute__((ext_vector_type(16)));
+typedef float f32v8 __attribute__((ext_vector_type(8)));
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ f32v16 mfma32(const bfv8& a, const bfv8& b, const f32v16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int D>
+struct FaGeom {
+  static constexpr int KP = 2 * D + 16;           // pitch (bytes) of row-read images
+  static constexpr int TP = (D == 128) ? 320 : 192;  // pitch (bytes) of transposed-read images
+  static constexpr int NKK = D / 16;              // k-steps of a D-deep product
+  static constexpr int NDT = D / 32;              // 32-wide output tiles along D
+  static constexpr int V8 = D / 8;                // 16-byte vectors per row
+};
+
+__device__ __forceinline__ bfv8 lds_b128(const char* p) { return *reinterpret_cast<const bfv8*>(p); }
+
+__device__ __forceinline__ s16v4 lds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16v4*)(p));
+}
+
+// A operand (rows = 32 consecutive columns c0.. of an LDS image, k = image rows) for the
+// accumulator-as-B product: element j of lane half hh <-> image row
+//   rbase + 8*(j>>2) + 4*hh + (j&3)
+// and column c0 + (lane & 31). Two transposed reads, 4 rows each.
+__device__ __forceinline__ bfv8 lds_trA(const char* img, int pitch, int rbase, int c0, int lane) {
+  const int g = lane >> 4, i16 = lane & 15;
+  const int row = rbase + 4 * (g >> 1) + (i16 >> 2);
+  const int col = c0 + 16 * (g & 1) + 4 * (i16 & 3);
+  const char* p = img + row * pitch + col * 2;
+  const s16v4 lo = lds_tr(p);
+  const s16v4 hi = lds_tr(p + 8 * pitch);
+  const s16v8 x = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bfv8, x);
+}
+
+// registers 8s..8s+7 of an accumulator tile as a bf16 B operand (k-step s)
+__device__ __forceinline__ bfv8 acc_as_b(const f32v16& a, int s) {
+  f32v8 f;
+  if (s == 0)
+    f = __builtin_shufflevector(a, a, 0, 1, 2, 3, 4, 5, 6, 7);
+  else
+    f = __builtin_shufflevector(a, a, 8, 9, 10, 11, 12, 13, 14, 15);
+  return __builtin_convertvector(f, bfv8);
+}
+
+__device__ __forceinline__ bfv8 gload8(const bf16* p, bool ok) {
+  if (ok) return *reinterpret_cast<const bfv8*>(p);
+  bfv8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.f;
+  return z;
+}
+
+struct AttnArgs {
+  const bf16* q;
+  const bf16* k;
+  const bf16* v;
+  const bf16* o;
+  const bf16* dout;
+  bf16* out;  // forward: O;  backward: dq
+  float* lse;
+  const float* delta;
+  const int* seg;
+  bf16* dk;
+  bf16* dv;
+  float* dk_part;
+  float* dv_part;
+  int B, S, Hq, Hkv;
+  int64_t q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh;
+  int64_t d_sb, d_ss, d_sh;    // dout strides
+  int64_t dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
+  float scale;
+  int causal, window;
+};
+
+__device__ __forceinline__ bool visible(int qi, int kj, int S, int causal, int window, const int* seg, int sq) {
+  bool ok = kj < S && qi < S;
+  if (causal) ok = ok && (kj <= qi);
+  if (window >= 0) ok = ok && (kj >= qi - window);
+  if (seg) ok = ok && (seg[kj] == sq);
+  return ok;
+}
+
+// ============================================================================ forward
+// grid: (ceil(S/128), Hq, B), block 256 = 4 waves x 32 queries; KV tiles of 64 keys.
+template <int D>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
+  using G = FaGeom<D>;
+  constexpr int BN = 64;
+  constexpr int NV = BN * G::V8 / 256;  // staged 16-B vectors per thread per tensor
+  __shared__ __attribute__((aligned(16))) char smem[BN * G::KP + BN * G::TP];
+  char* Ks = smem;
+  char* Vs = smem + BN * G::KP;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int nqb = (a.S + 127) / 128;
+  const int mb = nqb - 1 - (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const bf16* qp = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16* kp = a.k + b * a.k_sb + hk * a.k_sh;
+  const bf16* vp = a.v + b * a.v_sb + hk * a.v_sh;
+  const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
+  const int sq = (seg && qrow < S) ? seg[qrow] : 0;
+  const float sl2 = a.scale * kLog2e;
+
+  bfv8 qf[G::NKK];
+#pragma unroll
+  for (int kk = 0; kk < G::NKK; ++kk) qf[kk] = gload8(qp + (int64_t)qrow * a.q_ss + kk * 16 + hh * 8, qrow < S);
+
+  f32v16 ot[G::NDT];
+#pragma unroll
+  for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = kv_beg / BN * BN;
+
+  bfv8 kst[NV], vst[NV];
+  auto load_tile = [&](int n0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, kr = n0 + row;
+      kst[i] = gload8(kp + (int64_t)kr * a.k_ss + c8 * 8, kr < S);
+      vst[i] = gload8(vp + (int64_t)kr * a.v_ss + c8 * 8, kr < S);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8;
+      *reinterpret_cast<bfv8*>(Ks + row * G::KP + c8 * 16) = kst[i];
+      *reinterpret_cast<bfv8*>(Vs + row * G::TP + c8 * 16) = vst[i];
+    }
+  };
+
+  if (kv_beg < kv_end) {
+    load_tile(kv_beg);
+    store_tile();
+  }
+  __syncthreads();
+  for (int n0 = kv_beg; n0 < kv_end; n0 += BN) {
+    const bool has_next = n0 + BN < kv_end;
+    if (has_next) load_tile(n0 + BN);
+
+    f32v16 st[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[t][i] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < G::NKK; ++kk)
+        st[t] = mfma32(lds_b128(Ks + (32 * t + r) * G::KP + (kk * 16 + hh * 8) * 2), qf[kk], st[t]);
+    }
+    const bool need_mask = seg || (n0 + BN > S) || (a.causal && n0 + BN - 1 > qw) ||
+                           (a.window >= 0 && n0 < qw + 31 - a.window) || qw + 31 >= S;
+    float smax = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float s = st[t][i] * sl2;
+        if (need_mask) {
+          const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (!visible(qrow, kj, S, a.causal, a.window, seg, sq)) s = -INFINITY;
+        }
+        st[t][i] = s;
+        smax = fmaxf(smax, s);
+      }
+    smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
+    const float mnew = fmaxf(m, smax);
+    const float muse = (mnew == -INFINITY) ? 0.f : mnew;
+    const float alpha = exp2f(m - muse);
+    m = mnew;
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = exp2f(st[t][i] - muse);
+        st[t][i] = p;
+        rs += p;
+      }
+    l = l * alpha + rs;
+#pragma unroll
+    for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bfv8 pb = acc_as_b(st[t], s2);
+#pragma unroll
+        for (int dt = 0; dt < G::NDT; ++dt)
+          ot[dt] = mfma32(lds_trA(Vs, G::TP, 32 * t + 16 * s2, dt * 32, lane), pb, ot[dt]);
+      }
+    __syncthreads();
+    if (has_next) store_tile();
+    __syncthreads();
+  }
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < S) {
+    bf16* op = a.out + b * a.o_sb + (int64_t)qrow * a.o_ss + h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint2 w;
+        w.x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
+        w.y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
+        *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
+      }
+    if (hh == 0) {
+      const float muse = (m == -INFINITY) ? 0.f : m;
+      a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (muse + __log2f(lt)) * kLn2 : -INFINITY;
+    }
+  }
+}
+
+// ============================================================================ backward: delta = rowsum(dO * O)
+// one thread per (b, s, h) row of D elements (16-byte loads).
+template <int D>
+__global__ __launch_bounds__(256) void fa_bwd_delta_kernel(AttnArgs a) {
+  const int64_t nrows = (int64_t)a.B * a.S * a.Hq;
+  for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < nrows; row += (int64_t)gridDim.x * 256) {
+    const int64_t h = row % a.Hq;
+    const int64_t bs = row / a.Hq;
+    const int64_t sidx = bs % a.S;
+    const int64_t b = bs / a.S;
+    const bf16x8* op = reinterpret_cast<const bf16x8*>(a.o + b * a.o_sb + sidx * a.o_ss + h * a.o_sh);
+    const bf16x8* dp = reinterpret_cast<const bf16x8*>(a.dout + b * a.d_sb + sidx * a.d_ss + h * a.d_sh);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D / 8; ++c) {
+      float x[8], y[8];
+      unpack8(op[c], x);
+      unpack8(dp[c], y);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += x[i] * y[i];
+    }
+    ((float*)a.delta)[(b * a.Hq + h) * a.S + sidx] = s;
+  }
+}
+
+// ============================================================================ backward: dQ (query-parallel)
+// grid: (ceil(S/128), Hq, B); 4 waves x 32 queries; KV tiles of 64 keys.
+template <int D>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
+  using G = FaGeom<D>;
+  constexpr int BN = 64;
+  constexpr int NV = BN * G::V8 / 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BN * G::KP + BN * G::TP];
+  char* Ks = smem;                    // K rows (b128 reads)
+  char* Vs = smem + BN * G::KP;       // V rows (b128 reads)
+  char* Kt = smem + 2 * BN * G::KP;   // K for transposed reads
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int nqb = (a.S + 127) / 128;
+  const int mb = nqb - 1 - (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const bf16* qp = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16* dop = a.dout + b * a.d_sb + h * a.d_sh;
+  const bf16* kp = a.k + b * a.k_sb + hk * a.k_sh;
+  const bf16* vp = a.v + b * a.v_sb + hk * a.v_sh;
+  const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
+  const int sq = (seg && qrow < S) ? seg[qrow] : 0;
+  const float sl2 = a.scale * kLog2e;
+  const int64_t lrow = ((int64_t)b * a.Hq + h) * S + qrow;
+  const float lse2 = qrow < S ? a.lse[lrow] * kLog2e : INFINITY;
+  const float dlt = qrow < S ? a.delta[lrow] : 0.f;
+
+  bfv8 qf[G::NKK], df[G::NKK];
+#pragma unroll
+  for (int kk = 0; kk < G::NKK; ++kk) {
+    qf[kk] = gload8(qp + (int64_t)qrow * a.q_ss + kk * 16 + hh * 8, qrow < S);
+    df[kk] = gload8(dop + (int64_t)qrow * a.d_ss + kk * 16 + hh * 8, qrow < S);
+  }
+  f32v16 dqt[G::NDT];
+#pragma unroll
+  for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dqt[dt][i] = 0.f;
+
+  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = kv_beg / BN * BN;
+
+  bfv8 kst[NV], vst[NV];
+  auto load_tile = [&](int n0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, kr = n0 + row;
+      kst[i] = gload8(kp + (int64_t)kr * a.k_ss + c8 * 8, kr < S);
+      vst[i] = gload8(vp + (int64_t)kr * a.v_ss + c8 * 8, kr < S);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8;
+      *reinterpret_cast<bfv8*>(Ks + row * G::KP + c8 * 16) = kst[i];
+      *reinterpret_cast<bfv8*>(Kt + row * G::TP + c8 * 16) = kst[i];
+      *reinterpret_cast<bfv8*>(Vs + row * G::KP + c8 * 16) = vst[i];
+    }
+  };
+  if (kv_beg < kv_end) {
+    load_tile(kv_beg);
+    store_tile();
+  }
+  __syncthreads();
+  for (int n0 = kv_beg; n0 < kv_end; n0 += BN) {
+    const bool has_next = n0 + BN < kv_end;
+    if (has_next) load_tile(n0 + BN);
+    const bool need_mask = seg || (n0 + BN > S) || (a.causal && n0 + BN - 1 > qw) ||
+                           (a.window >= 0 && n0 < qw + 31 - a.window) || qw + 31 >= S;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32v16 st, dpt;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        st[i] = 0.f;
+        dpt[i] = 0.f;
+      }
+#pragma unroll
+      for (int kk = 0; kk < G::NKK; ++kk) {
+        st = mfma32(lds_b128(Ks + (32 * t + r) * G::KP + (kk * 16 + hh * 8) * 2), qf[kk], st);
+        dpt = mfma32(lds_b128(Vs + (32 * t + r) * G::KP + (kk * 16 + hh * 8) * 2), df[kk], dpt);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = exp2f(st[i] * sl2 - lse2);
+        if (need_mask) {
+          const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (!visible(qrow, kj, S, a.causal, a.window, seg, sq)) p = 0.f;
+        }
+        st[i] = p * (dpt[i] - dlt);  // dS^T
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bfv8 db = acc_as_b(st, s2);
+#pragma unroll
+        for (int dt = 0; dt < G::NDT; ++dt)
+          dqt[dt] = mfma32(lds_trA(Kt, G::TP, 32 * t + 16 * s2, dt * 32, lane), db, dqt[dt]);
+      }
+    }
+    __syncthreads();
+    if (has_next) store_tile();
+    __syncthreads();
+  }
+  if (qrow < S) {
+    bf16* dqp = a.out + b * a.dq_sb + (int64_t)qrow * a.dq_ss + h * a.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint2 w;
+        w.x = pack_bf16x2(dqt[dt][4 * c] * a.scale, dqt[dt][4 * c + 1] * a.scale);
+        w.y = pack_bf16x2(dqt[dt][4 * c + 2] * a.scale, dqt[dt][4 * c + 3] * a.scale);
+        *reinterpret_cast<uint2*>(dqp + dt * 32 + 8 * c + 4 * hh) = w;
+      }
+  }
+}
+
+// ============================================================================ backward: dK, dV (key-parallel)
+// grid: (ceil(S/128), Hq, B); 4 waves x 32 keys; query tiles of 32 rows.
+// Hq == Hkv: writes bf16 dk/dv directly.  GQA: writes fp32 per-q-head partials, reduced afterwards.
+template <int D, bool GQA>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
+  using G = FaGeom<D>;
+  constexpr int BM = 32;
+  constexpr int NV = (BM * G::V8 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BM * G::KP + 2 * BM * G::TP + 2 * BM * 4];
+  char* Qs = smem;
+  char* Ds = smem + BM * G::KP;
+  char* Qt = smem + 2 * BM * G::KP;
+  char* Dt = Qt + BM * G::TP;
+  float* Ls = reinterpret_cast<float*>(Dt + BM * G::TP);
+  float* Dl = Ls + BM;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int nkb = (a.S + 127) / 128;
+  const int kb = (int)blockIdx.x;  // early key blocks see the most queries: launch them first
+  (void)nkb;
+  const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int ks = kb * 128, kw = ks + wid * 32, kr = kw + r;
+  const bf16* qp = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16* dop = a.dout + b * a.d_sb + h * a.d_sh;
+  const bf16* kp = a.k + b * a.k_sb + hk * a.k_sh;
+  const bf16* vp = a.v + b * a.v_sb + hk * a.v_sh;
+  const float* lsep = a.lse + ((int64_t)b * a.Hq + h) * S;
+  const float* dlp = a.delta + ((int64_t)b * a.Hq + h) * S;
+  const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
+  const int sk = (seg && kr < S) ? seg[kr] : 0;
+  const float sl2 = a.scale * kLog2e;
+
+  bfv8 kf[G::NKK], vf[G::NKK];
+#pragma unroll
+  for (int kk = 0; kk < G::NKK; ++kk) {
+    kf[kk] = gload8(kp + (int64_t)kr * a.k_ss + kk * 16 + hh * 8, kr < S);
+    vf[kk] = gload8(vp + (int64_t)kr * a.v_ss + kk * 16 + hh * 8, kr < S);
+  }
+  f32v16 dkt[G::NDT], dvt[G::NDT];
+#pragma unroll
+  for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      dkt[dt][i] = 0.f;
+      dvt[dt][i] = 0.f;
+    }
+
+  int q_beg = a.causal ? ks : 0;
+  q_beg = q_beg / BM * BM;
+  const int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+
+  bfv8 qst[NV], dst_[NV];
+  float lst = 0.f, dls = 0.f;
+  auto load_tile = [&](int q0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, qi = q0 + row;
+      const bool ok = (e < BM * G::V8) && qi < S;
+      qst[i] = gload8(qp + (int64_t)qi * a.q_ss + c8 * 8, ok);
+      dst_[i] = gload8(dop + (int64_t)qi * a.d_ss + c8 * 8, ok);
+    }
+    if (tid < BM) {
+      const int qi = q0 + tid;
+      lst = qi < S ? lsep[qi] * kLog2e : INFINITY;
+      dls = qi < S ? dlp[qi] : 0.f;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8;
+      if (e < BM * G::V8) {
+        *reinterpret_cast<bfv8*>(Qs + row * G::KP + c8 * 16) = qst[i];
+        *reinterpret_cast<bfv8*>(Qt + row * G::TP + c8 * 16) = qst[i];
+        *reinterpret_cast<bfv8*>(Ds + row * G::KP + c8 * 16) = dst_[i];
+        *reinterpret_cast<bfv8*>(Dt + row * G::TP + c8 * 16) = dst_[i];
+      }
+    }
+    if (tid < BM) {
+      Ls[tid] = lst;
+      Dl[tid] = dls;
+    }
+  };
+  if (q_beg < q_end) {
+    load_tile(q_beg);
+    store_tile();
+  }
+  __syncthreads();
+  for (int q0 = q_beg; q0 < q_end; q0 += BM) {
+    const bool has_next = q0 + BM < q_end;
+    if (has_next) load_tile(q0 + BM);
+    f32v16 sacc, dpacc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      sacc[i] = 0.f;
+      dpacc[i] = 0.f;
+    }
+#pragma unroll
+    for (int kk = 0; kk < G::NKK; ++kk) {
+      sacc = mfma32(lds_b128(Qs + r * G::KP + (kk * 16 + hh * 8) * 2), kf[kk], sacc);
+      dpacc = mfma32(lds_b128(Ds + r * G::KP + (kk * 16 + hh * 8) * 2), vf[kk], dpacc);
+    }
+    const bool need_mask = seg || (q0 + BM > S) || (kw + 31 >= S) || (a.causal && kw + 31 > q0) ||
+                           (a.window >= 0 && q0 + BM - 1 > kw + a.window);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qloc = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      float p = exp2f(sacc[i] * sl2 - Ls[qloc]);
+      if (need_mask) {
+        const int qi = q0 + qloc;
+        const int sqq = (seg && qi < S) ? seg[qi] : 0;
+        bool ok = kr < S && qi < S;
+        if (a.causal) ok = ok && (kr <= qi);
+        if (a.window >= 0) ok = ok && (kr >= qi - a.window);
+        if (seg) ok = ok && (sqq == sk);
+        if (!ok) p = 0.f;
+      }
+      sacc[i] = p;                           // P
+      dpacc[i] = p * (dpacc[i] - Dl[qloc]);  // dS
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bfv8 pb = acc_as_b(sacc, s2);
+      const bfv8 db = acc_as_b(dpacc, s2);
+#pragma unroll
+      for (int dt = 0; dt < G::NDT; ++dt) {
+        dvt[dt] = mfma32(lds_trA(Dt, G::TP, 16 * s2, dt * 32, lane), pb, dvt[dt]);
+        dkt[dt] = mfma32(lds_trA(Qt, G::TP, 16 * s2, dt * 32, lane), db, dkt[dt]);
+      }
+    }
+    __syncthreads();
+    if (has_next) store_tile();
+    __syncthreads();
+  }
+  if (kr < S) {
+    if constexpr (GQA) {
+      float* dkp = a.dk_part + (((int64_t)b * S + kr) * a.Hq + h) * D;
+      float* dvp = a.dv_part + (((int64_t)b * S + kr) * a.Hq + h) * D;
+#pragma unroll
+      for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int d = dt * 32 + 8 * c + 4 * hh;
+          *reinterpret_cast<float4*>(dkp + d) =
+              make_float4(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale, dkt[dt][4 * c + 2] * a.scale,
+                          dkt[dt][4 * c + 3] * a.scale);
+          *reinterpret_cast<float4*>(dvp + d) =
+              make_float4(dvt[dt][4 * c], dvt[dt][4 * c + 1], dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
+        }
+    } else {
+      bf16* dkp = a.dk + b * a.dk_sb + (int64_t)kr * a.dk_ss + hk * a.dk_sh;
+      bf16* dvp = a.dv + b * a.dv_sb + (int64_t)kr * a.dv_ss + hk * a.dv_sh;
+#pragma unroll
+      for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int d = dt * 32 + 8 * c + 4 * hh;
+          uint2 wk, wv;
+          wk.x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
+          wk.y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
+          wv.x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
+          wv.y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
+          *reinterpret_cast<uint2*>(dkp + d) = wk;
+          *reinterpret_cast<uint2*>(dvp + d) = wv;
+        }
+    }
+  }
+}
+
+// GQA: dk[b, s, hk, :] = sum over the group's q heads of dk_part[b, s, h, :]  (same for dv)
+template <int D>
+__global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
+  const int grp = a.Hq / a.Hkv;
+  const int64_t total = (int64_t)a.B * a.S * a.Hkv * (D / 4);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(e % (D / 4));
+    const int64_t t = e / (D / 4);
+    const int hk = (int)(t % a.Hkv);
+    const int64_t bs = t / a.Hkv;
+    const int s = (int)(bs % a.S);
+    const int64_t b = bs / a.S;
+    float4 sk = make_float4(0.f, 0.f, 0.f, 0.f), sv = sk;
+    for (int g = 0; g < grp; ++g) {
+      const int64_t off = ((bs)*a.Hq + hk * grp + g) * D + c4 * 4;
+      const float4 x = *reinterpret_cast<const float4*>(a.dk_part + off);
+      const float4 y = *reinterpret_cast<const float4*>(a.dv_part + off);
+      sk.x += x.x; sk.y += x.y; sk.z += x.z; sk.w += x.w;
+      sv.x += y.x; sv.y += y.y; sv.z += y.z; sv.w += y.w;
+    }
+    uint2 wk, wv;
+    wk.x = pack_bf16x2(sk.x, sk.y);
+    wk.y = pack_bf16x2(sk.z, sk.w);
+    wv.x = pack_bf16x2(sv.x, sv.y);
+    wv.y = pack_bf16x2(sv.z, sv.w);
+    *reinterpret_cast<uint2*>(a.dk + b * a.dk_sb + (int64_t)s * a.dk_ss + hk * a.dk_sh + c4 * 4) = wk;
+    *reinterpret_cast<uint2*>(a.dv + b * a.dv_sb + (int64_t)s * a.dv_ss + hk * a.dv_sh + c4 * 4) = wv;
+  }
+}
+
+}  // namespace llmt
+
+using namespace llmt;
+
+static bool aligned16(const void* p, int64_t s0, int64_t s1, int64_t s2) {
+  return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (s0 % 8 == 0) && (s1 % 8 == 0) && (s2 % 8 == 0);
+}
+
+extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
+                                          const int* seg, int B, int S, int Hq, int Hkv, int D, int64_t q_sb,
+                                          int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh,
+                                          int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
+                                          int64_t o_sh, float scale, int causal, int window, hipStream_t stream) {
+  if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
+  if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
+      !aligned16(o, o_sb, o_ss, o_sh))
+    return hipErrorInvalidValue;
+  if (B == 0 || S == 0) return hipSuccess;
+  AttnArgs a{};
+  a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.out = (bf16*)o; a.lse = lse; a.seg = seg;
+  a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv;
+  a.q_sb = q_sb; a.q_ss = q_ss; a.q_sh = q_sh; a.k_sb = k_sb; a.k_ss = k_ss; a.k_sh = k_sh;
+  a.v_sb = v_sb; a.v_ss = v_ss; a.v_sh = v_sh; a.o_sb = o_sb; a.o_ss = o_ss; a.o_sh = o_sh;
+  a.scale = scale; a.causal = causal; a.window = window;
+  dim3 grid((S + 127) / 128, Hq, B);
+  switch (D) {
+    case 64: fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a); break;
+    case 96: fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a); break;
+    case 128: fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
+                                          const void* dout, const float* lse, float* delta, const int* seg, void* dq,
+                                          void* dk, void* dv, float* work, int B, int S, int Hq, int Hkv, int D,
+                                          int64_t q_sb, int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss,
+                                          int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb,
+                                          int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss, int64_t dq_sh,
+                                          int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb, int64_t dv_ss,
+                                          int64_t dv_sh, float scale, int causal, int window, hipStream_t stream) {
+  if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
+  if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
+      !aligned16(o, o_sb, o_ss, o_sh) || !aligned16(dout, o_sb, o_ss, o_sh) || !aligned16(dq, dq_sb, dq_ss, dq_sh) ||
+      !aligned16(dk, dk_sb, dk_ss, dk_sh) || !aligned16(dv, dv_sb, dv_ss, dv_sh))
+    return hipErrorInvalidValue;
+  if (B == 0 || S == 0) return hipSuccess;
+  AttnArgs a{};
+  a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (const bf16*)o;
+  a.dout = (const bf16*)dout; a.out = (bf16*)dq; a.lse = (float*)lse; a.delta = delta; a.seg = seg;
+  a.dk = (bf16*)dk; a.dv = (bf16*)dv;
+  const int64_t part = (int64_t)B * S * Hq * D;
+  a.dk_part = work; a.dv_part = work ? work + part : nullptr;
+  a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv;
+  a.q_sb = q_sb; a.q_ss = q_ss; a.q_sh = q_sh; a.k_sb = k_sb; a.k_ss = k_ss; a.k_sh = k_sh;
+  a.v_sb = v_sb; a.v_ss = v_ss; a.v_sh = v_sh; a.o_sb = o_sb; a.o_ss = o_ss; a.o_sh = o_sh;
+  a.d_sb = o_sb; a.d_ss = o_ss; a.d_sh = o_sh;  // dout shares O's layout (checked by the caller)
+  a.dq_sb = dq_sb; a.dq_ss = dq_ss; a.dq_sh = dq_sh; a.dk_sb = dk_sb; a.dk_ss = dk_ss; a.dk_sh = dk_sh;
+  a.dv_sb = dv_sb; a.dv_ss = dv_ss; a.dv_sh = dv_sh;
+  a.scale = scale; a.causal = causal; a.window = window;
+  const bool gqa = Hq != Hkv;
+  if (gqa && !work) return hipErrorInvalidValue;
+  const int64_t nrows = (int64_t)B * S * Hq;
+  dim3 grid((S + 127) / 128, Hq, B);
+  const int dgrid = stream_grid(nrows, 256);
+#define LLMT_BWD(DD)                                                                              \
+  fa_bwd_delta_kernel<DD><<<dgrid, 256, 0, stream>>>(a);                                          \
+  fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                              \
+  if (gqa) {                                                                                      \
+    fa_bwd_dkdv_kernel<DD, true><<<grid, 256, 0, stream>>>(a);                                    \
+    fa_gqa_reduce_kernel<DD><<<stream_grid((int64_t)B * S * Hkv * (DD / 4), 256), 256, 0, stream>>>(a); \
+  } else {                                                                                        \
+    fa_bwd_dkdv_kernel<DD, false><<<grid, 256, 0, stream>>>(a);                                   \
+  }
+  switch (D) {
+    case 64: { LLMT_BWD(64) } break;
+    case 96: { LLMT_BWD(96) } break;
+    case 128: { LLMT_BWD(128) } break;
+    default: return hipErrorInvalidValue;
+  }
+#undef LLMT_BWD
+  return hipGetLastError();
+}

@@ -1,0 +1,113 @@
+// Fused AdamW step and gradient-norm reduction on flat (sharded) buffers, gfx950.
+//
+// Replaces DeepSpeed FusedAdam (reference configs
+// config/examples/llama-3.1/llama-3.1-8b_pt_example.yaml:44) together with the 3-pass Python master-
+// weight wrapper (reference src/llm_training/optim/master_weight_wrapper.py:63-80: grad.float() copy ->
+// inner step -> copy back). One pass per element: read bf16 (or fp32) grad, fp32 master, m, v; write
+// master, m, v and the bf16 model parameter. The gradient-clipping coefficient is read from device
+// memory, so clipping never synchronises with the host.
+#include "common.h"
+
+namespace llmt {
+
+template <typename GradT>
+__device__ __forceinline__ void load4(const GradT* g, int64_t i, float* out);
+template <>
+__device__ __forceinline__ void load4<float>(const float* g, int64_t i, float* out) {
+  *reinterpret_cast<float4*>(out) = reinterpret_cast<const float4*>(g)[i];
+}
+template <>
+__device__ __forceinline__ void load4<bf16>(const bf16* g, int64_t i, float* out) {
+  const uint2 w = reinterpret_cast<const uint2*>(g)[i];
+  out[0] = bf16_lo(w.x);
+  out[1] = bf16_hi(w.x);
+  out[2] = bf16_lo(w.y);
+  out[3] = bf16_hi(w.y);
+}
+
+template <typename GradT>
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                    float* __restrict__ v, const GradT* __restrict__ g,
+                                                    bf16* __restrict__ pout, int64_t n4, float lr, float b1,
+                                                    float b2, float eps, float wd, float step_size,
+                                                    float inv_sqrt_bc2, const float* __restrict__ gscale) {
+  const float sc = gscale ? gscale[0] : 1.f;
+  const float decay = 1.f - lr * wd;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float gg[4];
+    load4<GradT>(g, i, gg);
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pf = reinterpret_cast<float*>(&pp);
+    float* mf = reinterpret_cast<float*>(&mm);
+    float* vf = reinterpret_cast<float*>(&vv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = gg[k] * sc;
+      mf[k] = b1 * mf[k] + (1.f - b1) * gk;
+      vf[k] = b2 * vf[k] + (1.f - b2) * gk * gk;
+      const float denom = sqrtf(vf[k]) * inv_sqrt_bc2 + eps;
+      pf[k] = pf[k] * decay - step_size * mf[k] / denom;
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (pout) {
+      uint2 o;
+      o.x = pack_bf16x2(pf[0], pf[1]);
+      o.y = pack_bf16x2(pf[2], pf[3]);
+      reinterpret_cast<uint2*>(pout)[i] = o;
+    }
+  }
+}
+
+// out[0] += sum(x^2) over n elements (n % 4 == 0); one atomic per block.
+template <typename T>
+__global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, int64_t n4, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float f[4];
+    load4<T>(x, i, f);
+    s += f[0] * f[0] + f[1] * f[1] + f[2] * f[2] + f[3] * f[3];
+  }
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+}  // namespace llmt
+
+using namespace llmt;
+
+extern "C" hipError_t llmt_adamw(float* p, float* m, float* v, const void* g, int grad_is_fp32, void* pout,
+                                 int64_t n, float lr, float b1, float b2, float eps, float wd, int64_t step,
+                                 const float* gscale, hipStream_t stream) {
+  if (n % 4) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return hipSuccess;
+  const double bc1 = 1.0 - pow((double)b1, (double)step);
+  const double bc2 = 1.0 - pow((double)b2, (double)step);
+  const float step_size = (float)(lr / bc1);
+  const float inv_sqrt_bc2 = (float)(1.0 / sqrt(bc2));
+  const int grid = stream_grid(n4, 256);
+  if (grad_is_fp32)
+    adamw_kernel<float><<<grid, 256, 0, stream>>>(p, m, v, (const float*)g, (bf16*)pout, n4, lr, b1, b2, eps, wd,
+                                                  step_size, inv_sqrt_bc2, gscale);
+  else
+    adamw_kernel<bf16><<<grid, 256, 0, stream>>>(p, m, v, (const bf16*)g, (bf16*)pout, n4, lr, b1, b2, eps, wd,
+                                                 step_size, inv_sqrt_bc2, gscale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t llmt_sumsq(const void* x, int is_fp32, int64_t n, float* out, hipStream_t stream) {
+  if (n % 4) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  if (n4 == 0) return hipSuccess;
+  const int grid = stream_grid(n4, 256) > 1024 ? 1024 : stream_grid(n4, 256);
+  if (is_fp32)
+    sumsq_kernel<float><<<grid, 256, 0, stream>>>((const float*)x, n4, out);
+  else
+    sumsq_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x, n4, out);
+  return hipGetLastError();
+}

@@ -1,0 +1,237 @@
+// RMSNorm forward/backward (+ fused residual add) for gfx950.
+//
+// Replaces the reference's Liger/Triton RMSNorm (reference call sites
+// src/llm_training/ops/liger_kernel/rms_norm_op.py:15-19, models/llama/llama_model.py:271-286).
+// Semantics follow src/llm_training/ops/rms_norm_op.py:4-14 ("llama" casting): the normalised
+// row is rounded to the input dtype before the weight multiply.
+//
+// Layout: one wave64 per row (4 rows per 256-thread block). A lane owns NC 16-byte chunks of the
+// row (8 bf16 each, columns (c*64+lane)*8), so the whole row lives in registers between the
+// reduction and the write — one HBM read and one write per element, no LDS round trip.
+// Backward dW: each block accumulates its rows' dy*n in registers, reduces its 4 waves through LDS
+// and writes one fp32 partial row; a second kernel reduces the partials column-wise and writes (or
+// accumulates into) the bf16/fp32 weight gradient.
+#include "common.h"
+
+namespace llmt {
+
+template <int NC, bool RES>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
+    const bf16x8* __restrict__ x, const bf16x8* __restrict__ res, const bf16x8* __restrict__ w,
+    bf16x8* __restrict__ y, bf16x8* __restrict__ res_out, float* __restrict__ rstd_out,
+    int T, int H8, float inv_h, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const int64_t base = (int64_t)row * H8;
+  float v[NC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = c * 64 + lane;
+    if (col < H8) {
+      unpack8(x[base + col], v[c]);
+      if constexpr (RES) {
+        float r[8];
+        unpack8(res[base + col], r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] += r[i];
+        // the residual stream is kept in bf16: round the sum before normalising (matches torch x + r)
+        bf16x8 s = pack8(v[c]);
+        res_out[base + col] = s;
+        unpack8(s, v[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss * inv_h + eps);
+  if (lane == 0 && rstd_out) rstd_out[row] = r;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = c * 64 + lane;
+    if (col < H8) {
+      float wf[8], o[8];
+      unpack8(w[col], wf);
+      float nf[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) nf[i] = v[c][i] * r;
+      unpack8(pack8(nf), nf);  // round the normalised row to bf16 ("llama" casting)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = nf[i] * wf[i];
+      y[base + col] = pack8(o);
+    }
+  }
+}
+
+// dx = rstd * (dn - xhat * mean(dn * xhat)),  dn = dy * w,  xhat = x * rstd.
+// Optional `dres` (gradient flowing along the residual stream) is added to dx.
+// Per-block partial dW (sum over the block's rows of dy * bf16(xhat)) goes to dw_part[blockIdx].
+template <int NC, bool DRES>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
+    const bf16x8* __restrict__ dy, const bf16x8* __restrict__ x, const bf16x8* __restrict__ w,
+    const float* __restrict__ rstd, const bf16x8* __restrict__ dres, bf16x8* __restrict__ dx,
+    float* __restrict__ dw_part, int T, int H8, float inv_h, int rows_per_block) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float dwacc[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dwacc[c][i] = 0.f;
+  const int row0 = blockIdx.x * rows_per_block;
+  const int row1 = min(T, row0 + rows_per_block);
+  for (int row = row0 + wid; row < row1; row += 4) {
+    const int64_t base = (int64_t)row * H8;
+    const float r = rstd[row];
+    bf16x8 xv[NC], gv[NC];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * 64 + lane;
+      if (col < H8) {
+        xv[c] = x[base + col];
+        gv[c] = dy[base + col];
+        float xf[8], g[8], wf[8], nf[8];
+        unpack8(xv[c], xf);
+        unpack8(gv[c], g);
+        unpack8(w[col], wf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          nf[i] = xf[i] * r;
+          dot += g[i] * wf[i] * nf[i];
+        }
+        unpack8(pack8(nf), nf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dwacc[c][i] += g[i] * nf[i];
+      }
+    }
+    dot = wave_sum(dot) * inv_h;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * 64 + lane;
+      if (col < H8) {
+        float xf[8], g[8], wf[8], o[8];
+        unpack8(xv[c], xf);
+        unpack8(gv[c], g);
+        unpack8(w[col], wf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = r * (g[i] * wf[i] - xf[i] * r * dot);
+        if constexpr (DRES) {
+          float d2[8];
+          unpack8(dres[base + col], d2);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += d2[i];
+        }
+        dx[base + col] = pack8(o);
+      }
+    }
+  }
+  // reduce the 4 waves' dW partials through LDS, one 512-column chunk at a time
+  const int H = H8 * 8;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = c * 64 + lane;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[wid][lane * 8 + i] = (col < H8) ? dwacc[c][i] : 0.f;
+    __syncthreads();
+    for (int j = threadIdx.x; j < 512; j += 256) {
+      const int gcol = c * 512 + j;
+      if (gcol < H) dw_part[(int64_t)blockIdx.x * H + gcol] = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+    }
+  }
+}
+
+// Column reduction of the per-block dW partials: out[j] (+)= sum_b part[b][j].
+template <typename OutT>
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, OutT* __restrict__ out,
+                                                     int nparts, int H, int accumulate) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= H) return;
+  float s = 0.f;
+  for (int b = 0; b < nparts; ++b) s += part[(int64_t)b * H + j];
+  if (accumulate) s += (float)out[j];
+  out[j] = (OutT)s;
+}
+
+}  // namespace llmt
+
+using namespace llmt;
+
+#define FWD_CASE(NC)                                                                                   \
+  case NC:                                                                                             \
+    if (res)                                                                                           \
+      rmsnorm_fwd_kernel<NC, true><<<grid, 256, 0, stream>>>((const bf16x8*)x, (const bf16x8*)res,     \
+                                                            (const bf16x8*)w, (bf16x8*)y,              \
+                                                            (bf16x8*)res_out, rstd, T, H8, inv_h, eps); \
+    else                                                                                               \
+      rmsnorm_fwd_kernel<NC, false><<<grid, 256, 0, stream>>>((const bf16x8*)x, nullptr,               \
+                                                             (const bf16x8*)w, (bf16x8*)y, nullptr,    \
+                                                             rstd, T, H8, inv_h, eps);                 \
+    break;
+
+extern "C" hipError_t llmt_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* res_out,
+                                       float* rstd, int T, int H, float eps, hipStream_t stream) {
+  if (H % 8 != 0 || H > 8192) return hipErrorInvalidValue;
+  const int H8 = H / 8;
+  const int nc = (H8 + 63) / 64;
+  const int grid = (T + 3) / 4;
+  const float inv_h = 1.f / H;
+  if (T == 0) return hipSuccess;
+  switch (nc <= 8 ? nc : (nc + 1) / 2 * 2) {
+    FWD_CASE(1) FWD_CASE(2) FWD_CASE(3) FWD_CASE(4) FWD_CASE(5) FWD_CASE(6) FWD_CASE(7) FWD_CASE(8)
+    FWD_CASE(10) FWD_CASE(12) FWD_CASE(14) FWD_CASE(16)
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+#define BWD_CASE(NC)                                                                                   \
+  case NC:                                                                                             \
+    if (dres)                                                                                          \
+      rmsnorm_bwd_kernel<NC, true><<<nblk, 256, 0, stream>>>(                                          \
+          (const bf16x8*)dy, (const bf16x8*)x, (const bf16x8*)w, rstd, (const bf16x8*)dres,            \
+          (bf16x8*)dx, dw_part, T, H8, inv_h, rpb);                                                    \
+    else                                                                                               \
+      rmsnorm_bwd_kernel<NC, false><<<nblk, 256, 0, stream>>>(                                         \
+          (const bf16x8*)dy, (const bf16x8*)x, (const bf16x8*)w, rstd, nullptr, (bf16x8*)dx, dw_part,  \
+          T, H8, inv_h, rpb);                                                                          \
+    break;
+
+// dw_part must hold nblocks*H floats where nblocks = llmt_rmsnorm_bwd_nblocks(T).
+extern "C" int llmt_rmsnorm_bwd_nblocks(int T) {
+  int nblk = (T + 15) / 16;  // >= 16 rows per block so partial traffic stays << activation traffic
+  if (nblk > 1024) nblk = 1024;
+  if (nblk < 1) nblk = 1;
+  return nblk;
+}
+
+extern "C" hipError_t llmt_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
+                                       const void* dres, void* dx, float* dw_part, void* dw, int dw_is_fp32,
+                                       int accumulate, int T, int H, hipStream_t stream) {
+  if (H % 8 != 0 || H > 8192) return hipErrorInvalidValue;
+  const int H8 = H / 8;
+  const int nc = (H8 + 63) / 64;
+  const int nblk = llmt_rmsnorm_bwd_nblocks(T);
+  const int rpb = (T + nblk - 1) / nblk;
+  const float inv_h = 1.f / H;
+  if (T > 0) {
+    switch (nc <= 8 ? nc : (nc + 1) / 2 * 2) {
+      BWD_CASE(1) BWD_CASE(2) BWD_CASE(3) BWD_CASE(4) BWD_CASE(5) BWD_CASE(6) BWD_CASE(7) BWD_CASE(8)
+      BWD_CASE(10) BWD_CASE(12) BWD_CASE(14) BWD_CASE(16)
+      default:
+        return hipErrorInvalidValue;
+    }
+  }
+  if (dw) {
+    const int g = (H + 255) / 256;
+    if (dw_is_fp32)
+      colsum_kernel<float><<<g, 256, 0, stream>>>(dw_part, (float*)dw, T > 0 ? nblk : 0, H, accumulate);
+    else
+      colsum_kernel<bf16><<<g, 256, 0, stream>>>(dw_part, (bf16*)dw, T > 0 ? nblk : 0, H, accumulate);
+  }
+  return hipGetLastError();
+}

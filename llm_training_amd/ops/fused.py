@@ -1,0 +1,470 @@
+"""Autograd front-ends of the fused hot ops.
+
+GPU tensors run the hand-written gfx950 kernels of ``csrc/`` (loaded by :mod:`.native`); CPU tensors
+run :mod:`.reference`. Weight gradients support *gradient-buffer views*: when a parameter carries a
+``main_grad`` tensor (a view into the flat per-unit gradient buffer owned by
+:class:`llm_training_amd.parallel.grad_buffer.GradBuffer`), the backward writes (first micro-batch)
+or accumulates (later micro-batches) the weight gradient straight into it and returns ``None`` to
+autograd — the same trick as fusing gradient accumulation into the weight-gradient GEMM, so there
+is no separate ``param.grad`` tensor, no ``grad += new`` pass and the ZeRO engine can reduce-scatter
+the flat buffer as soon as a unit's backward is done.
+
+Reference parity: these replace the Liger wrappers of src/llm_training/ops/liger_kernel/*.py and
+flash-attn calls of src/llm_training/ops/attention_op.py.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch.autograd import Function
+
+from . import reference as ref
+from .native import lib, use_native
+
+# ----------------------------------------------------------------------------- gradient-buffer helpers
+
+
+def _wgrad_mm(w: torch.Tensor, a_t: torch.Tensor, b: torch.Tensor):
+    """dW = a_t @ b. Writes into ``w.main_grad`` if present (returns None), else returns dW."""
+    mg = getattr(w, "main_grad", None)
+    if mg is None:
+        return (a_t @ b).to(w.dtype)
+    mg2 = mg.view(a_t.shape[0], b.shape[1])
+    if mg.dtype == a_t.dtype:
+        if getattr(w, "grad_added", False):
+            mg2.addmm_(a_t, b)
+        else:
+            torch.mm(a_t, b, out=mg2)
+    else:  # fp32 gradient buffer with bf16 operands
+        part = torch.mm(a_t, b, out_dtype=mg.dtype) if a_t.is_cuda else (a_t.float() @ b.float())
+        if getattr(w, "grad_added", False):
+            mg2.add_(part)
+        else:
+            mg2.copy_(part)
+    w.grad_added = True
+    return None
+
+
+def _wgrad_vec(w: torch.Tensor, g: torch.Tensor):
+    mg = getattr(w, "main_grad", None)
+    if mg is None:
+        return g.to(w.dtype)
+    if getattr(w, "grad_added", False):
+        mg.add_(g.view_as(mg))
+    else:
+        mg.copy_(g.view_as(mg))
+    w.grad_added = True
+    return None
+
+
+# ----------------------------------------------------------------------------- linear
+
+
+class _LinearFn(Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        y = torch.matmul(x, w.t())
+        if b is not None:
+            y = y + b
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(dy, w)
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad_mm(w, dy2.t(), x.reshape(-1, x.shape[-1]))
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    return _LinearFn.apply(x, w, b)
+
+
+# ----------------------------------------------------------------------------- RMSNorm
+
+
+class _RMSNormFn(Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        L = lib()
+        x = x.contiguous()
+        y, _, rstd = L.rmsnorm_fwd(x, None, w, eps)
+        ctx.save_for_backward(x, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        L = lib()
+        need_w = ctx.needs_input_grad[1]
+        mg = getattr(w, "main_grad", None) if need_w else None
+        dx, dw = L.rmsnorm_bwd(dy.contiguous(), x, w, rstd, None, mg, bool(getattr(w, "grad_added", False)),
+                               need_w)
+        if need_w:
+            if mg is not None:
+                w.grad_added = True
+                dw = None
+            else:
+                dw = dw.to(w.dtype)
+        else:
+            dw = None
+        return dx, dw, None
+
+
+class _AddRMSNormFn(Function):
+    """s = x + residual; y = rmsnorm(s) * w  ->  (y, s). One kernel each way."""
+
+    @staticmethod
+    def forward(ctx, x, res, w, eps):
+        L = lib()
+        y, s, rstd = L.rmsnorm_fwd(x.contiguous(), res.contiguous(), w, eps)
+        ctx.save_for_backward(s, w, rstd)
+        return y, s
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        s, w, rstd = ctx.saved_tensors
+        L = lib()
+        need_w = ctx.needs_input_grad[2]
+        mg = getattr(w, "main_grad", None) if need_w else None
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dres = ds.contiguous() if ds is not None else None
+        dx, dw = L.rmsnorm_bwd(dy.contiguous(), s, w, rstd, dres, mg, bool(getattr(w, "grad_added", False)), need_w)
+        if need_w:
+            if mg is not None:
+                w.grad_added = True
+                dw = None
+            else:
+                dw = dw.to(w.dtype)
+        else:
+            dw = None
+        return dx, dx, dw, None
+
+
+class _RefRMSNormFn(Function):
+    """CPU path with main_grad support (plain torch math)."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        ctx.save_for_backward(x, w)
+        ctx.eps = eps
+        return ref.rms_norm(x, w, eps)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        with torch.enable_grad():
+            xd = x.detach().requires_grad_(True)
+            wd = w.detach().requires_grad_(True)
+            y = ref.rms_norm(xd, wd, ctx.eps)
+            dx, dw = torch.autograd.grad(y, (xd, wd), dy)
+        return dx, (_wgrad_vec(w, dw) if ctx.needs_input_grad[1] else None), None
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None):
+    """RMSNorm; with ``residual`` returns ``(rmsnorm(x + residual), x + residual)``."""
+    if use_native(x):
+        if residual is None:
+            return _RMSNormFn.apply(x, w, eps)
+        return _AddRMSNormFn.apply(x, residual, w, eps)
+    if residual is None:
+        return _RefRMSNormFn.apply(x, w, eps)
+    s = x + residual
+    return _RefRMSNormFn.apply(s, w, eps), s
+
+
+# ----------------------------------------------------------------------------- SwiGLU
+
+
+class _SwiGLUFn(Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return lib().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dc):
+        (gu,) = ctx.saved_tensors
+        return lib().swiglu_bwd(gu, dc.contiguous())
+
+
+def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
+    """silu(gate) * up for a fused [..., 2I] buffer laid out [gate | up]."""
+    if use_native(gate_up):
+        return _SwiGLUFn.apply(gate_up)
+    return ref.swiglu_fused(gate_up)
+
+
+# ----------------------------------------------------------------------------- RoPE + flash attention
+
+
+class _RopeFlashAttnFn(Function):
+    """qkv [B, S, Hq+2Hkv, D] (fused QKV GEMM output) -> attention output [B, S, Hq, D].
+
+    RoPE is applied IN PLACE to the q and k heads of ``qkv`` (the buffer has no other consumer: the
+    QKV GEMM's backward needs its input, not its output), then the flash kernels read q/k/v as strided
+    views of the same buffer. The backward writes dq/dk/dv into one fused dQKV buffer and un-rotates
+    it in place, producing exactly the gradient of the QKV GEMM output.
+    """
+
+    # Activations are sequence-major: qkv is [S, B, Htot, D] contiguous, positions [S, B]. The flash
+    # kernels see [B, S, H, D] strided views (transpose(0, 1)) and return O in the same seq-major memory
+    # order, so the output projection consumes it without a copy.
+    @staticmethod
+    def forward(ctx, qkv, pos, cos, sin, seg, nq, nkv, causal, window, scale):
+        L = lib()
+        L.rope_(qkv, pos, cos, sin, nq + nkv, False)
+        x = qkv.transpose(0, 1)
+        q, k, v = x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:]
+        o, lse = L.flash_attn_fwd(q, k, v, seg, scale, causal, window)
+        ctx.save_for_backward(qkv, o, lse, pos, cos, sin, seg)
+        ctx.cfg = (nq, nkv, causal, window, scale)
+        return o.transpose(0, 1)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, pos, cos, sin, seg = ctx.saved_tensors
+        nq, nkv, causal, window, scale = ctx.cfg
+        L = lib()
+        do = do.transpose(0, 1)
+        if do.stride() != o.stride():
+            do = torch.empty_like(o).copy_(do)
+        dqkv = torch.empty_like(qkv)
+        x, dx = qkv.transpose(0, 1), dqkv.transpose(0, 1)
+        L.flash_attn_bwd(x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:], o, do, lse, seg, dx[:, :, :nq],
+                         dx[:, :, nq:nq + nkv], dx[:, :, nq + nkv:], scale, causal, window)
+        L.rope_(dqkv, pos, cos, sin, nq + nkv, True)
+        return dqkv, None, None, None, None, None, None, None, None, None
+
+
+class _FlashAttnFn(Function):
+    """Plain flash attention on separate q/k/v [B, S, H, D] tensors."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, seg, causal, window, scale):
+        o, lse = lib().flash_attn_fwd(q, k, v, seg, scale, causal, window)
+        ctx.save_for_backward(q, k, v, o, lse, seg)
+        ctx.cfg = (causal, window, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, seg = ctx.saved_tensors
+        causal, window, scale = ctx.cfg
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        lib().flash_attn_bwd(q, k, v, o, do.contiguous(), lse, seg, dq, dk, dv, scale, causal, window)
+        return dq, dk, dv, None, None, None, None
+
+
+def flash_attention(q, k, v, causal: bool = True, segment_ids=None, window: int = -1, scale: float | None = None):
+    """q: [B, S, Hq, D]; k/v: [B, S, Hkv, D]; segment_ids: optional int [B, S] (equal ids attend)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if use_native(q):
+        seg = segment_ids.to(torch.int32).contiguous() if segment_ids is not None else None
+        return _FlashAttnFn.apply(q, k, v, seg, causal, -1 if window is None else int(window), scale)
+    return ref.attention(q, k, v, causal, segment_ids, -1 if window is None else window, scale)
+
+
+def rope_tables_to_full(cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor):
+    """Half-width fp32 tables [P, D/2] gathered at positions -> full-width HF-style [.., D] cos/sin."""
+    c = cos[pos]
+    s = sin[pos]
+    return torch.cat([c, c], -1), torch.cat([s, s], -1)
+
+
+def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool = True, segment_ids=None,
+                   window: int = -1, scale: float | None = None, impl: str = "flash"):
+    """Fused RoPE + attention on the SEQ-MAJOR fused QKV buffer [S, B, n_q + 2 n_kv, D] -> [S, B, n_q, D].
+
+    ``cos``/``sin``: fp32 half-width tables [max_pos, D/2]; ``positions``: [B, S] int;
+    ``segment_ids``: optional [B, S] (tokens attend only within equal ids).
+    """
+    D = qkv.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    win = -1 if window is None else int(window)
+    if use_native(qkv) and impl in ("flash", "flash_attention_2", "hip"):
+        qkv = qkv.contiguous()
+        pos = positions.t().contiguous().reshape(-1)
+        seg = segment_ids.to(torch.int32).contiguous() if segment_ids is not None else None
+        return _RopeFlashAttnFn.apply(qkv, pos, cos, sin, seg, n_q, n_kv, causal, win, scale)
+    return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale,
+                               impl).transpose(0, 1)
+
+
+def _ref_rope_attention(qkv, positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale, impl):
+    q, k, v = qkv[:, :, :n_q], qkv[:, :, n_q:n_q + n_kv], qkv[:, :, n_q + n_kv:]
+    cf, sf = rope_tables_to_full(cos, sin, positions)
+    q, k = ref.apply_rope(q, k, cf.to(q.dtype) if q.dtype != torch.float32 else cf,
+                          sf.to(q.dtype) if q.dtype != torch.float32 else sf)
+    if impl == "sdpa" and segment_ids is None and win < 0:
+        rep = n_q // n_kv
+        qh, kh, vh = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        if rep > 1:
+            kh = kh.repeat_interleave(rep, dim=1)
+            vh = vh.repeat_interleave(rep, dim=1)
+        o = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh, is_causal=causal, scale=scale)
+        return o.transpose(1, 2)
+    if impl == "sdpa":
+        mask = ref.visibility_mask(q.shape[1], q.device, causal, segment_ids, win, q.shape[0])
+        rep = n_q // n_kv
+        qh, kh, vh = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        if rep > 1:
+            kh = kh.repeat_interleave(rep, dim=1)
+            vh = vh.repeat_interleave(rep, dim=1)
+        o = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask[:, None], scale=scale)
+        return o.transpose(1, 2)
+    return ref.attention(q, k, v, causal, segment_ids, win, scale)
+
+
+# ----------------------------------------------------------------------------- cross entropy
+
+
+class _FusedLinearCEFn(Function):
+    """loss = mean_{valid rows} CE(h @ W^T, labels), logits produced chunk by chunk.
+
+    Forward: per row chunk, one hipBLASLt GEMM for the bf16 logits, then the HIP CE kernel computes
+    the loss AND overwrites the logits with d loss / d logits (scaled by 1/n_valid read from device
+    memory — no host sync). Backward: dh = g * dlogits @ W and dW (+)= dlogits^T @ (g * h), written
+    straight into W's gradient buffer.
+    """
+
+    @staticmethod
+    def forward(ctx, h, w, labels, ignore_index, chunk):
+        L = lib()
+        N = h.shape[0]
+        valid = (labels != ignore_index).sum()
+        inv_n = (1.0 / valid.clamp(min=1).float()).reshape(1)
+        loss_rows = torch.empty(N, device=h.device, dtype=torch.float32)
+        grads = []
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = torch.matmul(h[s0:s1], w.t())
+            _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, inv_n, True)
+            loss_rows[s0:s1] = lr
+            grads.append(lg)
+        ctx.save_for_backward(h, w, *grads)
+        ctx.chunk = chunk
+        return loss_rows.sum() * inv_n[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w, *grads = ctx.saved_tensors
+        chunk = ctx.chunk
+        dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
+        hs = h * g.to(h.dtype)
+        dw_acc = None
+        for i, lg in enumerate(grads):
+            s0 = i * chunk
+            s1 = s0 + lg.shape[0]
+            if dh is not None:
+                torch.matmul(lg, w, out=dh[s0:s1])
+            if ctx.needs_input_grad[1]:
+                r = _wgrad_mm(w, lg.t(), hs[s0:s1])
+                if r is not None:
+                    dw_acc = r if dw_acc is None else dw_acc + r
+        if dh is not None:
+            dh.mul_(g.to(dh.dtype))
+        return dh, dw_acc, None, None, None
+
+
+def fused_linear_cross_entropy(h, w, labels, ignore_index: int = -100, chunk_size: int = 8192):
+    """Mean token CE of ``h @ w.T`` against ``labels`` (already shifted). h: [N, H], labels: [N]."""
+    h = h.reshape(-1, h.shape[-1])
+    labels = labels.reshape(-1)
+    if use_native(h):
+        return _FusedLinearCEFn.apply(h.contiguous(), w, labels.contiguous(), ignore_index, chunk_size)
+    logits = linear(h, w)
+    return ref.cross_entropy(logits, labels, ignore_index)
+
+
+class _CEFn(Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        L = lib()
+        lg = logits.reshape(-1, logits.shape[-1]).contiguous().clone()
+        lab = labels.reshape(-1).contiguous()
+        inv_n = (1.0 / (lab != ignore_index).sum().clamp(min=1).float()).reshape(1)
+        _, _, lr = L.cross_entropy_(lg, lab, 0, ignore_index, None, None, inv_n, True)
+        ctx.save_for_backward(lg)
+        ctx.shape = logits.shape
+        return lr.sum() * inv_n[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (lg,) = ctx.saved_tensors
+        return (lg * g.to(lg.dtype)).view(ctx.shape), None, None
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100):
+    """Mean CE over non-ignored tokens (bf16 logits on GPU, in-place-gradient kernel)."""
+    if use_native(logits) and logits.dtype == torch.bfloat16:
+        return _CEFn.apply(logits, labels, ignore_index)
+    return ref.cross_entropy(logits, labels, ignore_index)
+
+
+class _LinearLogpsFn(Function):
+    """Per-token log p(label) of h @ W^T without materialising log_softmax (DPO / ORPO heads).
+
+    Backward recomputes each logits chunk (one extra GEMM) instead of keeping [N, V] alive, and the
+    HIP kernel writes g_t * (onehot - softmax) in place (coef_row = -g).
+    """
+
+    @staticmethod
+    def forward(ctx, h, w, labels, ignore_index, chunk):
+        L = lib()
+        N = h.shape[0]
+        out = torch.empty(N, device=h.device, dtype=torch.float32)
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = torch.matmul(h[s0:s1], w.t())
+            _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, None, False)
+            out[s0:s1] = -lr
+        ctx.save_for_backward(h, w, labels)
+        ctx.cfg = (ignore_index, chunk)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w, labels = ctx.saved_tensors
+        ignore_index, chunk = ctx.cfg
+        L = lib()
+        N = h.shape[0]
+        dh = torch.empty_like(h)
+        coef = (-g).float().contiguous()
+        dw_acc = None
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = torch.matmul(h[s0:s1], w.t())
+            L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, coef[s0:s1], None, True)
+            torch.matmul(lg, w, out=dh[s0:s1])
+            if ctx.needs_input_grad[1]:
+                r = _wgrad_mm(w, lg.t(), h[s0:s1])
+                if r is not None:
+                    dw_acc = r if dw_acc is None else dw_acc + r
+        return dh, dw_acc, None, None, None
+
+
+def linear_token_logps(h, w, labels, ignore_index: int = -100, chunk_size: int = 8192):
+    """log p(labels) per token for logits = h @ w.T; zeros where label == ignore_index. h: [N, H]."""
+    h2 = h.reshape(-1, h.shape[-1])
+    lab = labels.reshape(-1)
+    if use_native(h2):
+        out = _LinearLogpsFn.apply(h2.contiguous(), w, lab.contiguous(), ignore_index, chunk_size)
+    else:
+        out = ref.token_logps(linear(h2, w), lab, ignore_index)
+    return out.view(labels.shape)
+
+
+def token_logps(logits, labels, ignore_index: int = -100):
+    return ref.token_logps(logits, labels, ignore_index)

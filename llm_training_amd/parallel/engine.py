@@ -1,0 +1,508 @@
+"""Flat-buffer data-parallel engine: DDP / ZeRO-1 / ZeRO-2 / ZeRO-3 over RCCL, with the fused AdamW.
+
+Replaces the reference's two strategy back-ends — DeepSpeed ZeRO (SURVEY K13/P2/P3,
+src/llm_training/lightning/strategy/deepspeed/deepspeed_strategy.py) and FSDP2 fully_shard + the
+MasterWeightsOptimizer wrapper (P4/C15, lightning/strategy/fsdp2/fsdp2_strategy.py:249-263,
+optim/master_weight_wrapper.py) — with one engine designed around MI355X:
+
+* **Units.** The model declares its FSDP units (embedding, each decoder layer, final norm + lm_head).
+  Each unit owns ONE flat bf16 parameter buffer and ONE flat gradient buffer; every parameter of the
+  unit is a view into them (offsets 64-element aligned so the HIP kernels' 16-byte vector accesses
+  hold). A Llama-3-8B decoder layer is 218 M params = 436 MB bf16: one collective per unit is far
+  above the size where RCCL spreads a ring over every xGMI link, so no further bucketing is needed.
+* **Gradients** are written straight into the flat buffer by the fused ops (``param.main_grad``,
+  see ops/fused.py), so a unit is complete when autograd produces the gradient of the unit's INPUT —
+  a tensor hook on that input launches the unit's reduce-scatter (ZeRO) or all-reduce (DDP) on a
+  dedicated communication stream while backward continues with the previous unit.
+* **Optimizer.** fp32 master weights, Adam m and v exist only for this rank's shard of each unit
+  (stage >= 1) — 12 B/param / dp — and are updated by ONE fused HIP AdamW launch per unit that also
+  writes the bf16 parameter shard. Gradient averaging (1/dp), accumulation (1/accum) and clipping are
+  folded into a single device-side scale, so the step never synchronises with the host.
+* **Parameters.** stage 0-2 keep the full bf16 parameters resident (an 8B model is 16 GB of 288 GB);
+  after the step each unit's shard is all-gathered in place on the comm stream and the next forward
+  waits for that unit only. Stage 3 keeps only the shard and all-gathers a unit right before its
+  forward (prefetching the next unit) and again before its backward, freeing it afterwards.
+
+Checkpoint layout (see ckpt/): per-unit shards of master / m / v plus the step counter.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import re
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops.native import lib, use_native
+from .context import ParallelContext
+
+logger = logging.getLogger("llm_training")
+
+ALIGN = 64  # elements
+
+
+def _round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+@dataclass
+class _Unit:
+    idx: int
+    module: nn.Module
+    params: list[nn.Parameter]
+    offsets: list[int]
+    numel: int                      # padded flat size (multiple of dp * ALIGN)
+    pflat: torch.Tensor | None = None     # full bf16 params (stage <3: persistent)
+    gflat: torch.Tensor | None = None     # full gradient buffer
+    pshard: torch.Tensor | None = None    # stage 3: persistent bf16 shard
+    gshard: torch.Tensor | None = None    # reduced gradient shard (stage >= 1)
+    master: torch.Tensor | None = None    # fp32 master (shard or full)
+    exp_avg: torch.Tensor | None = None
+    exp_avg_sq: torch.Tensor | None = None
+    ready: bool = False
+    reduced: bool = False
+    gathered: bool = True
+    ag_event: object = None
+    rs_event: object = None
+    hook_handles: list = field(default_factory=list)
+    replicated: bool = False
+
+    @property
+    def shard_numel(self):
+        return self.numel // max(1, getattr(self, "_dp", 1))
+
+
+class DataParallelEngine:
+    def __init__(self, model: nn.Module, pc: ParallelContext, zero_stage: int = 2, *, lr: float = 1e-5,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01,
+                 grad_dtype: torch.dtype | None = None, reduce_dtype: torch.dtype | None = None,
+                 reshard_after_forward: bool = True, overlap_comm: bool = True):
+        self.model = model
+        self.pc = pc
+        self.stage = int(zero_stage)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
+        self.dp = pc.dp_size
+        self.group = pc.dp_group if pc.dp else None
+        self.overlap = overlap_comm and self.dp > 1
+        self.reshard_after_forward = reshard_after_forward
+        self.step_count = 0
+        self.accum = 1
+        self.micro = 0
+        dev = next(model.parameters()).device
+        self.device = dev
+        self.cuda = dev.type == "cuda"
+        self.native = self.cuda and use_native(torch.empty(0, device=dev))
+        self.comm_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.overlap) else None
+        self.param_dtype = next(model.parameters()).dtype
+        self.grad_dtype = grad_dtype or self.param_dtype
+        self.reduce_dtype = reduce_dtype or self.grad_dtype
+        self.units: list[_Unit] = []
+        self._build_units()
+        self._install_hooks()
+        self.grad_norm = None
+        self._gscale = torch.ones(1, device=dev, dtype=torch.float32)
+
+    # ------------------------------------------------------------------ construction
+    def _build_units(self):
+        seen: set[int] = set()
+        mods = self.model.fsdp_units() if hasattr(self.model, "fsdp_units") else [self.model]
+        groups: list[tuple[nn.Module, list[nn.Parameter], bool]] = []
+        rep: list[nn.Parameter] = []
+        for m in mods:
+            params = []
+            for p in m.parameters():
+                if id(p) in seen or not p.requires_grad:
+                    continue
+                seen.add(id(p))
+                if self.pc.tp and getattr(p, "tp_replicated", False):
+                    rep.append(p)  # norm weights / rowwise biases: partial grads per sequence shard
+                else:
+                    params.append(p)
+            groups.append((m, params, False))
+        if rep:
+            groups.append((None, rep, True))
+        for i, (m, params, replicated) in enumerate(groups):
+            self.units.append(self._make_unit(i, m, params, replicated))
+        nparams = sum(p.numel() for u in self.units for p in u.params)
+        logger.info("engine: %d units, %.3f B trainable params (local), zero stage %d, dp %d, tp %d",
+                    len(self.units), nparams / 1e9, self.stage, self.dp, self.pc.tp_size)
+
+    def _make_unit(self, i, m, params, replicated: bool) -> _Unit:
+        # a replicated unit (TP only) keeps full fp32 masters everywhere and all-reduces over the world
+        dp = 1 if replicated else self.dp
+        offs, n = [], 0
+        for p in params:
+            offs.append(n)
+            n = _round_up(n + p.numel(), ALIGN)
+        numel = _round_up(max(n, 1), ALIGN * dp)
+        u = _Unit(i, m, params, offs, numel)
+        u._dp = dp
+        u.replicated = replicated
+        dev, dt = self.device, self.param_dtype
+        pflat = torch.zeros(numel, device=dev, dtype=dt)
+        for p, o in zip(params, offs):
+            pflat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+            p.data = pflat[o:o + p.numel()].view(p.shape)
+        u.pflat = pflat
+        u.gflat = torch.zeros(numel, device=dev, dtype=self.grad_dtype)
+        for p, o in zip(params, offs):
+            p.main_grad = u.gflat[o:o + p.numel()].view(p.shape)
+            p.grad_added = False
+        sn = numel // dp
+        r = self.pc.dp_rank if dp > 1 else 0
+        stage = 0 if replicated else self.stage
+        if stage >= 1:
+            u.master = pflat[r * sn:(r + 1) * sn].float().clone()
+            if dp > 1:
+                u.gshard = torch.zeros(sn, device=dev, dtype=self.reduce_dtype)
+        else:
+            u.master = pflat.float().clone()
+        u.exp_avg = torch.zeros_like(u.master)
+        u.exp_avg_sq = torch.zeros_like(u.master)
+        if stage >= 3 and dp > 1:
+            u.pshard = pflat[r * sn:(r + 1) * sn].clone()
+            self._free_full(u)
+        return u
+
+    def _ustage(self, u: _Unit) -> int:
+        return 0 if u.replicated else self.stage
+
+    def _udp(self, u: _Unit) -> int:
+        return 1 if u.replicated else self.dp
+
+    def _free_full(self, u: _Unit):
+        u.pflat.untyped_storage().resize_(0)
+        u.gathered = False
+
+    def _alloc_full(self, u: _Unit):
+        st = u.pflat.untyped_storage()
+        if st.size() == 0:
+            st.resize_(u.numel * u.pflat.element_size())
+
+    # ------------------------------------------------------------------ hooks
+    def _install_hooks(self):
+        for u in self.units:
+            if u.module is None:
+                continue
+            u.hook_handles.append(u.module.register_forward_pre_hook(self._make_pre_fwd(u)))
+            if self.stage >= 3 and self.dp > 1:
+                u.hook_handles.append(u.module.register_forward_hook(self._make_post_fwd(u)))
+
+    def _make_pre_fwd(self, u: _Unit):
+        def hook(mod, args):
+            if self.stage >= 3 and self.dp > 1:
+                self._gather_unit(u)
+                nxt = self.units[u.idx + 1] if u.idx + 1 < len(self.units) else None
+                if nxt is not None and torch.is_grad_enabled():
+                    self._gather_unit(nxt, async_=True)
+            elif u.ag_event is not None:
+                torch.cuda.current_stream().wait_event(u.ag_event)
+                u.ag_event = None
+            if torch.is_grad_enabled() and (self.dp > 1 or self.pc.tp):
+                for a in args:
+                    if isinstance(a, torch.Tensor) and a.requires_grad:
+                        a.register_hook(self._make_grad_ready(u))
+                        break
+            return None
+        return hook
+
+    def _make_post_fwd(self, u: _Unit):
+        def hook(mod, args, out):
+            if self.reshard_after_forward and u.idx != len(self.units) - 1:
+                self._release_unit(u)
+            # re-gather before this unit's backward: hook the unit's output gradient
+            if torch.is_grad_enabled():
+                outs = out if isinstance(out, (tuple, list)) else (out,)
+                for t in outs:
+                    if isinstance(t, torch.Tensor) and t.requires_grad:
+                        t.register_hook(self._make_pre_bwd(u))
+                        break
+            return None
+        return hook
+
+    def _make_pre_bwd(self, u: _Unit):
+        def hook(g):
+            self._gather_unit(u)
+            if u.idx > 0:
+                self._gather_unit(self.units[u.idx - 1], async_=True)
+            return g
+        return hook
+
+    def _make_grad_ready(self, u: _Unit):
+        def hook(g):
+            if not u.reduced and self.micro == self.accum - 1:
+                self._reduce_unit(u)
+            return g
+        return hook
+
+    # ------------------------------------------------------------------ stage-3 gather / release
+    def _gather_unit(self, u: _Unit, async_: bool = False):
+        if u.gathered:
+            if u.ag_event is not None and not async_:
+                torch.cuda.current_stream().wait_event(u.ag_event)
+                u.ag_event = None
+            return
+        self._alloc_full(u)
+        sn = u.numel // self.dp
+        if self.cuda and self.comm_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                dist.all_gather_into_tensor(u.pflat, u.pshard, group=self.group)
+                done = torch.cuda.Event()
+                done.record(self.comm_stream)
+            u.ag_event = done
+            if not async_:
+                torch.cuda.current_stream().wait_event(done)
+                u.ag_event = None
+        else:
+            dist.all_gather_into_tensor(u.pflat, u.pshard, group=self.group)
+        u.gathered = True
+        del sn
+
+    def _release_unit(self, u: _Unit):
+        if self.cuda:
+            u.pflat.record_stream(torch.cuda.current_stream())
+        self._free_full(u)
+
+    # ------------------------------------------------------------------ gradient reduction
+    def _reduce_unit(self, u: _Unit):
+        u.reduced = True
+        if u.replicated:
+            # partial grads of sequence shards (TP) and of data shards (DP): sum over the whole world
+            dist.all_reduce(u.gflat)
+            return
+        if self.dp == 1:
+            return
+        src = u.gflat if u.gflat.dtype == self.reduce_dtype else u.gflat.to(self.reduce_dtype)
+
+        def op():
+            if self.stage >= 1:
+                dist.reduce_scatter_tensor(u.gshard, src, group=self.group)
+            else:
+                dist.all_reduce(src, group=self.group)
+                if src is not u.gflat:
+                    u.gflat.copy_(src)
+
+        if self.comm_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                op()
+                done = torch.cuda.Event()
+                done.record(self.comm_stream)
+            u.rs_event = done
+        else:
+            op()
+
+    # ------------------------------------------------------------------ public API used by the trainer
+    def begin_step(self, accumulate_grad_batches: int = 1):
+        self.accum = max(1, int(accumulate_grad_batches))
+        self.micro = 0
+
+    def begin_micro(self, i: int):
+        self.micro = i
+
+    def zero_grad(self):
+        for u in self.units:
+            u.reduced = False
+            for p in u.params:
+                p.grad_added = False
+                p.grad = None
+
+    def finish_backward(self):
+        """Called after the last micro-batch's backward: reduce units whose hook did not fire."""
+        for u in self.units:
+            if not u.reduced:
+                # params that received no gradient this step contribute zeros
+                for p in u.params:
+                    if not p.grad_added:
+                        p.main_grad.zero_()
+                        p.grad_added = True
+                self._reduce_unit(u)
+        if self.comm_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+        for u in self.units:
+            u.rs_event = None
+
+    def _grad_shard(self, u: _Unit) -> torch.Tensor:
+        if self._ustage(u) >= 1 and self._udp(u) > 1:
+            return u.gshard
+        return u.gflat
+
+    def clip_and_scale(self, max_norm: float | None):
+        """Global grad norm computed on device; returns the device scalar scale used by the optimizer."""
+        denom = float(self.dp * self.accum)
+        need_norm = max_norm is not None and max_norm > 0
+        sumsq = torch.zeros(1, device=self.device, dtype=torch.float32)
+        rep = torch.zeros(1, device=self.device, dtype=torch.float32)
+        for u in self.units:
+            g = self._grad_shard(u)
+            if u.replicated:
+                acc = rep  # identical on every rank after the world all-reduce: count once
+            elif self.stage == 0 and self.dp > 1 and self.pc.dp_rank != 0:
+                continue  # DP-replicated full grads: count once
+            else:
+                acc = sumsq
+            if self.native:
+                lib().sumsq_(g, acc)
+            else:
+                acc += g.float().pow(2).sum()
+        if self.pc.world_size > 1:
+            dist.all_reduce(sumsq)
+        norm = (sumsq + rep).sqrt() / denom
+        self.grad_norm = norm
+        if need_norm:
+            coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+            scale = coef / denom
+        else:
+            scale = torch.full_like(norm, 1.0 / denom)
+        self._gscale = scale.reshape(1).float().contiguous()
+        return self._gscale
+
+    @torch.no_grad()
+    def step(self, lr: float):
+        self.step_count += 1
+        b1, b2 = self.betas
+        dp, r = self.dp, self.pc.dp_rank
+        for u in self.units:
+            g = self._grad_shard(u)
+            st, udp = self._ustage(u), self._udp(u)
+            sn = u.numel // udp
+            rr = r if udp > 1 else 0
+            if st >= 1:
+                pout = u.pshard if (st >= 3 and udp > 1) else u.pflat[rr * sn:(rr + 1) * sn]
+            else:
+                pout = u.pflat
+            if self.native:
+                lib().adamw_(u.master, u.exp_avg, u.exp_avg_sq, g, pout, lr, b1, b2, self.eps,
+                             self.weight_decay, self.step_count, self._gscale)
+            else:
+                _adamw_ref(u.master, u.exp_avg, u.exp_avg_sq, g.float() * self._gscale, lr, b1, b2, self.eps,
+                           self.weight_decay, self.step_count)
+                pout.copy_(u.master)
+        # refresh the full bf16 parameters (stage 1/2): in-place all-gather of the updated shards
+        if self.stage in (1, 2) and dp > 1:
+            for u in self.units:
+                if u.replicated:
+                    continue
+                sn = u.numel // dp
+                shard = u.pflat[r * sn:(r + 1) * sn]
+                if self.comm_stream is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream())
+                    with torch.cuda.stream(self.comm_stream):
+                        self.comm_stream.wait_event(ev)
+                        dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
+                        done = torch.cuda.Event()
+                        done.record(self.comm_stream)
+                    u.ag_event = done
+                else:
+                    dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
+        if self.stage >= 3 and dp > 1:
+            for u in self.units:
+                if u.gathered and not u.replicated:
+                    self._release_unit(u)
+
+    def wait_params(self):
+        if self.comm_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+        for u in self.units:
+            u.ag_event = None
+
+    # ------------------------------------------------------------------ state (checkpointing)
+    def optimizer_state(self) -> dict:
+        return {
+            "step": self.step_count,
+            "units": [{"master": u.master, "exp_avg": u.exp_avg, "exp_avg_sq": u.exp_avg_sq} for u in self.units],
+            "stage": self.stage, "dp": self.dp, "dp_rank": self.pc.dp_rank,
+            "numels": [u.numel for u in self.units],
+        }
+
+    @torch.no_grad()
+    def load_optimizer_state(self, st: dict):
+        self.step_count = int(st["step"])
+        for u, s in zip(self.units, st["units"]):
+            u.master.copy_(s["master"])
+            u.exp_avg.copy_(s["exp_avg"])
+            u.exp_avg_sq.copy_(s["exp_avg_sq"])
+        self.sync_params_from_master()
+
+    @torch.no_grad()
+    def sync_params_from_master(self):
+        """Write bf16 params from the fp32 masters (after loading weights / optimizer state)."""
+        for u in self.units:
+            dp, st = self._udp(u), self._ustage(u)
+            r = self.pc.dp_rank if dp > 1 else 0
+            sn = u.numel // dp
+            if st >= 3 and dp > 1:
+                u.pshard.copy_(u.master)
+            elif st >= 1:
+                u.pflat[r * sn:(r + 1) * sn].copy_(u.master)
+                if dp > 1:
+                    dist.all_gather_into_tensor(u.pflat, u.pflat[r * sn:(r + 1) * sn].clone(), group=self.group)
+            else:
+                u.pflat.copy_(u.master)
+
+    @torch.no_grad()
+    def sync_master_from_params(self):
+        """Re-derive fp32 masters from the (freshly loaded) bf16/fp32 params."""
+        for u in self.units:
+            dp, st = self._udp(u), self._ustage(u)
+            r = self.pc.dp_rank if dp > 1 else 0
+            sn = u.numel // dp
+            if st >= 3 and dp > 1:
+                u.master.copy_(u.pshard)
+            elif st >= 1:
+                u.master.copy_(u.pflat[r * sn:(r + 1) * sn])
+            else:
+                u.master.copy_(u.pflat)
+
+    def full_params_context(self):
+        """Context manager materialising full params (stage 3) e.g. for export/eval."""
+        eng = self
+
+        class _Ctx:
+            def __enter__(self_):
+                if eng.stage >= 3 and eng.dp > 1:
+                    for u in eng.units:
+                        if not u.replicated:
+                            eng._gather_unit(u)
+                return eng.model
+
+            def __exit__(self_, *a):
+                if eng.stage >= 3 and eng.dp > 1:
+                    for u in eng.units:
+                        if not u.replicated:
+                            eng._release_unit(u)
+                return False
+
+        return _Ctx()
+
+
+def _adamw_ref(p, m, v, g, lr, b1, b2, eps, wd, step):
+    p.mul_(1 - lr * wd)
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+def freeze_modules(model: nn.Module, patterns: list[str] | None):
+    """Reference ``frozen_modules`` (regex over parameter names, src/llm_training/lms/base_lm.py:233-241)."""
+    if not patterns:
+        return []
+    regs = [re.compile(p) for p in patterns]
+    frozen = []
+    for n, p in model.named_parameters():
+        if any(r.search(n) for r in regs):
+            p.requires_grad_(False)
+            frozen.append(n)
+    return frozen

@@ -1,0 +1,157 @@
+"""Vocab-parallel fused linear + cross-entropy / token log-probs for tensor parallelism.
+
+Reference: ``loss_parallel()`` around F.cross_entropy on vocab-sharded DTensor logits
+(src/llm_training/lms/clm/clm.py:113-134) and the manual vocab-window gather + all_reduce of DPO/ORPO
+log-probs (lms/dpo/dpo.py:89-108, lms/orpo/orpo.py:68-87) — SURVEY K10/P7.
+
+Here each TP rank multiplies the (sequence-gathered) hidden states by its lm_head vocab shard, the
+HIP CE kernel produces the LOCAL log-sum-exp and target logit per row, ONE all-gather of the
+[tp, N] lse rows and ONE all-reduce of the target logits (N fp32 each) combine them, and a second
+kernel pass writes the local dlogits in place. dh is returned as a per-rank partial: the
+sequence-gather that produced h reduce-scatters (sums) it on the way back.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+from torch.autograd import Function
+
+from ..ops.fused import _wgrad_mm
+from ..ops.native import lib, use_native
+
+
+def _combine_lse(lse_local: torch.Tensor, group) -> torch.Tensor:
+    n = dist.get_world_size(group)
+    allv = torch.empty((n, *lse_local.shape), dtype=lse_local.dtype, device=lse_local.device)
+    dist.all_gather_into_tensor(allv, lse_local.contiguous(), group=group)
+    return torch.logsumexp(allv, dim=0)
+
+
+def _local_stats(lg, lab, v0, ignore_index, native):
+    """(lse_local, tgt_local) of logits lg [n, Vl] for global labels lab."""
+    if native:
+        lse, tgt, _ = lib().cross_entropy_(lg, lab, v0, ignore_index, None, None, None, False)
+        return lse, tgt
+    lf = lg.float()
+    lse = torch.logsumexp(lf, -1)
+    loc = lab - v0
+    hit = (lab != ignore_index) & (loc >= 0) & (loc < lg.shape[1])
+    tgt = lf.gather(1, loc.clamp(0, lg.shape[1] - 1).unsqueeze(1)).squeeze(1) * hit
+    return lse, tgt
+
+
+def _local_grad(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, native):
+    """Overwrite lg with coef * (softmax_global - onehot)."""
+    if native:
+        lib().cross_entropy_(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, True)
+        return lg
+    p = torch.exp(lg.float() - lse.unsqueeze(1))
+    loc = lab - v0
+    hit = (lab != ignore_index) & (loc >= 0) & (loc < lg.shape[1])
+    p[hit, loc[hit]] -= 1.0
+    c = (lab != ignore_index).float()
+    if coef_row is not None:
+        c = c * coef_row
+    if coef_scalar is not None:
+        c = c * coef_scalar
+    lg.copy_((p * c.unsqueeze(1)).to(lg.dtype))
+    return lg
+
+
+class _VPFusedCE(Function):
+    @staticmethod
+    def forward(ctx, h, w, labels, v0, ignore_index, group, chunk):
+        native = use_native(h)
+        N = h.shape[0]
+        inv_n = (1.0 / (labels != ignore_index).sum().clamp(min=1).float()).reshape(1)
+        lgs, lses, tgts = [], [], []
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = torch.matmul(h[s0:s1], w.t())
+            lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
+            lgs.append(lg)
+            lses.append(lse)
+            tgts.append(tgt)
+        lse = _combine_lse(torch.cat(lses), group)
+        tgt = torch.cat(tgts)
+        dist.all_reduce(tgt, group=group)
+        valid = labels != ignore_index
+        loss = ((lse - tgt) * valid).sum() * inv_n[0]
+        for i, lg in enumerate(lgs):
+            s0 = i * chunk
+            s1 = s0 + lg.shape[0]
+            _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), None, inv_n, native)
+        ctx.save_for_backward(h, w, *lgs)
+        ctx.chunk = chunk
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w, *lgs = ctx.saved_tensors
+        chunk = ctx.chunk
+        dh = torch.empty_like(h)
+        hs = h * g.to(h.dtype)
+        dw = None
+        for i, lg in enumerate(lgs):
+            s0 = i * chunk
+            s1 = s0 + lg.shape[0]
+            torch.matmul(lg, w, out=dh[s0:s1])
+            r = _wgrad_mm(w, lg.t(), hs[s0:s1])
+            if r is not None:
+                dw = r if dw is None else dw + r
+        dh.mul_(g.to(dh.dtype))
+        return dh, dw, None, None, None, None, None
+
+
+class _VPLogps(Function):
+    @staticmethod
+    def forward(ctx, h, w, labels, v0, ignore_index, group, chunk):
+        native = use_native(h)
+        N = h.shape[0]
+        lses, tgts = [], []
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = torch.matmul(h[s0:s1], w.t())
+            lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
+            lses.append(lse)
+            tgts.append(tgt)
+        lse = _combine_lse(torch.cat(lses), group)
+        tgt = torch.cat(tgts)
+        dist.all_reduce(tgt, group=group)
+        valid = labels != ignore_index
+        ctx.save_for_backward(h, w, labels, lse)
+        ctx.cfg = (v0, ignore_index, chunk)
+        return (tgt - lse) * valid
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w, labels, lse = ctx.saved_tensors
+        v0, ignore_index, chunk = ctx.cfg
+        native = use_native(h)
+        N = h.shape[0]
+        dh = torch.empty_like(h)
+        coef = (-g).float().contiguous()
+        dw = None
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = torch.matmul(h[s0:s1], w.t())
+            _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), coef[s0:s1], None, native)
+            torch.matmul(lg, w, out=dh[s0:s1])
+            r = _wgrad_mm(w, lg.t(), h[s0:s1])
+            if r is not None:
+                dw = r if dw is None else dw + r
+        return dh, dw, None, None, None, None, None
+
+
+def vocab_parallel_cross_entropy(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192):
+    h = h.reshape(-1, h.shape[-1]).contiguous()
+    return _VPFusedCE.apply(h, w_local, labels.reshape(-1).contiguous(), int(vocab_start), ignore_index, group,
+                            chunk_size)
+
+
+def vocab_parallel_token_logps(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192):
+    shape = labels.shape
+    h = h.reshape(-1, h.shape[-1]).contiguous()
+    out = _VPLogps.apply(h, w_local, labels.reshape(-1).contiguous(), int(vocab_start), ignore_index, group,
+                         chunk_size)
+    return out.view(shape)

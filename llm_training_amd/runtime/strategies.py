@@ -1,0 +1,102 @@
+"""Distributed strategies (YAML ``trainer.strategy``), all executed by the flat-buffer engine.
+
+Reference strategy surfaces: FSDP2Strategy (src/llm_training/lightning/strategy/fsdp2/
+fsdp2_strategy.py:49-78), DeepSpeedStrategy (lightning/strategy/deepspeed/deepspeed_strategy.py:17-72)
+and Lightning's ddp / single-device. The knobs keep their names; the ones that only make sense for
+DeepSpeed's engine (bucket sizes, offload, ZeRO++ quantisation) are accepted and recorded but the
+engine's own choices apply (per-layer units; see parallel/engine.py for why no extra bucketing is
+needed on xGMI).
+"""
+from __future__ import annotations
+
+import datetime
+import logging
+from dataclasses import dataclass, field
+from typing import Any
+
+logger = logging.getLogger("llm_training")
+
+
+@dataclass
+class Strategy:
+    zero_stage: int = 0
+    data_parallel_size: Any = "auto"
+    tensor_parallel_size: Any = 1
+    process_group_backend: str | None = None
+    timeout: Any = datetime.timedelta(minutes=30)
+    reshard_after_forward: bool = True
+    grad_reduce_dtype: str | None = None
+    overlap_comm: bool = True
+    save_distributed_checkpoint: bool = True
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def timeout_minutes(self) -> float:
+        t = self.timeout
+        if isinstance(t, datetime.timedelta):
+            return t.total_seconds() / 60
+        return float(t)
+
+
+class SingleDeviceStrategy(Strategy):
+    def __init__(self, **kw):
+        super().__init__(zero_stage=0, data_parallel_size=1, tensor_parallel_size=1)
+        self.extra = kw
+
+
+class DDPStrategy(Strategy):
+    def __init__(self, process_group_backend=None, timeout=datetime.timedelta(minutes=30), **kw):
+        super().__init__(zero_stage=0, process_group_backend=process_group_backend, timeout=timeout)
+        self.extra = kw
+
+
+class FSDP2Strategy(Strategy):
+    """ZeRO-3 (parameters, gradients and optimizer state sharded over the data-parallel group) x TP."""
+
+    def __init__(self, data_parallel_size="auto", tensor_parallel_size=1, save_distributed_checkpoint=True,
+                 process_group_backend=None, timeout=datetime.timedelta(minutes=30), reshard_after_forward=True,
+                 mp_policy=None, offload_policy=None, use_master_weights=True, zero_stage: int | None = None, **kw):
+        stage = 3 if zero_stage is None else int(zero_stage)
+        if zero_stage is None and reshard_after_forward is False:
+            # reference TP examples set reshard_after_forward=false: params stay gathered across the
+            # step; with 288 GB of HBM that is exactly ZeRO-2 (sharded grads + optimizer state)
+            stage = 2
+        super().__init__(zero_stage=stage, data_parallel_size=data_parallel_size,
+                         tensor_parallel_size=tensor_parallel_size, process_group_backend=process_group_backend,
+                         timeout=timeout, reshard_after_forward=bool(reshard_after_forward),
+                         save_distributed_checkpoint=save_distributed_checkpoint)
+        if offload_policy not in (None, {}) and not isinstance(offload_policy, dict):
+            logger.warning("FSDP2Strategy: CPU offload is not supported on this engine; ignored")
+        self.extra = {"mp_policy": mp_policy, "use_master_weights": use_master_weights, **kw}
+
+
+class DeepSpeedStrategy(Strategy):
+    """ZeRO stage 1/2/3 with DeepSpeed's argument names (stage=2 default, as in the reference)."""
+
+    def __init__(self, stage: int = 2, offload_optimizer: bool = False, offload_parameters: bool = False,
+                 exclude_frozen_parameters: bool = True, allgather_bucket_size: float = 2e8,
+                 reduce_bucket_size: float = 2e8, overlap_comm: bool = True, process_group_backend=None,
+                 timeout=datetime.timedelta(minutes=30), **kw):
+        super().__init__(zero_stage=int(stage), process_group_backend=process_group_backend, timeout=timeout,
+                         overlap_comm=overlap_comm)
+        if offload_optimizer or offload_parameters:
+            logger.warning("DeepSpeedStrategy: offload is not supported on this engine; ignored")
+        self.extra = {"exclude_frozen_parameters": exclude_frozen_parameters,
+                      "allgather_bucket_size": allgather_bucket_size, "reduce_bucket_size": reduce_bucket_size, **kw}
+
+
+STRATEGY_NAMES = {"ddp": DDPStrategy, "auto": DDPStrategy, "single_device": SingleDeviceStrategy,
+                  "fsdp": FSDP2Strategy, "fsdp2": FSDP2Strategy, "deepspeed": DeepSpeedStrategy,
+                  "deepspeed_stage_1": lambda: DeepSpeedStrategy(stage=1),
+                  "deepspeed_stage_2": lambda: DeepSpeedStrategy(stage=2),
+                  "deepspeed_stage_3": lambda: DeepSpeedStrategy(stage=3)}
+
+
+def resolve_strategy(s) -> Strategy:
+    if s is None:
+        return DDPStrategy()
+    if isinstance(s, Strategy):
+        return s
+    if isinstance(s, str):
+        return STRATEGY_NAMES[s]()
+    raise TypeError(f"unknown strategy {s!r}")

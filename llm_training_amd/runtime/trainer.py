@@ -1,0 +1,341 @@
+"""The training loop (replaces Lightning's Trainer for this framework).
+
+Reference behaviour reproduced: Lightning ``Trainer.fit`` as driven by the reference CLI
+(src/llm_training/lightning/cli/cli.py, trainer.py:4-11), gradient accumulation with loss averaging
+(SURVEY Q13), ``gradient_clip_val`` (norm clipping, every example sets 1.0), step-interval LR
+schedulers with auto-injected ``num_total_steps`` (base_lm.py:269-288), validation every
+``val_check_interval``, checkpoint callbacks, resume from ``ckpt_path`` with the data loader skipping
+consumed batches (data/resumable_dataloader.py) and grad-norm logging (base_lm.py:290-300).
+
+MI355X-specific choices: one process per GPU, weights built directly on the device in bf16 (TP-aware),
+one fused-AdamW launch per FSDP unit, device-side clipping (no host sync), metrics kept on device and
+read only every ``log_every_n_steps``.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import time
+from typing import Any
+
+import torch
+import torch.distributed as dist
+
+from ..optim import resolve_optimizer
+from ..parallel.context import ParallelContext, init_distributed
+from ..parallel.engine import DataParallelEngine, freeze_modules
+from .strategies import Strategy, resolve_strategy
+
+logger = logging.getLogger("llm_training")
+
+PRECISIONS = {"bf16-true": torch.bfloat16, "bf16": torch.bfloat16, "16-true": torch.float16,
+              "32-true": torch.float32, "32": torch.float32, "bf16-mixed": torch.bfloat16, 32: torch.float32,
+              16: torch.float16, "16-mixed": torch.float16}
+
+
+class TrainerState:
+    def __init__(self):
+        self.global_step = 0
+        self.epoch = 0
+        self.batch_idx = 0  # batches consumed in the current epoch
+        self.consumed: dict[str, float] = {}
+
+    def state_dict(self):
+        return {"global_step": self.global_step, "epoch": self.epoch, "batch_idx": self.batch_idx,
+                "consumed": dict(self.consumed)}
+
+    def load_state_dict(self, st):
+        self.global_step = int(st["global_step"])
+        self.epoch = int(st["epoch"])
+        self.batch_idx = int(st["batch_idx"])
+        self.consumed = dict(st.get("consumed", {}))
+
+
+class Trainer:
+    def __init__(self, strategy: Any = None, precision: Any = "bf16-true", logger: Any = None,
+                 callbacks: list | None = None, max_epochs: int | None = None, max_steps: int = -1,
+                 accumulate_grad_batches: int = 1, gradient_clip_val: float | None = None,
+                 gradient_clip_algorithm: str = "norm", val_check_interval: Any = None,
+                 check_val_every_n_epoch: int | None = 1, log_every_n_steps: int = 10, num_nodes: int = 1,
+                 devices: Any = "auto", accelerator: Any = "auto", limit_train_batches: Any = None,
+                 limit_val_batches: Any = None, enable_checkpointing: bool = True, enable_progress_bar: bool = True,
+                 default_root_dir: str = "logs", num_sanity_val_steps: int = 0, seed: int | None = None,
+                 deterministic: bool = False, benchmark: Any = None, **unused):
+        self.strategy: Strategy = resolve_strategy(strategy)
+        self.precision = precision
+        self.loggers = [] if logger in (None, False) else (list(logger) if isinstance(logger, list) else [logger])
+        self.callbacks = list(callbacks or [])
+        self.max_epochs = max_epochs
+        self.max_steps = max_steps if max_steps is not None else -1
+        self.accumulate_grad_batches = int(accumulate_grad_batches)
+        self.gradient_clip_val = gradient_clip_val
+        if gradient_clip_algorithm != "norm":
+            raise ValueError("only norm clipping is supported")
+        self.val_check_interval = val_check_interval
+        self.log_every_n_steps = max(1, int(log_every_n_steps))
+        self.num_nodes = num_nodes
+        self.limit_train_batches = limit_train_batches
+        self.limit_val_batches = limit_val_batches
+        self.enable_checkpointing = enable_checkpointing
+        self.enable_progress_bar = enable_progress_bar
+        self.default_root_dir = default_root_dir
+        self.seed = seed
+        self.state = TrainerState()
+        self.should_stop = False
+        self.unused = unused
+        if unused:
+            logger.debug("Trainer: ignoring unsupported arguments %s", sorted(unused))
+        self.pc: ParallelContext | None = None
+        self.engine: DataParallelEngine | None = None
+        self.lm = None
+        self.datamodule = None
+        self.scheduler = None
+        self.config_dict: dict | None = None
+        self._log_buffer: list[tuple[int, dict]] = []
+        self.last_metrics: dict[str, float] = {}
+        self.step_times: list[float] = []
+
+    # ------------------------------------------------------------------ properties used by callbacks
+    @property
+    def global_step(self):
+        return self.state.global_step
+
+    @property
+    def is_global_zero(self):
+        return self.pc is None or self.pc.rank == 0
+
+    @property
+    def world_size(self):
+        return self.pc.world_size if self.pc else 1
+
+    @property
+    def log_dir(self) -> str:
+        for lg in self.loggers:
+            d = getattr(lg, "log_dir", None)
+            if d:
+                return d
+        return self.default_root_dir
+
+    @property
+    def param_dtype(self):
+        return PRECISIONS.get(self.precision, torch.bfloat16)
+
+    # ------------------------------------------------------------------ setup
+    def setup(self, lm, datamodule, ckpt_path: str | None = None):
+        st = self.strategy
+        rank, local, world, device = init_distributed(st.process_group_backend, st.timeout_minutes)
+        self.device = device
+        self.pc = ParallelContext.create(st.data_parallel_size, st.tensor_parallel_size, device)
+        seed = self.seed if self.seed is not None else 42
+        torch.manual_seed(seed + self.pc.dp_rank)
+        self.lm, self.datamodule = lm, datamodule
+        for cb in self.callbacks:
+            _call(cb, "setup", self, lm, "fit")
+        datamodule.prepare_data()
+        datamodule.setup("fit")
+        resuming = ckpt_path is not None
+        lm.configure_model(self.pc, device, self.param_dtype, seed=seed, resuming=resuming)
+        frozen = freeze_modules(lm.model, getattr(lm.config, "frozen_modules", None))
+        if frozen:
+            logger.info("frozen %d parameters", len(frozen))
+        ospec = lm.optimizer_spec()
+        hp = resolve_optimizer(ospec["name"], ospec["kwargs"])
+        self.base_lr = hp["lr"]
+        rd = getattr(st, "grad_reduce_dtype", None)
+        self.engine = DataParallelEngine(lm.model, self.pc, st.zero_stage, lr=hp["lr"], betas=hp["betas"],
+                                         eps=hp["eps"], weight_decay=hp["weight_decay"],
+                                         reduce_dtype=getattr(torch, rd) if rd else None,
+                                         reshard_after_forward=st.reshard_after_forward,
+                                         overlap_comm=st.overlap_comm)
+        self.scheduler = lm.build_lr_scheduler(self.base_lr, self.estimated_stepping_batches())
+        if ckpt_path:
+            from ..ckpt.checkpoint import load_checkpoint
+            load_checkpoint(self, ckpt_path)
+        for lg in self.loggers:
+            _call(lg, "setup", self)
+
+    def train_loader(self):
+        return self.datamodule.train_dataloader(self.pc.dp_rank, self.pc.dp_size,
+                                                seed=(self.seed if self.seed is not None else 42),
+                                                skip_batches=self.state.batch_idx, epoch=self.state.epoch)
+
+    def num_batches_per_epoch(self) -> int:
+        n = len(self.datamodule.train_dataloader(self.pc.dp_rank, self.pc.dp_size).batch_sampler)
+        lim = self.limit_train_batches
+        if lim is not None:
+            n = min(n, int(lim) if (isinstance(lim, int) or float(lim) > 1) else int(n * float(lim)))
+        return n
+
+    def estimated_stepping_batches(self) -> int:
+        per_epoch = max(1, self.num_batches_per_epoch() // self.accumulate_grad_batches)
+        if self.max_steps is not None and self.max_steps > 0:
+            return self.max_steps
+        epochs = self.max_epochs if self.max_epochs is not None else 1
+        return per_epoch * epochs
+
+    # ------------------------------------------------------------------ loop
+    def fit(self, lm, datamodule=None, ckpt_path: str | None = None):
+        self.setup(lm, datamodule, ckpt_path)
+        for cb in self.callbacks:
+            _call(cb, "on_fit_start", self, lm)
+        max_epochs = self.max_epochs if self.max_epochs is not None else (1 if self.max_steps <= 0 else 10 ** 9)
+        lm.train()
+        nbe = self.num_batches_per_epoch()
+        while self.state.epoch < max_epochs and not self.should_stop:
+            loader = self.train_loader()
+            it = iter(loader)
+            accum = self.accumulate_grad_batches
+            while self.state.batch_idx + accum <= nbe and not self.should_stop:
+                batches = [next(it) for _ in range(accum)]
+                self.train_step(batches)
+                self.state.batch_idx += accum
+                if self.max_steps > 0 and self.state.global_step >= self.max_steps:
+                    self.should_stop = True
+                if self._should_validate(nbe):
+                    self.validate()
+            self.state.epoch += 1
+            self.state.batch_idx = 0
+            for cb in self.callbacks:
+                _call(cb, "on_train_epoch_end", self, lm)
+        self._flush_logs(force=True)
+        for cb in self.callbacks:
+            _call(cb, "on_fit_end", self, lm)
+        for lg in self.loggers:
+            _call(lg, "finalize", "success")
+        return self
+
+    def _should_validate(self, nbe: int) -> bool:
+        v = self.val_check_interval
+        if v is None or self.datamodule.datasets.get("validation") is None:
+            return False
+        if isinstance(v, float) and v <= 1.0:
+            every = max(1, int(nbe * v) // self.accumulate_grad_batches)
+        else:
+            every = int(v)
+        return self.state.global_step % every == 0
+
+    def to_device(self, batch: dict) -> dict:
+        out = {}
+        for k, v in batch.items():
+            out[k] = v.to(self.device, non_blocking=True) if isinstance(v, torch.Tensor) else v
+        return out
+
+    def train_step(self, batches: list[dict]):
+        eng, lm = self.engine, self.lm
+        t0 = time.perf_counter()
+        for cb in self.callbacks:
+            _call(cb, "on_train_batch_start", self, lm, batches[0], self.state.batch_idx)
+        eng.begin_step(len(batches))
+        eng.zero_grad()
+        metrics_acc: dict[str, torch.Tensor] = {}
+        counters: dict[str, Any] = {}
+        for i, b in enumerate(batches):
+            eng.begin_micro(i)
+            if i == 0:
+                eng.wait_params()
+            b = self.to_device(b)
+            loss, metrics, cnt = lm.training_step(b, self.state.batch_idx + i)
+            loss.backward()
+            for k, v in metrics.items():
+                metrics_acc[k] = metrics_acc.get(k, 0) + v.detach().float().to(self.device) / len(batches)
+            for k, v in cnt.items():
+                counters[k] = counters.get(k, 0) + v
+        eng.finish_backward()
+        eng.clip_and_scale(self.gradient_clip_val)
+        lr = self.scheduler.get_lr()
+        eng.step(lr)
+        self.scheduler.step()
+        self.state.global_step += 1
+        for k, v in counters.items():
+            self.state.consumed[k] = self.state.consumed.get(k, 0) + v
+        metrics_acc["lr"] = torch.tensor(lr)
+        if getattr(lm.config, "log_grad_norm", True) and eng.grad_norm is not None:
+            metrics_acc["Gradient Norm"] = eng.grad_norm.reshape(())
+        self._log_buffer.append((self.state.global_step, metrics_acc))
+        self.step_times.append(time.perf_counter() - t0)
+        self._flush_logs()
+        for cb in self.callbacks:
+            _call(cb, "on_train_batch_end", self, lm, None, batches[-1], self.state.batch_idx)
+
+    def _flush_logs(self, force: bool = False):
+        if not self._log_buffer:
+            return
+        if not force and self.state.global_step % self.log_every_n_steps != 0:
+            return
+        # one host sync per logging interval; DP-average the scalar metrics
+        keys = sorted({k for _, m in self._log_buffer for k in m})
+        rows = []
+        for step, m in self._log_buffer:
+            vec = torch.stack([torch.as_tensor(m.get(k, float("nan")), device=self.device).float().reshape(())
+                               for k in keys])
+            rows.append((step, vec))
+        mat = torch.stack([r[1] for r in rows])
+        if self.pc.dp and self.pc.world_size > 1:
+            dist.all_reduce(mat, group=self.pc.dp_group)
+            mat = mat / self.pc.dp_size
+        mat = mat.cpu().tolist()
+        consumed = dict(self.state.consumed)
+        if self.pc.dp and consumed:
+            t = torch.tensor([float(consumed[k]) for k in sorted(consumed)], device=self.device)
+            dist.all_reduce(t, group=self.pc.dp_group)
+            consumed = dict(zip(sorted(consumed), t.cpu().tolist()))
+        for (step, _), vals in zip(rows, mat):
+            d = dict(zip(keys, vals))
+            d.update({k: float(v) for k, v in consumed.items()})
+            self.last_metrics = d
+            if self.is_global_zero:
+                for lg in self.loggers:
+                    _call(lg, "log_metrics", d, step)
+        if self.is_global_zero and self.enable_progress_bar:
+            d = self.last_metrics
+            loss = next((d[k] for k in d if k.startswith("Loss/Train") or k == "Loss/Train/Step"), float("nan"))
+            logger.info("step %d | loss %.4f | lr %.3e | grad_norm %.3f", self.state.global_step, loss,
+                        d.get("lr", float("nan")), d.get("Gradient Norm", float("nan")))
+        self._log_buffer.clear()
+
+    @torch.no_grad()
+    def validate(self):
+        dl = self.datamodule.val_dataloader(self.pc.dp_rank, self.pc.dp_size)
+        if dl is None:
+            return {}
+        self.lm.eval()
+        sums: dict[str, torch.Tensor] = {}
+        n = 0
+        for i, b in enumerate(dl):
+            if self.limit_val_batches is not None and i >= int(self.limit_val_batches):
+                break
+            m = self.lm.validation_step(self.to_device(b), i)
+            for k, v in m.items():
+                sums[k] = sums.get(k, 0) + v.float()
+            n += 1
+        self.lm.train()
+        if n == 0:
+            return {}
+        keys = sorted(sums)
+        vec = torch.stack([sums[k].reshape(()) / n for k in keys])
+        if self.pc.world_size > 1:
+            dist.all_reduce(vec)
+            vec = vec / self.pc.world_size
+        out = dict(zip(keys, vec.cpu().tolist()))
+        if "Loss/Val" in out and "Perplexity/Val" in out:
+            out["Perplexity/Val"] = math.exp(out["Loss/Val"])
+        if self.is_global_zero:
+            for lg in self.loggers:
+                _call(lg, "log_metrics", out, self.state.global_step)
+            logger.info("validation @ step %d: %s", self.state.global_step, out)
+        for cb in self.callbacks:
+            _call(cb, "on_validation_end", self, self.lm, out)
+        return out
+
+    # ------------------------------------------------------------------ checkpoint helpers for callbacks
+    def save_checkpoint(self, path: str):
+        from ..ckpt.checkpoint import save_checkpoint
+        save_checkpoint(self, path)
+
+
+def _call(obj, name, *args):
+    fn = getattr(obj, name, None)
+    if fn is not None:
+        return fn(*args)
+    return None

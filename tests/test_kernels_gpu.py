@@ -1,0 +1,214 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+
+from llm_training_amd.ops import fused as F_
+from llm_training_amd.ops import reference as ref
+from llm_training_amd.ops.native import lib
+from llm_training_amd.ops.rope_utils import compute_rope_tables
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_native_loaded():
+    L = lib()
+    assert hasattr(L, "rmsnorm_fwd")
+
+
+@pytest.mark.parametrize("H", [768, 3072, 4096, 5120])
+@pytest.mark.parametrize("residual", [False, True])
+def test_rmsnorm(H, residual):
+    torch.manual_seed(0)
+    T = 1000
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True) if residual else None
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16().requires_grad_(True)
+    if residual:
+        y, s = F_.rms_norm(x, w, 1e-5, r)
+    else:
+        y = F_.rms_norm(x, w, 1e-5)
+    dy = torch.randn_like(y)
+    ds = torch.randn_like(y) if residual else None
+    (y.float() * dy.float()).sum().add((s.float() * ds.float()).sum() if residual else 0).backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if residual else None
+    sr = xr + rr if residual else xr
+    yr = ref.rms_norm(sr, wr, 1e-5)
+    ((yr * dy.float()).sum() + ((sr * ds.float()).sum() if residual else 0)).backward()
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    if residual:
+        assert _rel(s, sr) < 1e-2
+        assert _rel(r.grad, rr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("I", [512, 14336])
+def test_swiglu(I):
+    torch.manual_seed(0)
+    gu = torch.randn(300, 2 * I, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    c = F_.swiglu(gu)
+    dc = torch.randn_like(c)
+    (c.float() * dc.float()).sum().backward()
+    gr = gu.detach().float().requires_grad_(True)
+    cr = ref.swiglu_fused(gr)
+    (cr * dc.float()).sum().backward()
+    assert _rel(c, cr) < 1e-2
+    assert _rel(gu.grad, gr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("D", [64, 96, 128])
+def test_rope_inplace_roundtrip(D):
+    torch.manual_seed(0)
+    S, B, H = 257, 2, 6
+    qkv = torch.randn(S, B, H, D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (B, S), device=DEV)
+    cos, sin = compute_rope_tables(D, 4096, 500000.0, device=DEV)
+    x = qkv.clone()
+    lib().rope_(x, pos.t().contiguous().reshape(-1), cos, sin, 4, False)
+    cf, sf = F_.rope_tables_to_full(cos, sin, pos.t())  # [S, B, D]
+    q = qkv[:, :, :4].float()
+    exp = q * cf[:, :, None] + ref.rotate_half(q) * sf[:, :, None]
+    assert _rel(x[:, :, :4], exp) < 1e-2
+    assert torch.equal(x[:, :, 4:], qkv[:, :, 4:])
+    lib().rope_(x, pos.t().contiguous().reshape(-1), cos, sin, 4, True)
+    assert _rel(x, qkv) < 2e-2
+
+
+@pytest.mark.parametrize("V", [32064, 128256, 50257])
+def test_cross_entropy(V):
+    torch.manual_seed(0)
+    N = 257
+    logits = (3 * torch.randn(N, V, device=DEV)).bfloat16().requires_grad_(True)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[::7] = -100
+    loss = F_.cross_entropy(logits, labels)
+    loss.backward()
+    lr_ = logits.detach().float().requires_grad_(True)
+    lref = torch.nn.functional.cross_entropy(lr_, labels, ignore_index=-100)
+    lref.backward()
+    assert abs(loss.item() - lref.item()) < 1e-3 * max(1, abs(lref.item()))
+    assert _rel(logits.grad, lr_.grad) < 2e-2
+
+
+def test_fused_linear_cross_entropy():
+    torch.manual_seed(0)
+    N, H, V = 600, 256, 32064
+    h = torch.randn(N, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (0.05 * torch.randn(V, H, device=DEV)).bfloat16().requires_grad_(True)
+    lab = torch.randint(0, V, (N,), device=DEV)
+    lab[:50] = -100
+    loss = F_.fused_linear_cross_entropy(h, w, lab, chunk_size=256)
+    loss.backward()
+    hr = h.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    lref = torch.nn.functional.cross_entropy(hr @ wr.t(), lab, ignore_index=-100)
+    lref.backward()
+    assert abs(loss.item() - lref.item()) < 1e-2
+    assert _rel(h.grad, hr.grad) < 3e-2
+    assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def test_linear_token_logps():
+    torch.manual_seed(0)
+    N, H, V = 300, 128, 5000
+    h = torch.randn(N, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (0.1 * torch.randn(V, H, device=DEV)).bfloat16().requires_grad_(True)
+    lab = torch.randint(0, V, (N,), device=DEV)
+    lab[::5] = -100
+    lp = F_.linear_token_logps(h, w, lab, chunk_size=128)
+    g = torch.randn_like(lp)
+    (lp * g).sum().backward()
+    hr = h.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    lpr = ref.token_logps(hr @ wr.t(), lab)
+    (lpr * g).sum().backward()
+    assert _rel(lp, lpr) < 1e-2
+    assert _rel(h.grad, hr.grad) < 3e-2
+    assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def test_adamw_matches_torch():
+    torch.manual_seed(0)
+    n = 4096 * 3
+    p0 = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV).bfloat16()
+    p, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    pout = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    scale = torch.tensor([0.5], device=DEV)
+    tp = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([tp], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        lib().adamw_(p, m, v, g, pout, 1e-2, 0.9, 0.95, 1e-8, 0.1, step, scale)
+        tp.grad = g.float() * 0.5
+        opt.step()
+    assert _rel(p, tp.detach()) < 1e-5
+    assert _rel(pout, tp.detach()) < 1e-2
+    out = torch.zeros(1, device=DEV)
+    lib().sumsq_(g, out)
+    assert abs(out.item() - g.float().pow(2).sum().item()) / out.item() < 1e-4
+
+
+def _attn_case(B, S, Hq, Hkv, D, causal=True, seg=None, window=-1, layout="bshd"):
+    torch.manual_seed(0)
+    q = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = F_.flash_attention(q, k, v, causal, seg, window)
+    do = torch.randn_like(o)
+    (o.float() * do.float()).sum().backward()
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    orf = ref.attention(qr, kr, vr, causal, seg, window)
+    (orf * do.float()).sum().backward()
+    errs = (_rel(o, orf), _rel(q.grad, qr.grad), _rel(k.grad, kr.grad), _rel(v.grad, vr.grad))
+    assert errs[0] < 2e-2, errs
+    assert max(errs[1:]) < 4e-2, errs
+
+
+@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("Hq,Hkv", [(4, 4), (8, 2)])
+def test_flash_attention_causal(D, Hq, Hkv):
+    _attn_case(2, 300, Hq, Hkv, D)
+
+
+def test_flash_attention_noncausal():
+    _attn_case(1, 200, 4, 2, 128, causal=False)
+
+
+def test_flash_attention_segments():
+    B, S = 2, 384
+    seg = torch.ones(B, S, dtype=torch.int32, device=DEV)
+    seg[0, 100:250] = 2
+    seg[0, 250:] = 3
+    seg[1, 300:] = 0
+    _attn_case(B, S, 4, 2, 128, seg=seg)
+
+
+def test_flash_attention_window():
+    _attn_case(1, 512, 4, 4, 96, window=100)
+
+
+def test_rope_attention_fused_matches_reference():
+    torch.manual_seed(0)
+    S, B, nq, nkv, D = 256, 2, 8, 2, 128
+    qkv = torch.randn(S, B, nq + 2 * nkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    pos = torch.arange(S, device=DEV).expand(B, S)
+    cos, sin = compute_rope_tables(D, 1024, 500000.0, device=DEV)
+    o = F_.rope_attention(qkv * 1.0, pos, cos, sin, nq, nkv)
+    do = torch.randn_like(o)
+    (o.float() * do.float()).sum().backward()
+    qr = qkv.detach().float().requires_grad_(True)
+    orf = F_._ref_rope_attention(qr.transpose(0, 1), pos, cos, sin, nq, nkv, True, None, -1, 1 / math.sqrt(D),
+                                 "eager").transpose(0, 1)
+    (orf * do.float()).sum().backward()
+    assert _rel(o, orf) < 2e-2
+    assert _rel(qkv.grad, qr.grad) < 4e-2
