@@ -100,16 +100,17 @@ def main():
         engine.step(3e-5)
         return loss
 
-    batches = [make_batch() for _ in range(2)]
+    # fresh synthetic batches for every step (pre-generated so the timed loop does no data work)
+    batches = [make_batch() for _ in range(args.warmup + args.steps)]
     for i in range(args.warmup):
-        loss = step(batches[i % 2])
+        loss = step(batches[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = step(batches[i % 2])
+        loss = step(batches[args.warmup + i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
