@@ -81,13 +81,57 @@ __device__ __forceinline__ bfv8 acc_as_b(const f32v16& a, int s) {
   return __builtin_convertvector(f, bfv8);
 }
 
-__device__ __forceinline__ bfv8 gload8(const bf16* p, bool ok) {
-  if (ok) return *reinterpret_cast<const bfv8*>(p);
-  bfv8 z;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.f;
-  return z;
+// 16-byte buffer load; rows past the descriptor's num_records come back as zeros (no selects).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)min<int64_t>(bytes, 0x7fffffff),
+                                           0x00020000);
 }
+__device__ __forceinline__ bfv8 bload8(__amdgpu_buffer_rsrc_t r, int off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return __builtin_bit_cast(bfv8, v);
+}
+
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Dual-use LDS image of a [rows][D] bf16 tile: for D = 128 one XOR-swizzled image of 256-byte rows
+// serves both ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads conflict-free
+// (chunk' = chunk ^ ((r&3)<<2 | (r>>2)&3)); other D use a padded row image plus a padded tr image.
+template <int D>
+struct Img {
+  static constexpr bool kDual = (D == 128);
+  static constexpr int RP = kDual ? 256 : 2 * D + 16;
+  static constexpr int TPb = kDual ? 256 : ((D == 128) ? 320 : 192);
+  static constexpr int bytes(int rows) { return kDual ? rows * 256 : rows * (RP + TPb); }
+  __device__ static __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+  // row image: byte offset of 16-byte chunk ch of row r
+  __device__ static __forceinline__ int roff(int r, int ch) {
+    if constexpr (kDual) return 256 * r + 16 * (ch ^ swz(r));
+    else return r * RP + 16 * ch;
+  }
+  // transposed-read image: byte offset of element `col` (multiple of 4) of row r
+  __device__ static __forceinline__ int toff(int rows, int r, int col) {
+    if constexpr (kDual) return 256 * r + 16 * ((col >> 3) ^ swz(r)) + 2 * (col & 7);
+    else return rows * RP + r * TPb + 2 * col;
+  }
+  __device__ static __forceinline__ void store(char* base, int rows, int r, int ch, const bfv8& v) {
+    *reinterpret_cast<bfv8*>(base + roff(r, ch)) = v;
+    if constexpr (!kDual) *reinterpret_cast<bfv8*>(base + rows * RP + r * TPb + 16 * ch) = v;
+  }
+  __device__ static __forceinline__ bfv8 row_read(const char* base, int r, int ch) {
+    return *reinterpret_cast<const bfv8*>(base + roff(r, ch));
+  }
+  // A operand of the accumulator-as-B product (see lds_trA): rows rbase.., columns c0 + (lane & 31)
+  __device__ static __forceinline__ bfv8 trA(const char* base, int rows, int rbase, int c0, int lane) {
+    const int g = lane >> 4, i16 = lane & 15;
+    const int row = rbase + 4 * (g >> 1) + (i16 >> 2);
+    const int col = c0 + 16 * (g & 1) + 4 * (i16 & 3);
+    const s16v4 lo = lds_tr(base + toff(rows, row, col));
+    const s16v4 hi = lds_tr(base + toff(rows, row + 8, col));
+    return __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
 
 struct AttnArgs {
   const bf16* q;
@@ -111,24 +155,18 @@ struct AttnArgs {
   int causal, window;
 };
 
-__device__ __forceinline__ bool visible(int qi, int kj, int S, int causal, int window, const int* seg, int sq) {
-  bool ok = kj < S && qi < S;
-  if (causal) ok = ok && (kj <= qi);
-  if (window >= 0) ok = ok && (kj >= qi - window);
-  if (seg) ok = ok && (seg[kj] == sq);
-  return ok;
-}
+constexpr float kThr = 6.0f;  // defer-max threshold (log2 units): P <= 2^6 before a forced rescale
 
 // ============================================================================ forward
-// grid: (ceil(S/128), Hq, B), block 256 = 4 waves x 32 queries; KV tiles of 64 keys.
+// grid: (ceil(S/128), Hq, B), block 256 = 4 waves x 32 queries; KV tiles of 64 keys, double-buffered LDS
+// (one barrier per tile), next tile's buffer loads in flight during the current tile's MFMAs.
 template <int D>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
   using G = FaGeom<D>;
   constexpr int BN = 64;
   constexpr int NV = BN * G::V8 / 256;  // staged 16-B vectors per thread per tensor
-  __shared__ __attribute__((aligned(16))) char smem[BN * G::KP + BN * G::TP];
-  char* Ks = smem;
-  char* Vs = smem + BN * G::KP;
+  constexpr int BUF = BN * G::KP + BN * G::TP + BN * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int nqb = (a.S + 127) / 128;
@@ -137,15 +175,16 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
   const int S = a.S;
   const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
   const bf16* qp = a.q + b * a.q_sb + h * a.q_sh;
-  const bf16* kp = a.k + b * a.k_sb + hk * a.k_sh;
-  const bf16* vp = a.v + b * a.v_sb + hk * a.v_sh;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + b * a.k_sb + hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + b * a.v_sb + hk * a.v_sh, (int64_t)S * a.v_ss * 2);
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(qp, (int64_t)S * a.q_ss * 2);
   const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
   const int sq = (seg && qrow < S) ? seg[qrow] : 0;
   const float sl2 = a.scale * kLog2e;
 
   bfv8 qf[G::NKK];
 #pragma unroll
-  for (int kk = 0; kk < G::NKK; ++kk) qf[kk] = gload8(qp + (int64_t)qrow * a.q_ss + kk * 16 + hh * 8, qrow < S);
+  for (int kk = 0; kk < G::NKK; ++kk) qf[kk] = bload8(qrs, (int)(qrow * a.q_ss + kk * 16 + hh * 8) * 2);
 
   f32v16 ot[G::NDT];
 #pragma unroll
@@ -159,31 +198,38 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
   kv_beg = kv_beg / BN * BN;
 
   bfv8 kst[NV], vst[NV];
+  int sst = 0;
   auto load_tile = [&](int n0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, kr = n0 + row;
-      kst[i] = gload8(kp + (int64_t)kr * a.k_ss + c8 * 8, kr < S);
-      vst[i] = gload8(vp + (int64_t)kr * a.v_ss + c8 * 8, kr < S);
+      kst[i] = bload8(krs, (int)(kr * a.k_ss + c8 * 8) * 2);
+      vst[i] = bload8(vrs, (int)(kr * a.v_ss + c8 * 8) * 2);
     }
+    if (seg && tid < BN) sst = (n0 + tid < S) ? seg[n0 + tid] : -1;
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](char* buf) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8;
-      *reinterpret_cast<bfv8*>(Ks + row * G::KP + c8 * 16) = kst[i];
-      *reinterpret_cast<bfv8*>(Vs + row * G::TP + c8 * 16) = vst[i];
+      *reinterpret_cast<bfv8*>(buf + row * G::KP + c8 * 16) = kst[i];
+      *reinterpret_cast<bfv8*>(buf + BN * G::KP + row * G::TP + c8 * 16) = vst[i];
     }
+    if (seg && tid < BN) reinterpret_cast<int*>(buf + BN * G::KP + BN * G::TP)[tid] = sst;
   };
 
   if (kv_beg < kv_end) {
     load_tile(kv_beg);
-    store_tile();
+    store_tile(smem);
   }
   __syncthreads();
-  for (int n0 = kv_beg; n0 < kv_end; n0 += BN) {
+  int cur = 0;
+  for (int n0 = kv_beg; n0 < kv_end; n0 += BN, cur ^= 1) {
     const bool has_next = n0 + BN < kv_end;
     if (has_next) load_tile(n0 + BN);
+    const char* Ks = smem + cur * BUF;
+    const char* Vs = Ks + BN * G::KP;
+    const int* Ss = reinterpret_cast<const int*>(Vs + BN * G::TP);
 
     f32v16 st[2];
 #pragma unroll
@@ -194,40 +240,65 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
       for (int kk = 0; kk < G::NKK; ++kk)
         st[t] = mfma32(lds_b128(Ks + (32 * t + r) * G::KP + (kk * 16 + hh * 8) * 2), qf[kk], st[t]);
     }
-    const bool need_mask = seg || (n0 + BN > S) || (a.causal && n0 + BN - 1 > qw) ||
-                           (a.window >= 0 && n0 < qw + 31 - a.window) || qw + 31 >= S;
+    // masking only where needed: diagonal (causal), window edge, sequence end, packed segments
+    const bool m_causal = a.causal && (n0 + BN - 1 > qw);
+    const bool m_window = a.window >= 0 && (n0 < qw + 31 - a.window);
+    const bool m_end = n0 + BN > S;
     float smax = -INFINITY;
+    if (m_causal || m_window || m_end || seg) {
+      const int lim = qrow - n0 - 4 * hh;         // causal: key offset <= lim
+      const int lo = qrow - a.window - n0 - 4 * hh;  // window: key offset >= lo
+      const int hi = S - 1 - n0 - 4 * hh;            // bounds
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float s = st[t][i] * sl2;
-        if (need_mask) {
-          const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (!visible(qrow, kj, S, a.causal, a.window, seg, sq)) s = -INFINITY;
+        for (int c = 0; c < 4; ++c) {
+          int4 sk = make_int4(sq, sq, sq, sq);
+          if (seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * t + 8 * c + 4 * hh);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int i = 4 * c + j, ko = 32 * t + 8 * c + j;
+            bool ok = (ko <= hi) && (qrow < S);
+            if (a.causal) ok = ok && (ko <= lim);
+            if (a.window >= 0) ok = ok && (ko >= lo);
+            if (seg) ok = ok && ((&sk.x)[j] == sq);
+            const float s = ok ? st[t][i] * sl2 : -INFINITY;
+            st[t][i] = s;
+            smax = fmaxf(smax, s);
+          }
         }
-        st[t][i] = s;
-        smax = fmaxf(smax, s);
-      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          st[t][i] *= sl2;
+          smax = fmaxf(smax, st[t][i]);
+        }
+    }
     smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
-    const float mnew = fmaxf(m, smax);
-    const float muse = (mnew == -INFINITY) ? 0.f : mnew;
-    const float alpha = exp2f(m - muse);
-    m = mnew;
+    // deferred rescale: keep the running max unless some row grew by more than kThr
+    if (__any(smax > m + kThr)) {
+      const float mnew = fmaxf(m, smax);
+      const float alpha = (mnew == -INFINITY) ? 1.f : fexp2(m - mnew);  // m = -inf -> 0
+      m = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < G::NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
+    }
+    const float muse = (m == -INFINITY) ? 0.f : m;
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(st[t][i] - muse);
+        const float p = fexp2(st[t][i] - muse);
         st[t][i] = p;
         rs += p;
       }
-    l = l * alpha + rs;
-#pragma unroll
-    for (int dt = 0; dt < G::NDT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
+    l += rs;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -237,8 +308,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
         for (int dt = 0; dt < G::NDT; ++dt)
           ot[dt] = mfma32(lds_trA(Vs, G::TP, 32 * t + 16 * s2, dt * 32, lane), pb, ot[dt]);
       }
-    __syncthreads();
-    if (has_next) store_tile();
+    if (has_next) store_tile(smem + (cur ^ 1) * BUF);
     __syncthreads();
   }
 
@@ -263,7 +333,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward: delta = rowsum(dO * O)
-// one thread per (b, s, h) row of D elements (16-byte loads).
 template <int D>
 __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(AttnArgs a) {
   const int64_t nrows = (int64_t)a.B * a.S * a.Hq;
@@ -288,16 +357,16 @@ __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward: dQ (query-parallel)
-// grid: (ceil(S/128), Hq, B); 4 waves x 32 queries; KV tiles of 64 keys.
+// grid: (ceil(S/128), Hq, B); 4 waves x 32 queries; KV tiles of 64 keys, double-buffered.
 template <int D>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
   using G = FaGeom<D>;
+  using KI = Img<D>;
   constexpr int BN = 64;
   constexpr int NV = BN * G::V8 / 256;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BN * G::KP + BN * G::TP];
-  char* Ks = smem;                    // K rows (b128 reads)
-  char* Vs = smem + BN * G::KP;       // V rows (b128 reads)
-  char* Kt = smem + 2 * BN * G::KP;   // K for transposed reads
+  constexpr int KB = KI::bytes(BN);
+  constexpr int BUF = KB + BN * G::KP + BN * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int nqb = (a.S + 127) / 128;
@@ -305,10 +374,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
   const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
   const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
-  const bf16* qp = a.q + b * a.q_sb + h * a.q_sh;
-  const bf16* dop = a.dout + b * a.d_sb + h * a.d_sh;
-  const bf16* kp = a.k + b * a.k_sb + hk * a.k_sh;
-  const bf16* vp = a.v + b * a.v_sb + hk * a.v_sh;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(a.q + b * a.q_sb + h * a.q_sh, (int64_t)S * a.q_ss * 2);
+  const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.dout + b * a.d_sb + h * a.d_sh, (int64_t)S * a.d_ss * 2);
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + b * a.k_sb + hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + b * a.v_sb + hk * a.v_sh, (int64_t)S * a.v_ss * 2);
   const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
   const int sq = (seg && qrow < S) ? seg[qrow] : 0;
   const float sl2 = a.scale * kLog2e;
@@ -319,8 +388,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
   bfv8 qf[G::NKK], df[G::NKK];
 #pragma unroll
   for (int kk = 0; kk < G::NKK; ++kk) {
-    qf[kk] = gload8(qp + (int64_t)qrow * a.q_ss + kk * 16 + hh * 8, qrow < S);
-    df[kk] = gload8(dop + (int64_t)qrow * a.d_ss + kk * 16 + hh * 8, qrow < S);
+    qf[kk] = bload8(qrs, (int)(qrow * a.q_ss + kk * 16 + hh * 8) * 2);
+    df[kk] = bload8(drs, (int)(qrow * a.d_ss + kk * 16 + hh * 8) * 2);
   }
   f32v16 dqt[G::NDT];
 #pragma unroll
@@ -333,31 +402,37 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
   kv_beg = kv_beg / BN * BN;
 
   bfv8 kst[NV], vst[NV];
+  int sst = 0;
   auto load_tile = [&](int n0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, kr = n0 + row;
-      kst[i] = gload8(kp + (int64_t)kr * a.k_ss + c8 * 8, kr < S);
-      vst[i] = gload8(vp + (int64_t)kr * a.v_ss + c8 * 8, kr < S);
+      kst[i] = bload8(krs, (int)(kr * a.k_ss + c8 * 8) * 2);
+      vst[i] = bload8(vrs, (int)(kr * a.v_ss + c8 * 8) * 2);
     }
+    if (seg && tid < BN) sst = (n0 + tid < S) ? seg[n0 + tid] : -1;
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](char* buf) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8;
-      *reinterpret_cast<bfv8*>(Ks + row * G::KP + c8 * 16) = kst[i];
-      *reinterpret_cast<bfv8*>(Kt + row * G::TP + c8 * 16) = kst[i];
-      *reinterpret_cast<bfv8*>(Vs + row * G::KP + c8 * 16) = vst[i];
+      KI::store(buf, BN, row, c8, kst[i]);
+      *reinterpret_cast<bfv8*>(buf + KB + row * G::KP + c8 * 16) = vst[i];
     }
+    if (seg && tid < BN) reinterpret_cast<int*>(buf + KB + BN * G::KP)[tid] = sst;
   };
   if (kv_beg < kv_end) {
     load_tile(kv_beg);
-    store_tile();
+    store_tile(smem);
   }
   __syncthreads();
-  for (int n0 = kv_beg; n0 < kv_end; n0 += BN) {
+  int cur = 0;
+  for (int n0 = kv_beg; n0 < kv_end; n0 += BN, cur ^= 1) {
     const bool has_next = n0 + BN < kv_end;
     if (has_next) load_tile(n0 + BN);
+    const char* Ks = smem + cur * BUF;
+    const char* Vs = Ks + KB;
+    const int* Ss = reinterpret_cast<const int*>(Vs + BN * G::KP);
     const bool need_mask = seg || (n0 + BN > S) || (a.causal && n0 + BN - 1 > qw) ||
                            (a.window >= 0 && n0 < qw + 31 - a.window) || qw + 31 >= S;
 #pragma unroll
@@ -370,28 +445,41 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
       }
 #pragma unroll
       for (int kk = 0; kk < G::NKK; ++kk) {
-        st = mfma32(lds_b128(Ks + (32 * t + r) * G::KP + (kk * 16 + hh * 8) * 2), qf[kk], st);
+        st = mfma32(KI::row_read(Ks, 32 * t + r, 2 * kk + hh), qf[kk], st);
         dpt = mfma32(lds_b128(Vs + (32 * t + r) * G::KP + (kk * 16 + hh * 8) * 2), df[kk], dpt);
       }
+      if (need_mask) {
+        const int lim = qrow - n0 - 32 * t - 4 * hh;
+        const int lo = qrow - a.window - n0 - 32 * t - 4 * hh;
+        const int hi = S - 1 - n0 - 32 * t - 4 * hh;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = exp2f(st[i] * sl2 - lse2);
-        if (need_mask) {
-          const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (!visible(qrow, kj, S, a.causal, a.window, seg, sq)) p = 0.f;
+        for (int c = 0; c < 4; ++c) {
+          int4 sk = make_int4(sq, sq, sq, sq);
+          if (seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * t + 8 * c + 4 * hh);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int i = 4 * c + j, ko = 8 * c + j;
+            bool ok = (ko <= hi) && (qrow < S);
+            if (a.causal) ok = ok && (ko <= lim);
+            if (a.window >= 0) ok = ok && (ko >= lo);
+            if (seg) ok = ok && ((&sk.x)[j] == sq);
+            const float p = ok ? fexp2(st[i] * sl2 - lse2) : 0.f;
+            st[i] = p * (dpt[i] - dlt);
+          }
         }
-        st[i] = p * (dpt[i] - dlt);  // dS^T
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) st[i] = fexp2(st[i] * sl2 - lse2) * (dpt[i] - dlt);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const bfv8 db = acc_as_b(st, s2);
 #pragma unroll
         for (int dt = 0; dt < G::NDT; ++dt)
-          dqt[dt] = mfma32(lds_trA(Kt, G::TP, 32 * t + 16 * s2, dt * 32, lane), db, dqt[dt]);
+          dqt[dt] = mfma32(KI::trA(Ks, BN, 32 * t + 16 * s2, dt * 32, lane), db, dqt[dt]);
       }
     }
-    __syncthreads();
-    if (has_next) store_tile();
+    if (has_next) store_tile(smem + (cur ^ 1) * BUF);
     __syncthreads();
   }
   if (qrow < S) {
@@ -409,32 +497,27 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward: dK, dV (key-parallel)
-// grid: (ceil(S/128), Hq, B); 4 waves x 32 keys; query tiles of 32 rows.
+// grid: (ceil(S/128), Hq, B); 4 waves x 32 keys; query tiles of 32 rows, double-buffered.
 // Hq == Hkv: writes bf16 dk/dv directly.  GQA: writes fp32 per-q-head partials, reduced afterwards.
 template <int D, bool GQA>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
   using G = FaGeom<D>;
+  using QI = Img<D>;
   constexpr int BM = 32;
   constexpr int NV = (BM * G::V8 + 255) / 256;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BM * G::KP + 2 * BM * G::TP + 2 * BM * 4];
-  char* Qs = smem;
-  char* Ds = smem + BM * G::KP;
-  char* Qt = smem + 2 * BM * G::KP;
-  char* Dt = Qt + BM * G::TP;
-  float* Ls = reinterpret_cast<float*>(Dt + BM * G::TP);
-  float* Dl = Ls + BM;
+  constexpr int IB = QI::bytes(BM);
+  constexpr int BUF = 2 * IB + 3 * BM * 4;  // Q image, dO image, lse*log2e, delta, segment ids
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, hh = lane >> 5;
-  const int nkb = (a.S + 127) / 128;
-  const int kb = (int)blockIdx.x;  // early key blocks see the most queries: launch them first
-  (void)nkb;
+  const int kb = (int)blockIdx.x;  // early key blocks see the most queries: launched first
   const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
   const int ks = kb * 128, kw = ks + wid * 32, kr = kw + r;
-  const bf16* qp = a.q + b * a.q_sb + h * a.q_sh;
-  const bf16* dop = a.dout + b * a.d_sb + h * a.d_sh;
-  const bf16* kp = a.k + b * a.k_sb + hk * a.k_sh;
-  const bf16* vp = a.v + b * a.v_sb + hk * a.v_sh;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(a.q + b * a.q_sb + h * a.q_sh, (int64_t)S * a.q_ss * 2);
+  const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.dout + b * a.d_sb + h * a.d_sh, (int64_t)S * a.d_ss * 2);
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + b * a.k_sb + hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + b * a.v_sb + hk * a.v_sh, (int64_t)S * a.v_ss * 2);
   const float* lsep = a.lse + ((int64_t)b * a.Hq + h) * S;
   const float* dlp = a.delta + ((int64_t)b * a.Hq + h) * S;
   const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
@@ -444,8 +527,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
   bfv8 kf[G::NKK], vf[G::NKK];
 #pragma unroll
   for (int kk = 0; kk < G::NKK; ++kk) {
-    kf[kk] = gload8(kp + (int64_t)kr * a.k_ss + kk * 16 + hh * 8, kr < S);
-    vf[kk] = gload8(vp + (int64_t)kr * a.v_ss + kk * 16 + hh * 8, kr < S);
+    kf[kk] = bload8(krs, (int)(kr * a.k_ss + kk * 16 + hh * 8) * 2);
+    vf[kk] = bload8(vrs, (int)(kr * a.v_ss + kk * 16 + hh * 8) * 2);
   }
   f32v16 dkt[G::NDT], dvt[G::NDT];
 #pragma unroll
@@ -462,44 +545,53 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
 
   bfv8 qst[NV], dst_[NV];
   float lst = 0.f, dls = 0.f;
+  int sst = 0;
   auto load_tile = [&](int q0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, qi = q0 + row;
-      const bool ok = (e < BM * G::V8) && qi < S;
-      qst[i] = gload8(qp + (int64_t)qi * a.q_ss + c8 * 8, ok);
-      dst_[i] = gload8(dop + (int64_t)qi * a.d_ss + c8 * 8, ok);
+      if (e < BM * G::V8) {
+        qst[i] = bload8(qrs, (int)(qi * a.q_ss + c8 * 8) * 2);
+        dst_[i] = bload8(drs, (int)(qi * a.d_ss + c8 * 8) * 2);
+      }
     }
     if (tid < BM) {
       const int qi = q0 + tid;
       lst = qi < S ? lsep[qi] * kLog2e : INFINITY;
       dls = qi < S ? dlp[qi] : 0.f;
+      if (seg) sst = qi < S ? seg[qi] : -1;
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](char* buf) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8;
       if (e < BM * G::V8) {
-        *reinterpret_cast<bfv8*>(Qs + row * G::KP + c8 * 16) = qst[i];
-        *reinterpret_cast<bfv8*>(Qt + row * G::TP + c8 * 16) = qst[i];
-        *reinterpret_cast<bfv8*>(Ds + row * G::KP + c8 * 16) = dst_[i];
-        *reinterpret_cast<bfv8*>(Dt + row * G::TP + c8 * 16) = dst_[i];
+        QI::store(buf, BM, row, c8, qst[i]);
+        QI::store(buf + IB, BM, row, c8, dst_[i]);
       }
     }
     if (tid < BM) {
-      Ls[tid] = lst;
-      Dl[tid] = dls;
+      float* L = reinterpret_cast<float*>(buf + 2 * IB);
+      L[tid] = lst;
+      L[BM + tid] = dls;
+      reinterpret_cast<int*>(L)[2 * BM + tid] = sst;
     }
   };
   if (q_beg < q_end) {
     load_tile(q_beg);
-    store_tile();
+    store_tile(smem);
   }
   __syncthreads();
-  for (int q0 = q_beg; q0 < q_end; q0 += BM) {
+  int cur = 0;
+  for (int q0 = q_beg; q0 < q_end; q0 += BM, cur ^= 1) {
     const bool has_next = q0 + BM < q_end;
     if (has_next) load_tile(q0 + BM);
+    const char* Qs = smem + cur * BUF;
+    const char* Ds = Qs + IB;
+    const float* Ls = reinterpret_cast<const float*>(Qs + 2 * IB);
+    const float* Dl = Ls + BM;
+    const int* Sg = reinterpret_cast<const int*>(Ls + 2 * BM);
     f32v16 sacc, dpacc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -508,26 +600,31 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
     }
 #pragma unroll
     for (int kk = 0; kk < G::NKK; ++kk) {
-      sacc = mfma32(lds_b128(Qs + r * G::KP + (kk * 16 + hh * 8) * 2), kf[kk], sacc);
-      dpacc = mfma32(lds_b128(Ds + r * G::KP + (kk * 16 + hh * 8) * 2), vf[kk], dpacc);
+      sacc = mfma32(QI::row_read(Qs, r, 2 * kk + hh), kf[kk], sacc);
+      dpacc = mfma32(QI::row_read(Ds, r, 2 * kk + hh), vf[kk], dpacc);
     }
     const bool need_mask = seg || (q0 + BM > S) || (kw + 31 >= S) || (a.causal && kw + 31 > q0) ||
                            (a.window >= 0 && q0 + BM - 1 > kw + a.window);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qloc = (i & 3) + 8 * (i >> 2) + 4 * hh;
-      float p = exp2f(sacc[i] * sl2 - Ls[qloc]);
-      if (need_mask) {
-        const int qi = q0 + qloc;
-        const int sqq = (seg && qi < S) ? seg[qi] : 0;
-        bool ok = kr < S && qi < S;
-        if (a.causal) ok = ok && (kr <= qi);
-        if (a.window >= 0) ok = ok && (kr >= qi - a.window);
-        if (seg) ok = ok && (sqq == sk);
-        if (!ok) p = 0.f;
+    for (int c = 0; c < 4; ++c) {
+      const float4 l4 = *reinterpret_cast<const float4*>(Ls + 8 * c + 4 * hh);
+      const float4 d4 = *reinterpret_cast<const float4*>(Dl + 8 * c + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * c + j;
+        const int qloc = 8 * c + 4 * hh + j;
+        float p = fexp2(sacc[i] * sl2 - (&l4.x)[j]);
+        if (need_mask) {
+          const int qi = q0 + qloc;
+          bool ok = kr < S && qi < S;
+          if (a.causal) ok = ok && (kr <= qi);
+          if (a.window >= 0) ok = ok && (kr >= qi - a.window);
+          if (seg) ok = ok && (Sg[qloc] == sk);
+          p = ok ? p : 0.f;
+        }
+        sacc[i] = p;                                 // P
+        dpacc[i] = p * (dpacc[i] - (&d4.x)[j]);      // dS
       }
-      sacc[i] = p;                           // P
-      dpacc[i] = p * (dpacc[i] - Dl[qloc]);  // dS
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -535,12 +632,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
       const bfv8 db = acc_as_b(dpacc, s2);
 #pragma unroll
       for (int dt = 0; dt < G::NDT; ++dt) {
-        dvt[dt] = mfma32(lds_trA(Dt, G::TP, 16 * s2, dt * 32, lane), pb, dvt[dt]);
-        dkt[dt] = mfma32(lds_trA(Qt, G::TP, 16 * s2, dt * 32, lane), db, dkt[dt]);
+        dvt[dt] = mfma32(QI::trA(Ds, BM, 16 * s2, dt * 32, lane), pb, dvt[dt]);
+        dkt[dt] = mfma32(QI::trA(Qs, BM, 16 * s2, dt * 32, lane), db, dkt[dt]);
       }
     }
-    __syncthreads();
-    if (has_next) store_tile();
+    if (has_next) store_tile(smem + (cur ^ 1) * BUF);
     __syncthreads();
   }
   if (kr < S) {
@@ -612,6 +708,9 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 
 using namespace llmt;
 
+// buffer-load offsets are 32-bit: every row of one (batch, head) slice must be addressable
+static bool fits32(int64_t S, int64_t row_stride) { return S * row_stride * 2 < 0x7fffffffLL; }
+
 static bool aligned16(const void* p, int64_t s0, int64_t s1, int64_t s2) {
   return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (s0 % 8 == 0) && (s1 % 8 == 0) && (s2 % 8 == 0);
 }
@@ -626,6 +725,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
       !aligned16(o, o_sb, o_ss, o_sh))
     return hipErrorInvalidValue;
   if (B == 0 || S == 0) return hipSuccess;
+  if (!fits32(S, q_ss) || !fits32(S, k_ss) || !fits32(S, v_ss)) return hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.out = (bf16*)o; a.lse = lse; a.seg = seg;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv;
@@ -656,6 +756,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       !aligned16(dk, dk_sb, dk_ss, dk_sh) || !aligned16(dv, dv_sb, dv_ss, dv_sh))
     return hipErrorInvalidValue;
   if (B == 0 || S == 0) return hipSuccess;
+  if (!fits32(S, q_ss) || !fits32(S, k_ss) || !fits32(S, v_ss) || !fits32(S, o_ss)) return hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (const bf16*)o;
   a.dout = (const bf16*)dout; a.out = (bf16*)dq; a.lse = (float*)lse; a.delta = delta; a.seg = seg;
