@@ -145,15 +145,25 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
 }
 
 // Column reduction of the per-block dW partials: out[j] (+)= sum_b part[b][j].
+// 256 threads = 64 columns x 4 row groups (coalesced 256-byte rows), LDS combine of the 4 groups.
 template <typename OutT>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, OutT* __restrict__ out,
                                                      int nparts, int H, int accumulate) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= H) return;
+  __shared__ float red[4][64];
+  const int cx = threadIdx.x & 63, gy = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cx;
   float s = 0.f;
-  for (int b = 0; b < nparts; ++b) s += part[(int64_t)b * H + j];
-  if (accumulate) s += (float)out[j];
-  out[j] = (OutT)s;
+  if (j < H) {
+#pragma unroll 4
+    for (int b = gy; b < nparts; b += 4) s += part[(int64_t)b * H + j];
+  }
+  red[gy][cx] = s;
+  __syncthreads();
+  if (gy == 0 && j < H) {
+    float t = red[0][cx] + red[1][cx] + red[2][cx] + red[3][cx];
+    if (accumulate) t += (float)out[j];
+    out[j] = (OutT)t;
+  }
 }
 
 }  // namespace llmt
@@ -203,8 +213,8 @@ extern "C" hipError_t llmt_rmsnorm_fwd(const void* x, const void* res, const voi
 
 // dw_part must hold nblocks*H floats where nblocks = llmt_rmsnorm_bwd_nblocks(T).
 extern "C" int llmt_rmsnorm_bwd_nblocks(int T) {
-  int nblk = (T + 15) / 16;  // >= 16 rows per block so partial traffic stays << activation traffic
-  if (nblk > 1024) nblk = 1024;
+  int nblk = (T + 31) / 32;  // >= 32 rows per block so partial traffic stays << activation traffic
+  if (nblk > 256) nblk = 256;
   if (nblk < 1) nblk = 1;
   return nblk;
 }
@@ -227,7 +237,7 @@ extern "C" hipError_t llmt_rmsnorm_bwd(const void* dy, const void* x, const void
     }
   }
   if (dw) {
-    const int g = (H + 255) / 256;
+    const int g = (H + 63) / 64;
     if (dw_is_fp32)
       colsum_kernel<float><<<g, 256, 0, stream>>>(dw_part, (float*)dw, T > 0 ? nblk : 0, H, accumulate);
     else

@@ -1,0 +1,253 @@
+"""Training callbacks with the reference's names and knobs.
+
+Reference: src/llm_training/lightning/callbacks/ — ModelCheckpoint (model_checkpoint.py:13-18, plus
+Lightning's every_n_train_steps / save_top_k / save_on_train_epoch_end), OutputRedirection
+(output_redirection.py:16-101), SaveConfigCallback (save_config_callback.py:14-49: resolved YAML +
+world size + SLURM env, config stored in every checkpoint), TQDMProgressBar (tqdm_progress.py:6-11),
+TrainingTimeEstimator (training_time_estimator.py:12-83), ExtraConfig (extra_config.py:27-45) and
+Lightning's LearningRateMonitor.
+"""
+from __future__ import annotations
+
+import io
+import json
+import logging
+import os
+import re
+import shutil
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+import yaml
+
+logger = logging.getLogger("llm_training")
+
+
+class Callback:
+    pass
+
+
+class LearningRateMonitor(Callback):
+    """The trainer logs ``lr`` every step already; this keeps YAML configs that list it valid."""
+
+    def __init__(self, logging_interval: str | None = "step", log_momentum: bool = False, **kw):
+        self.logging_interval = logging_interval
+
+
+class ModelCheckpoint(Callback):
+    def __init__(self, dirpath: str | None = None, filename: str | None = None, every_n_train_steps: int | None = None,
+                 save_on_train_epoch_end: bool | None = None, save_top_k: int = 1, save_last: bool | None = None,
+                 monitor: str | None = None, mode: str = "min", **kw):
+        self.dirpath = dirpath
+        self.filename = filename or "epoch={epoch}-step={step}"
+        self.every_n_train_steps = every_n_train_steps
+        self.save_on_train_epoch_end = save_on_train_epoch_end
+        self.save_top_k = save_top_k
+        self.save_last = save_last
+        self.monitor = monitor
+        self.mode = mode
+        self.saved: list[str] = []
+
+    def _dir(self, trainer) -> str:
+        # reference: <log_dir>/checkpoints when logging to a run directory (model_checkpoint.py:13-18)
+        return self.dirpath or os.path.join(trainer.log_dir, "checkpoints")
+
+    def _save(self, trainer):
+        if self.save_top_k == 0:
+            return
+        name = self.filename.format(epoch=trainer.state.epoch, step=trainer.global_step) + ".ckpt"
+        path = os.path.join(self._dir(trainer), name)
+        if path in self.saved:
+            return
+        trainer.save_checkpoint(path)
+        self.saved.append(path)
+        if self.save_top_k > 0 and self.monitor is None:
+            while len(self.saved) > self.save_top_k:
+                old = self.saved.pop(0)
+                if trainer.is_global_zero and os.path.exists(old):
+                    shutil.rmtree(old, ignore_errors=True)
+        if self.save_last and trainer.is_global_zero:
+            link = os.path.join(self._dir(trainer), "last.ckpt")
+            try:
+                if os.path.islink(link) or os.path.exists(link):
+                    os.remove(link)
+                os.symlink(os.path.basename(path), link)
+            except OSError:
+                pass
+
+    def on_train_batch_end(self, trainer, lm, outputs, batch, batch_idx):
+        n = self.every_n_train_steps
+        if n and trainer.global_step > 0 and trainer.global_step % n == 0:
+            self._save(trainer)
+
+    def on_train_epoch_end(self, trainer, lm):
+        if self.save_on_train_epoch_end or (self.save_on_train_epoch_end is None and not self.every_n_train_steps):
+            self._save(trainer)
+
+
+class SaveConfigCallback(Callback):
+    """Saves the resolved config (+ world size / SLURM env) and embeds it in every checkpoint."""
+
+    def __init__(self, config: dict | None = None, config_filename: str = "config.yaml", overwrite: bool = True):
+        self.config = config or {}
+        self.config_filename = config_filename
+        self.overwrite = overwrite
+
+    def setup(self, trainer, lm, stage):
+        cfg = dict(self.config)
+        cfg["world_size"] = trainer.world_size if trainer.pc else int(os.environ.get("WORLD_SIZE", 1))
+        slurm = {k: v for k, v in os.environ.items() if k.startswith("SLURM_")}
+        if slurm:
+            cfg["slurm"] = slurm
+        trainer.config_dict = cfg
+        if trainer.is_global_zero:
+            os.makedirs(trainer.log_dir, exist_ok=True)
+            p = os.path.join(trainer.log_dir, self.config_filename)
+            if self.overwrite or not os.path.exists(p):
+                with open(p, "w") as f:
+                    yaml.safe_dump(_plain(cfg), f, sort_keys=False)
+
+
+def _plain(x):
+    if isinstance(x, dict):
+        return {str(k): _plain(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_plain(v) for v in x]
+    if isinstance(x, (str, int, float, bool)) or x is None:
+        return x
+    return str(x)
+
+
+class _Tee(io.TextIOBase):
+    def __init__(self, stream, buf):
+        self.stream, self.buf = stream, buf
+
+    def write(self, s):
+        self.stream.write(s)
+        self.buf.write(s)
+        return len(s)
+
+    def flush(self):
+        self.stream.flush()
+        self.buf.flush()
+
+
+class OutputRedirection(Callback):
+    """Tee stdout/stderr into ``<log_dir>/<log_file_name>.log`` (file name agreed from rank 0)."""
+
+    def __init__(self, log_file_name: str = "{index}-{version}", redirect_stdout: bool = True,
+                 redirect_stderr: bool = True, enabled: bool = True):
+        self.log_file_name, self.redirect_stdout, self.redirect_stderr, self.enabled = \
+            log_file_name, redirect_stdout, redirect_stderr, enabled
+        self._f = None
+        self._orig = (sys.stdout, sys.stderr)
+
+    def setup(self, trainer, lm, stage):
+        if not self.enabled:
+            return
+        d = trainer.log_dir
+        name = [None]
+        if trainer.is_global_zero:
+            os.makedirs(d, exist_ok=True)
+            idx = len([p for p in os.listdir(d) if p.endswith(".log")])
+            name[0] = self.log_file_name.format(index=idx, version=time.strftime("%Y%m%d-%H%M%S"))
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.broadcast_object_list(name, src=0)
+        rank = trainer.pc.rank if trainer.pc else 0
+        fname = os.path.join(d, name[0] + (f".rank{rank}" if rank else "") + ".log")
+        os.makedirs(d, exist_ok=True)
+        self._f = open(fname, "a", buffering=1)
+        if self.redirect_stdout:
+            sys.stdout = _Tee(self._orig[0], self._f)
+        if self.redirect_stderr:
+            sys.stderr = _Tee(self._orig[1], self._f)
+        for h in logging.getLogger("llm_training").handlers:
+            if isinstance(h, logging.StreamHandler) and not isinstance(h, logging.FileHandler):
+                h.setStream(sys.stderr)
+
+    def on_fit_end(self, trainer, lm):
+        if self._f:
+            sys.stdout, sys.stderr = self._orig
+            self._f.close()
+            self._f = None
+
+
+class TQDMProgressBar(Callback):
+    def __init__(self, refresh_rate: int = 1, **kw):
+        self.refresh_rate = refresh_rate
+        self.bar = None
+
+    def on_fit_start(self, trainer, lm):
+        if not trainer.is_global_zero:
+            return
+        try:
+            from tqdm.auto import tqdm
+        except ImportError:
+            return
+        total = trainer.estimated_stepping_batches()
+        # restarts begin at the resumed step (reference tqdm_progress.py:6-11)
+        self.bar = tqdm(total=total, initial=trainer.global_step, dynamic_ncols=True)
+
+    def on_train_batch_end(self, trainer, lm, outputs, batch, batch_idx):
+        if self.bar is not None:
+            self.bar.update(1)
+            if trainer.last_metrics:
+                loss = trainer.last_metrics.get("Loss/Train/Step")
+                if loss is not None:
+                    self.bar.set_postfix(loss=f"{loss:.4f}")
+
+    def on_fit_end(self, trainer, lm):
+        if self.bar is not None:
+            self.bar.close()
+
+
+class TrainingTimeEstimator(Callback):
+    """Time steps [num_warmup_steps, num_test_steps), stop, print steps/s, tokens/s and ETA."""
+
+    def __init__(self, num_test_steps: int, num_warmup_steps: int = 2, enable_checkpointing: bool = False):
+        self.num_test_steps, self.num_warmup_steps = num_test_steps, num_warmup_steps
+        self.enable_checkpointing = enable_checkpointing
+        self.t0 = None
+        self.result: dict | None = None
+
+    def setup(self, trainer, lm, stage):
+        if not self.enable_checkpointing:
+            trainer.callbacks = [c for c in trainer.callbacks if not isinstance(c, ModelCheckpoint)]
+
+    def on_train_batch_end(self, trainer, lm, outputs, batch, batch_idx):
+        step = trainer.global_step
+        if step == self.num_warmup_steps:
+            if trainer.device.type == "cuda":
+                torch.cuda.synchronize()
+            self.t0 = time.perf_counter()
+            self.tok0 = trainer.state.consumed.get("Consumed Tokens", 0)
+        if step == self.num_test_steps:
+            if trainer.device.type == "cuda":
+                torch.cuda.synchronize()
+            el = time.perf_counter() - self.t0
+            n = self.num_test_steps - self.num_warmup_steps
+            total = trainer.estimated_stepping_batches()
+            sps = n / el
+            self.result = {"steps_per_sec": sps, "sec_per_step": el / n,
+                           "eta_hours": (total - step) / sps / 3600, "total_steps": total}
+            if trainer.is_global_zero:
+                logger.info("TrainingTimeEstimator: %s", json.dumps(self.result))
+            trainer.should_stop = True
+
+
+class ExtraConfig(Callback):
+    """``float32_matmul_precision`` and ``logging_level`` (reference extra_config.py:27-38)."""
+
+    def __init__(self, float32_matmul_precision: str | None = None, logging_level: str | int = "INFO"):
+        self.fp32 = float32_matmul_precision
+        self.level = logging_level
+        self.apply()
+
+    def apply(self):
+        if self.fp32:
+            torch.set_float32_matmul_precision(self.fp32)
+        lvl = self.level if isinstance(self.level, int) else getattr(logging, str(self.level).upper(), logging.INFO)
+        logging.getLogger("llm_training").setLevel(lvl)
