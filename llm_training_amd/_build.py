@@ -73,13 +73,15 @@ def build(verbose: bool = False, debug: bool = False) -> Path:
         if _stale(obj, [src, *headers]):
             jobs.append([_hipcc(), f"--offload-arch={ARCH}", *opt, "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
                          f"-I{CSRC}", "-c", str(src), "-o", str(obj)])
-    bsrc = CSRC / "bindings.cpp"
-    bobj = BUILD / "bindings.o"
-    objs.append(bobj)
-    if _stale(bobj, [bsrc, *headers]):
-        jobs.append([_clangxx(), "-x", "c++", *opt, "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-                     f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *[f"-I{p}" for p in inc], f"-I{ROCM / 'include'}",
-                     f"-I{sysconfig.get_paths()['include']}", "-c", str(bsrc), "-o", str(bobj)])
+    # host-only C++ (torch op registrations, CPU data-pipeline code): compiled without device passes
+    for bsrc in sorted(CSRC.glob("*.cpp")):
+        bobj = BUILD / (bsrc.stem + ".o")
+        objs.append(bobj)
+        if _stale(bobj, [bsrc, *headers]):
+            jobs.append([_clangxx(), "-x", "c++", *opt, "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1",
+                         "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", *[f"-I{p}" for p in inc],
+                         f"-I{ROCM / 'include'}", f"-I{sysconfig.get_paths()['include']}", "-c", str(bsrc), "-o",
+                         str(bobj)])
     if jobs:
         workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8")))
         with cf.ThreadPoolExecutor(workers) as ex:

@@ -114,8 +114,8 @@ class BaseDataModule:
             ds = self.load_pre_processed_data(self.config.pre_processed_data_path)
         else:
             ds = self.pre_process_data(self.load_data())
-        ds = self.post_process_data(ds)
-        self.datasets = self.split(ds)
+        self.pre_processed_datasets = ds
+        self.datasets = self.post_process_data(self.split(ds))
 
     def split(self, ds):
         if isinstance(ds, dict):
