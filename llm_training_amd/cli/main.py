@@ -126,7 +126,8 @@ def main(argv: list[str] | None = None):
     if not argv or argv[0] in ("-h", "--help") or argv[0] not in COMMANDS:
         print("usage: llm-training {fit,validate,convert-to-hf,pre-process} [--config cfg.yaml] [--a.b.c value ...]")
         return 0 if argv and argv[0] in ("-h", "--help") else 2
-    return COMMANDS[argv[0]](argv[1:])
+    r = COMMANDS[argv[0]](argv[1:])
+    return r if isinstance(r, int) else 0
 
 
 if __name__ == "__main__":

@@ -1,0 +1,153 @@
+"""Wrapper for any Hugging Face ``AutoModelForCausalLM`` (e.g. the GPT-2 small CPU plumbing config).
+
+Reference: src/llm_training/models/hf_causal_lm/hf_causal_lm.py (packed-mask patch :19-20, HF gradient
+checkpointing :37-38, optional Liger patch :42-43, FSDP units by ``_no_split_modules`` plus
+leftovers :88-114; no TP) and hf_causal_lm_config.py:8-17.
+
+The model body runs through transformers (its own attention: eager / sdpa); the loss heads use our
+fused lm_head + cross-entropy on the final hidden states, and the ZeRO engine shards the HF model
+by its ``_no_split_modules`` blocks. ``hf_config`` builds a random-init model from a config dict
+(no checkpoint needed); ``hf_path`` loads a LOCAL checkpoint.
+"""
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+import torch.nn as nn
+
+from ..parallel.context import ParallelContext
+from .base import BaseModel, BaseModelConfig, CausalLMOutput
+
+
+class HFCausalLMConfig(BaseModelConfig):
+    hf_config: dict[str, Any] | None = None
+    enable_gradient_checkpointing: bool = False
+    enable_liger_kernel: bool = False  # accepted for parity; the fused loss head is always used
+    loss_chunk_size: int = 8192
+
+
+class HFCausalLM(BaseModel):
+    config_class = HFCausalLMConfig
+    writes_main_grad = False  # transformers modules produce ordinary .grad tensors
+
+    def __init__(self, config: HFCausalLMConfig, pc: ParallelContext | None = None, dtype=None, device=None):
+        super().__init__(config, pc)
+        if self.pc.tp:
+            raise NotImplementedError("HFCausalLM does not support tensor parallelism (as in the reference)")
+        from transformers import AutoConfig, AutoModelForCausalLM
+
+        if config.hf_config is not None:
+            d = dict(config.hf_config)
+            mt = d.pop("model_type")
+            hf_cfg = AutoConfig.for_model(mt, **d)
+        elif config.hf_path:
+            hf_cfg = AutoConfig.from_pretrained(config.hf_path, local_files_only=True,
+                                                trust_remote_code=config.trust_remote_code)
+        else:
+            raise ValueError("HFCausalLM needs `hf_config` or a local `hf_path`")
+        impl = config.attn_implementation
+        if impl in (None, "flash_attention_2", "flash", "hip"):
+            impl = "sdpa"
+        hf_cfg._attn_implementation = impl
+        if dtype is None:
+            dtype = config.torch_dtype if isinstance(config.torch_dtype, torch.dtype) else torch.float32
+        self.hf_model = AutoModelForCausalLM.from_config(hf_cfg, torch_dtype=dtype)
+        if device is not None:
+            self.hf_model.to(device)
+        if config.enable_gradient_checkpointing:
+            self.hf_model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+
+    @property
+    def hf_config(self):
+        return self.hf_model.config
+
+    def init_weights(self, seed: int = 0):
+        torch.manual_seed(seed)
+        self.hf_model.apply(self.hf_model._init_weights)
+        if getattr(self.hf_model.config, "tie_word_embeddings", False):
+            self.hf_model.tie_weights()
+
+    def lm_head_weight(self):
+        return self.hf_model.get_output_embeddings().weight
+
+    def get_input_embeddings(self):
+        return self.hf_model.get_input_embeddings()
+
+    def get_output_embeddings(self):
+        return self.hf_model.get_output_embeddings()
+
+    def fsdp_units(self):
+        names = set(getattr(self.hf_model, "_no_split_modules", None) or [])
+        units, seen = [], set()
+        for m in self.hf_model.modules():
+            if type(m).__name__ in names:
+                units.append(m)
+                seen.update(id(p) for p in m.parameters())
+        rest = [p for p in self.hf_model.parameters() if id(p) not in seen]
+        if rest:  # one more unit for the leftovers (embeddings, final norm, lm_head)
+            units.insert(0, _ParamsUnit(rest))
+        return units or [self.hf_model]
+
+    @staticmethod
+    def _hf_mask(segment_ids, B, S, dtype, device):
+        """2-D padding mask when the ids are 0/1, else a 4-D block-diagonal causal mask (packed rows)."""
+        if segment_ids is None:
+            return None
+        seg = segment_ids.to(device)
+        if bool((seg <= 1).all()):
+            return seg.long()
+        i = torch.arange(S, device=device)
+        vis = (i[None, :] <= i[:, None])[None] & (seg[:, :, None] == seg[:, None, :])
+        m = torch.zeros(B, 1, S, S, dtype=dtype, device=device)
+        return m.masked_fill(~vis[:, None], torch.finfo(dtype).min)
+
+    def hidden_states(self, input_ids=None, position_ids=None, segment_ids=None, inputs_embeds=None,
+                      gather_sequence: bool = True, embed_hook=None):
+        if input_ids is not None:
+            B, S = input_ids.shape
+            dev = input_ids.device
+        else:
+            B, S = inputs_embeds.shape[:2]
+            dev = inputs_embeds.device
+        if embed_hook is not None:
+            emb = self.get_input_embeddings()(input_ids) if inputs_embeds is None else inputs_embeds
+            inputs_embeds = embed_hook(emb.transpose(0, 1)).transpose(0, 1)
+            input_ids = None
+        mask = self._hf_mask(segment_ids, B, S, next(self.parameters()).dtype, dev)
+        out = self.hf_model(input_ids=input_ids, inputs_embeds=inputs_embeds, attention_mask=mask,
+                            position_ids=position_ids, output_hidden_states=True, use_cache=False)
+        return out.hidden_states[-1].transpose(0, 1)
+
+    def forward(self, input_ids=None, attention_mask=None, position_ids=None, inputs_embeds=None,
+                return_last_hidden_states: bool = False, segment_ids=None):
+        h = self.hidden_states(input_ids, position_ids, segment_ids if segment_ids is not None else attention_mask,
+                               inputs_embeds)
+        logits = torch.nn.functional.linear(h, self.lm_head_weight()).transpose(0, 1)
+        return CausalLMOutput(logits=logits, last_hidden_states=h.transpose(0, 1) if return_last_hidden_states
+                              else None)
+
+    @classmethod
+    def convert_state_dict_from_hf(cls, sd, config):
+        return {"hf_model." + k: v for k, v in sd.items()}
+
+    @classmethod
+    def convert_state_dict_to_hf(cls, sd, config):
+        return {k[len("hf_model."):]: v for k, v in sd.items() if k.startswith("hf_model.")}
+
+    def hf_config_dict(self) -> dict:
+        return self.hf_model.config.to_dict()
+
+    def _tp_rule(self, key):
+        return "rep", None
+
+
+class _ParamsUnit(nn.Module):
+    """Parameter container used as an engine unit (no forward hooks fire on it)."""
+
+    def __init__(self, params):
+        super().__init__()
+        self._plist = list(params)
+
+    def parameters(self, recurse: bool = True):
+        return iter(self._plist)

@@ -96,6 +96,9 @@ class DataParallelEngine:
         self.cuda = dev.type == "cuda"
         self.native = self.cuda and use_native(torch.empty(0, device=dev))
         self.comm_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.overlap) else None
+        # models built from our fused ops write weight grads straight into the flat buffers; others
+        # (transformers modules) leave ordinary .grad tensors that are absorbed after backward
+        self.autograd_grads = not getattr(model, "writes_main_grad", True)
         self.param_dtype = next(model.parameters()).dtype
         self.grad_dtype = grad_dtype or self.param_dtype
         self.reduce_dtype = reduce_dtype or self.grad_dtype
@@ -201,7 +204,7 @@ class DataParallelEngine:
             elif u.ag_event is not None:
                 torch.cuda.current_stream().wait_event(u.ag_event)
                 u.ag_event = None
-            if torch.is_grad_enabled() and (self.dp > 1 or self.pc.tp):
+            if torch.is_grad_enabled() and (self.dp > 1 or self.pc.tp) and not self.autograd_grads:
                 for a in args:
                     if isinstance(a, torch.Tensor) and a.requires_grad:
                         a.register_hook(self._make_grad_ready(u))
@@ -319,6 +322,14 @@ class DataParallelEngine:
         """Called after the last micro-batch's backward: reduce units whose hook did not fire."""
         for u in self.units:
             if not u.reduced:
+                for p in u.params:
+                    if p.grad is not None:  # autograd-produced gradient (non-fused modules)
+                        if p.grad_added:
+                            p.main_grad.add_(p.grad.view_as(p.main_grad))
+                        else:
+                            p.main_grad.copy_(p.grad.view_as(p.main_grad))
+                        p.grad_added = True
+                        p.grad = None
                 # params that received no gradient this step contribute zeros
                 for p in u.params:
                     if not p.grad_added:

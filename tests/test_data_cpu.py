@@ -1,0 +1,177 @@
+"""Data pipeline: packers (vs the reference algorithms), collators, pre-training / instruction / preference
+modules on local files, resumable sampler."""
+import json
+import random
+
+import pytest
+import torch
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from llm_training_amd.data.packing import bfd_assign, group_by_length
+from llm_training_amd.data.pre_training import (PreTrainingDataCollator, PreTrainingDataModule,
+                                                PreTrainingDataModuleConfig, bfd_pack_batch, naive_pack_batch,
+                                                truncate_batch)
+from llm_training_amd.data.base import ResumableDistributedSampler
+from tests.helpers import toy_tokenizer
+
+
+def ref_best_fit(capacity, lengths):
+    """The reference's O(n*bins) best fit (pre_training_datamodule.py:156-179)."""
+    bins, contents = [], []
+    for i, n in enumerate(lengths):
+        best, space = -1, float("inf")
+        for j in range(len(bins)):
+            if bins[j] >= n and bins[j] - n < space:
+                best, space = j, bins[j] - n
+        if best != -1:
+            bins[best] -= n
+            contents[best].append(i)
+        else:
+            bins.append(capacity - n)
+            contents.append([i])
+    return contents
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.integers(1, 64), min_size=1, max_size=200))
+def test_bfd_matches_reference(lengths):
+    lengths = sorted(lengths, reverse=True)
+    bins = bfd_assign(lengths, 64)
+    groups = {}
+    for i, b in enumerate(bins):
+        groups.setdefault(b, []).append(i)
+    assert [groups[k] for k in sorted(groups)] == ref_best_fit(64, lengths)
+    for g in groups.values():
+        assert sum(lengths[i] for i in g) <= 64
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.integers(1, 50), min_size=1, max_size=200))
+def test_group_by_length_matches_reference(lengths):
+    groups, cur, s = [], [], 0
+    for i, n in sorted(enumerate(lengths), key=lambda x: x[1]):
+        if s + n + len(cur) <= 64:
+            cur.append(i)
+            s += n
+        else:
+            groups.append(cur)
+            cur, s = [i], n
+    if cur:
+        groups.append(cur)
+    assert group_by_length(lengths, 64) == groups
+
+
+def test_naive_packing_and_truncate():
+    b = {"source": ["a"] * 3, "input_ids": [[1] * 5, [2] * 7, [3] * 4], "length": [5, 7, 4]}
+    t = truncate_batch(b, 6, 6)
+    assert t["length"] == [5, 6, 1, 4]
+    p = naive_pack_batch(t, 6)
+    assert all(len(x) <= 6 for x in p["input_ids"])
+    assert sum(p["length"]) == 16
+    assert p["attention_mask"][0][0] == 1
+    bp = bfd_pack_batch(t, 6)
+    assert sorted(sum(bp["input_ids"], [])) == sorted(sum(t["input_ids"], []))
+
+
+def test_pretraining_collator_semantics():
+    tok = toy_tokenizer()
+    tok.padding_side = "right"
+    cfg = PreTrainingDataModuleConfig(tokenizer=tok, max_length=8, pad_to_multiple_of=4)
+    col = PreTrainingDataCollator(cfg)
+    out = col([{"input_ids": [tok.bos_token_id, 10, 11, tok.eos_token_id], "attention_mask": [1, 1, 2, 2]},
+               {"input_ids": [tok.bos_token_id, 12], "attention_mask": [1, 1]}])
+    # +1 padding rule: n = (4 // 4 + 1) * 4 = 8
+    assert out["input_ids"].shape == (2, 8)
+    assert out["labels"][0, 0] == -100 and out["labels"][0, 1] == 10
+    assert (out["labels"][1, 2:] == -100).all()
+    assert out["attention_mask"][0].tolist() == [1, 1, 1, 1, 0, 0, 0, 0]  # segment ids discarded (parity)
+    cfg2 = PreTrainingDataModuleConfig(tokenizer=tok, max_length=8, isolate_documents=True, reset_position_ids=True)
+    out2 = PreTrainingDataCollator(cfg2)([{"input_ids": [1, 2, 3, 4], "attention_mask": [1, 1, 2, 2]}])
+    assert out2["attention_mask"][0].tolist() == [1, 1, 2, 2]
+    assert out2["position_ids"][0].tolist() == [0, 1, 0, 1]
+
+
+@pytest.mark.parametrize("method", ["naive_packing", "best_fit_bin_packing", "no_packing"])
+def test_pretraining_module_on_local_json(tmp_path, method):
+    rng = random.Random(0)
+    words = "hello world how are you the a of to and is it in that good bad yes no".split()
+    rows = [{"text": " ".join(rng.choice(words) for _ in range(rng.randint(3, 30))), "source": rng.choice("xy")}
+            for _ in range(60)]
+    f = tmp_path / "d.jsonl"
+    f.write_text("\n".join(json.dumps(r) for r in rows))
+    tok = toy_tokenizer()
+    dm = PreTrainingDataModule({"dataset_kwargs": {"path": "json", "data_files": str(f)}, "tokenizer": tok,
+                                "max_length": 32, "packing_method": method, "batch_size": 2,
+                                "validation_split": 0.1, "sample_rate": {"x": 2.0}, "enable_cache": False})
+    dm.setup()
+    assert "train" in dm.datasets and "validation" in dm.datasets
+    for r in dm.datasets["train"]:
+        assert len(r["input_ids"]) <= 32
+    b = next(iter(dm.train_dataloader()))
+    assert b["input_ids"].shape[0] == 2 and b["labels"].shape == b["input_ids"].shape
+    table = dm.tokens_table(dm.datasets)
+    assert "Tokens" in table
+
+
+def test_instruction_tuning_module(tmp_path):
+    from llm_training_amd.data.instruction_tuning import InstructionTuningDataModule
+    rows = [{"messages": [{"role": "user", "content": "hello world " * (i % 5 + 1)},
+                          {"role": "assistant", "content": "fine thanks " * (i % 3 + 1)}]} for i in range(20)]
+    f = tmp_path / "it.jsonl"
+    f.write_text("\n".join(json.dumps(r) for r in rows))
+    tok = toy_tokenizer()
+    dm = InstructionTuningDataModule({"dataset_kwargs": {"path": "json", "data_files": str(f)}, "tokenizer": tok,
+                                      "chat_template": "chatml", "max_length": 40,
+                                      "packing_method": "group_by_length", "overlong_handling_method": "truncate",
+                                      "batch_size": 2, "pad_to_multiple_of": 8, "enable_cache": False})
+    dm.setup()
+    b = next(iter(dm.train_dataloader()))
+    ids, lab, seg = b["input_ids"], b["labels"], b["attention_mask"]
+    assert ids.shape[1] % 8 == 0
+    assert seg.max() >= 2  # packed rows carry segment ids
+    assistant = tok.convert_tokens_to_ids("assistant")
+    fine = tok.convert_tokens_to_ids("fine")
+    valid = lab != -100
+    assert (lab[valid] != assistant).all()
+    assert (ids[valid] == lab[valid]).all() and (lab == fine).any()
+
+
+def test_preference_module(tmp_path):
+    from llm_training_amd.data.preference_tuning import PreferenceTuningDataModule
+    rows = [{"chosen": [{"role": "user", "content": "question"}, {"role": "assistant", "content": "good answer"}],
+             "rejected": [{"role": "user", "content": "question"}, {"role": "assistant", "content": "bad"}]}
+            for _ in range(6)]
+    f = tmp_path / "p.jsonl"
+    f.write_text("\n".join(json.dumps(r) for r in rows))
+    dm = PreferenceTuningDataModule({"dataset_kwargs": {"path": "json", "data_files": str(f)},
+                                     "tokenizer": toy_tokenizer(), "chat_template": "chatml", "batch_size": 2,
+                                     "enable_cache": False})
+    dm.setup()
+    b = next(iter(dm.train_dataloader()))
+    for k in ("chosen_input_ids", "rejected_input_ids", "chosen_labels", "rejected_labels",
+              "chosen_attention_mask", "chosen_position_ids"):
+        assert k in b
+    assert (b["chosen_labels"] != -100).sum() > (b["rejected_labels"] != -100).sum()
+
+
+def test_resumable_sampler_skip():
+    s = ResumableDistributedSampler(40, 4, dp_rank=1, dp_size=2, seed=3)
+    full = list(s)
+    s2 = ResumableDistributedSampler(40, 4, dp_rank=1, dp_size=2, seed=3)
+    s2.set_skip(2)
+    assert list(s2) == full[2:]
+    other = list(ResumableDistributedSampler(40, 4, dp_rank=0, dp_size=2, seed=3))
+    assert not set(sum(full, [])) & set(sum(other, []))
+
+
+def test_chat_templates_all_render():
+    from llm_training_amd.data.chat_templates import NAMES, get_chat_template
+    tok = toy_tokenizer()
+    msgs = [{"role": "system", "content": "fine"}, {"role": "user", "content": "hello"},
+            {"role": "assistant", "content": "good answer"}]
+    assert len(NAMES) == 9
+    for n in NAMES:
+        enc = tok.apply_chat_template([msgs], chat_template=get_chat_template(n), return_dict=True, tokenize=True,
+                                      return_assistant_tokens_mask=True)
+        assert sum(enc["assistant_masks"][0]) >= 2, n

@@ -1,0 +1,186 @@
+"""Model parity on CPU: our Llama / Phi-3 vs transformers' implementations with the same weights
+(through the HF key conversion), RoPE tables vs transformers, HFCausalLM (GPT-2), DPO / ORPO heads."""
+import math
+
+import pytest
+import torch
+
+from llm_training_amd.models.llama import Llama, LlamaConfig
+from llm_training_amd.ops.rope_utils import compute_rope_tables
+from tests.helpers import tiny_llama_cfg
+
+
+def _ours_logits(model, ids):
+    model.eval()
+    with torch.no_grad():
+        return model(input_ids=ids).logits
+
+
+def test_llama_matches_transformers():
+    from transformers import LlamaConfig as HFC, LlamaForCausalLM
+
+    cfg = tiny_llama_cfg(rope_theta=500000.0, rope_scaling={"rope_type": "llama3", "factor": 8.0,
+                                                             "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                                             "original_max_position_embeddings": 64})
+    ours = Llama(cfg, dtype=torch.float32)
+    ours.init_weights(3)
+    hf = LlamaForCausalLM(HFC(**ours.hf_config_dict()))
+    hf.load_state_dict(Llama.convert_state_dict_to_hf(ours.state_dict(), cfg))
+    ids = torch.randint(0, cfg.vocab_size, (2, 100))
+    a = _ours_logits(ours, ids)
+    hf.eval()
+    with torch.no_grad():
+        b = hf(input_ids=ids).logits
+    assert torch.allclose(a, b, atol=2e-4, rtol=1e-3), (a - b).abs().max()
+    # round trip of the key conversion
+    back = Llama.convert_state_dict_from_hf(hf.state_dict(), cfg)
+    for k, v in ours.state_dict().items():
+        assert torch.equal(back[k], v), k
+
+
+def test_phi3_matches_transformers():
+    from transformers import Phi3Config as HFC, Phi3ForCausalLM
+
+    from llm_training_amd.models.phi3 import Phi3, Phi3Config
+
+    half = 8
+    cfg = Phi3Config(vocab_size=128, hidden_size=64, intermediate_size=96, num_hidden_layers=2,
+                     num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=512,
+                     original_max_position_embeddings=64,
+                     rope_scaling={"type": "longrope", "short_factor": [1.0 + 0.1 * i for i in range(half)],
+                                   "long_factor": [1.5 + 0.2 * i for i in range(half)]}, pad_token_id=0)
+    ours = Phi3(cfg, dtype=torch.float32)
+    ours.init_weights(5)
+    hf_cfg = dict(ours.hf_config_dict())
+    hf = Phi3ForCausalLM(HFC(**hf_cfg))
+    hf.load_state_dict(Phi3.convert_state_dict_to_hf(ours.state_dict(), cfg))
+    hf.eval()
+    for S in (40, 100):  # short factors (<= 64) and long factors (> 64)
+        ids = torch.randint(1, cfg.vocab_size, (1, S))
+        a = _ours_logits(ours, ids)
+        with torch.no_grad():
+            b = hf(input_ids=ids).logits
+        assert torch.allclose(a, b, atol=3e-4, rtol=1e-3), (S, (a - b).abs().max())
+
+
+def test_rope_tables_match_transformers_default():
+    from transformers.modeling_rope_utils import ROPE_INIT_FUNCTIONS  # noqa: F401
+    cos, sin = compute_rope_tables(128, 64, 10000.0)
+    inv = 1.0 / (10000.0 ** (torch.arange(0, 128, 2).double() / 128))
+    f = torch.outer(torch.arange(64).double(), inv)
+    assert torch.allclose(cos, f.cos().float()) and torch.allclose(sin, f.sin().float())
+
+
+def test_gpt2_hf_causal_lm_trains_cpu():
+    from llm_training_amd.lms.clm import CLM
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+
+    cfg = HFCausalLMConfig(hf_config={"model_type": "gpt2", "n_layer": 2, "n_head": 2, "n_embd": 32,
+                                      "vocab_size": 100, "n_positions": 64})
+    m = HFCausalLM(cfg)
+    m.init_weights(0)
+    eng = DataParallelEngine(m, ParallelContext.single(), 2, lr=1e-2)
+    lm = CLM({"model": None})
+    lm.model = m
+    ids = torch.randint(0, 100, (2, 32))
+    losses = []
+    for _ in range(6):
+        eng.begin_step(1)
+        eng.zero_grad()
+        loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+        loss.backward()
+        eng.finish_backward()
+        eng.clip_and_scale(1.0)
+        eng.step(1e-2)
+        losses.append(loss.item())
+    assert losses[-1] < losses[0] - 0.3, losses
+
+
+def test_engine_grads_match_autograd_reference():
+    """Flat-buffer main-grad path == plain autograd on an identical copy."""
+    import copy
+
+    from llm_training_amd.lms.clm import CLM
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+
+    cfg = tiny_llama_cfg()
+    a = Llama(cfg, dtype=torch.float32)
+    a.init_weights(1)
+    b = copy.deepcopy(a)
+    ids = torch.randint(0, cfg.vocab_size, (2, 24))
+    lm = CLM({"model": None})
+    lm.model = b
+    loss_b, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+    loss_b.backward()
+    eng = DataParallelEngine(a, ParallelContext.single(), 0)
+    lm.model = a
+    eng.begin_step(1)
+    eng.zero_grad()
+    loss_a, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+    loss_a.backward()
+    eng.finish_backward()
+    pb = dict(b.named_parameters())
+    for n, p in a.named_parameters():
+        assert torch.allclose(p.main_grad, pb[n].grad, atol=1e-5, rtol=1e-4), n
+    assert abs(loss_a.item() - loss_b.item()) < 1e-6
+
+
+def _pref_batch(V, B=2, S=12):
+    g = torch.Generator().manual_seed(0)
+    c = torch.randint(1, V, (B, S), generator=g)
+    r = torch.randint(1, V, (B, S - 3), generator=g)
+    cl, rl = c.clone(), r.clone()
+    cl[:, :4] = -100
+    rl[:, :4] = -100
+    return {"chosen_input_ids": c, "chosen_labels": cl, "chosen_attention_mask": torch.ones_like(c),
+            "chosen_position_ids": torch.arange(S)[None], "rejected_input_ids": r, "rejected_labels": rl,
+            "rejected_attention_mask": torch.ones_like(r), "rejected_position_ids": torch.arange(S - 3)[None]}
+
+
+def _seq_logps(model, ids, labels):
+    from llm_training_amd.ops.reference import shift_labels, token_logps
+    lab = shift_labels(labels)
+    with torch.no_grad():
+        lg = model(input_ids=ids).logits
+    lp = token_logps(lg, lab)
+    return lp.sum(-1), (lab != -100).sum(-1)
+
+
+def test_dpo_loss_matches_formula():
+    from llm_training_amd.lms.preference import DPO
+    cfg = tiny_llama_cfg()
+    dpo = DPO({"model": None, "beta": 0.2})
+    dpo.model = Llama(cfg, dtype=torch.float32)
+    dpo.model.init_weights(1)
+    dpo.ref_model = Llama(cfg, dtype=torch.float32)
+    dpo.ref_model.init_weights(2)
+    batch = _pref_batch(cfg.vocab_size)
+    loss, m, _ = dpo.training_step(batch)
+    pc, _ = _seq_logps(dpo.model, batch["chosen_input_ids"], batch["chosen_labels"])
+    pr, _ = _seq_logps(dpo.model, batch["rejected_input_ids"], batch["rejected_labels"])
+    rc, _ = _seq_logps(dpo.ref_model, batch["chosen_input_ids"], batch["chosen_labels"])
+    rr, _ = _seq_logps(dpo.ref_model, batch["rejected_input_ids"], batch["rejected_labels"])
+    exp = -torch.nn.functional.logsigmoid(0.2 * ((pc - pr) - (rc - rr))).mean()
+    assert abs(loss.item() - exp.item()) < 1e-4
+    loss.backward()
+    assert all(p.grad is not None for p in dpo.model.parameters())
+
+
+def test_orpo_loss_matches_formula():
+    from llm_training_amd.lms.preference import ORPO
+    cfg = tiny_llama_cfg()
+    orpo = ORPO({"model": None, "beta": 0.1})
+    orpo.model = Llama(cfg, dtype=torch.float32)
+    orpo.model.init_weights(4)
+    batch = _pref_batch(cfg.vocab_size)
+    loss, m, _ = orpo.training_step(batch)
+    cs, cn = _seq_logps(orpo.model, batch["chosen_input_ids"], batch["chosen_labels"])
+    rs, rn = _seq_logps(orpo.model, batch["rejected_input_ids"], batch["rejected_labels"])
+    c, r = cs / cn, rs / rn
+    lo = (c - r) - (torch.log1p(-torch.exp(c)) - torch.log1p(-torch.exp(r)))
+    or_loss = -(0.1 * torch.nn.functional.logsigmoid(lo)).mean()
+    ce = -cs.sum() / cn.sum()
+    assert abs(loss.item() - (or_loss + ce).item()) < 1e-4
