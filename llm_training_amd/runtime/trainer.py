@@ -43,7 +43,7 @@ class TrainerState:
 
     def state_dict(self):
         return {"global_step": self.global_step, "epoch": self.epoch, "batch_idx": self.batch_idx,
-                "consumed": dict(self.consumed)}
+                "consumed": {k: float(v) for k, v in self.consumed.items()}}
 
     def load_state_dict(self, st):
         self.global_step = int(st["global_step"])
@@ -188,16 +188,16 @@ class Trainer:
             accum = self.accumulate_grad_batches
             while self.state.batch_idx + accum <= nbe and not self.should_stop:
                 batches = [next(it) for _ in range(accum)]
-                self.train_step(batches)
-                self.state.batch_idx += accum
+                self.train_step(batches)  # advances batch_idx before the batch-end callbacks run
                 if self.max_steps > 0 and self.state.global_step >= self.max_steps:
                     self.should_stop = True
                 if self._should_validate(nbe):
                     self.validate()
-            self.state.epoch += 1
-            self.state.batch_idx = 0
-            for cb in self.callbacks:
-                _call(cb, "on_train_epoch_end", self, lm)
+            if self.state.batch_idx + accum > nbe:  # epoch completed (not an early stop mid-epoch)
+                for cb in self.callbacks:
+                    _call(cb, "on_train_epoch_end", self, lm)
+                self.state.epoch += 1
+                self.state.batch_idx = 0
         self._flush_logs(force=True)
         for cb in self.callbacks:
             _call(cb, "on_fit_end", self, lm)
@@ -252,6 +252,7 @@ class Trainer:
         metrics_acc["lr"] = torch.tensor(lr)
         if getattr(lm.config, "log_grad_norm", True) and eng.grad_norm is not None:
             metrics_acc["Gradient Norm"] = eng.grad_norm.reshape(())
+        self.state.batch_idx += len(batches)
         self._log_buffer.append((self.state.global_step, metrics_acc))
         self.step_times.append(time.perf_counter() - t0)
         self._flush_logs()

@@ -1,0 +1,94 @@
+"""Trainer loop, LR schedules, checkpoint save -> resume (exact continuation), HF export round trip."""
+import math
+import os
+
+import pytest
+import torch
+
+from llm_training_amd.data.dummy import DummyDataModule
+from llm_training_amd.lms.clm import CLM
+from llm_training_amd.lr_schedulers import ConstantWarmupLR, CosineAnnealingWarmupLR, LinearWarmupLR
+from llm_training_amd.runtime.callbacks import ModelCheckpoint
+from llm_training_amd.runtime.loggers import JSONLLogger
+from llm_training_amd.runtime.strategies import DeepSpeedStrategy, FSDP2Strategy
+from llm_training_amd.runtime.trainer import Trainer
+
+
+def test_lr_schedules_match_reference_formulas():
+    c = CosineAnnealingWarmupLR(1.0, num_warmup_steps=4, num_total_steps=14, min_lr=0.1)
+    assert [round(c.lr_at(s), 6) for s in range(4)] == [0.25, 0.5, 0.75, 1.0]
+    assert abs(c.lr_at(4) - 1.0) < 1e-9 and abs(c.lr_at(14) - 0.1) < 1e-9
+    assert abs(c.lr_at(9) - (0.1 + 0.9 * (1 + math.cos(math.pi * 5 / 10)) / 2)) < 1e-9
+    k = ConstantWarmupLR(2.0, factor=0.5, total_iters=3, num_warmup_steps=2)
+    assert [k.lr_at(s) for s in range(7)] == [1.0, 2.0, 1.0, 1.0, 1.0, 2.0, 2.0]
+    lin = LinearWarmupLR(1.0, num_warmup_steps=3, num_total_steps=13, min_lr=0.0)
+    assert abs(lin.lr_at(0) - 0.25) < 1e-9 and abs(lin.lr_at(13)) < 1e-9 and abs(lin.lr_at(8) - 0.5) < 1e-9
+
+
+def _lm(seed=0):
+    return CLM({"model": {"model_class": "llm_training.models.Llama",
+                          "model_config": {"vocab_size": 96, "hidden_size": 32, "intermediate_size": 64,
+                                           "num_hidden_layers": 2, "num_attention_heads": 4,
+                                           "num_key_value_heads": 2}},
+                "optim": {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 5e-3},
+                          "lr_scheduler_class": "llm_training.lr_schedulers.CosineAnnealingWarmupLR",
+                          "lr_scheduler_kwargs": {"num_warmup_steps": 2, "min_lr": 1e-4}}})
+
+
+def _dm():
+    return DummyDataModule({"batch_size": 2, "vocab_size": 96, "max_length": 16, "num_samples": 64, "base_seed": 5})
+
+
+def _losses(tmp):
+    rows = [__import__("json").loads(l) for l in open(os.path.join(tmp, "metrics.jsonl"))]
+    return {r["step"]: r["Loss/Train/Step"] for r in rows if "Loss/Train/Step" in r}
+
+
+@pytest.mark.parametrize("strategy", [FSDP2Strategy(), DeepSpeedStrategy(stage=2)], ids=["fsdp2", "zero2"])
+def test_resume_is_exact(tmp_path, strategy):
+    log1 = tmp_path / "a"
+    t1 = Trainer(strategy=strategy, precision="32-true", logger=JSONLLogger(str(log1), "r"), max_steps=6,
+                 log_every_n_steps=1, accumulate_grad_batches=2, gradient_clip_val=1.0, seed=11,
+                 callbacks=[ModelCheckpoint(dirpath=str(tmp_path / "ck"), every_n_train_steps=3, save_top_k=-1)])
+    t1.fit(_lm(), _dm())
+    full = _losses(log1 / "r")
+    ck = tmp_path / "ck" / "epoch=0-step=3.ckpt"
+    assert (ck / "meta.json").exists() and (ck / "tp0.safetensors").exists()
+    log2 = tmp_path / "b"
+    t2 = Trainer(strategy=strategy, precision="32-true", logger=JSONLLogger(str(log2), "r"), max_steps=6,
+                 log_every_n_steps=1, accumulate_grad_batches=2, gradient_clip_val=1.0, seed=11)
+    t2.fit(_lm(), _dm(), ckpt_path=str(ck))
+    resumed = _losses(log2 / "r")
+    assert sorted(resumed) == [4, 5, 6]
+    for s in (4, 5, 6):
+        assert abs(resumed[s] - full[s]) < 1e-5, (s, resumed[s], full[s])
+
+
+def test_convert_to_hf_roundtrip(tmp_path):
+    from transformers import AutoModelForCausalLM
+
+    from llm_training_amd.tools.convert_to_hf import convert
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=2, log_every_n_steps=1, seed=1,
+                default_root_dir=str(tmp_path))
+    lm = _lm()
+    t.fit(lm, _dm())
+    ck = tmp_path / "ck"
+    t.save_checkpoint(str(ck))
+    out = convert(str(ck), str(tmp_path / "hf"), dtype="float32")
+    hf = AutoModelForCausalLM.from_pretrained(out, local_files_only=True)
+    hf.eval()
+    lm.model.eval()
+    ids = torch.randint(0, 96, (2, 16))
+    with torch.no_grad():
+        a = lm.model(input_ids=ids).logits
+        b = hf(input_ids=ids).logits
+    assert torch.allclose(a, b, atol=1e-4), (a - b).abs().max()
+
+
+def test_training_time_estimator_stops(tmp_path):
+    from llm_training_amd.runtime.callbacks import TrainingTimeEstimator
+    est = TrainingTimeEstimator(num_test_steps=4, num_warmup_steps=2)
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=50, callbacks=[est], seed=1,
+                default_root_dir=str(tmp_path))
+    t.fit(_lm(), _dm())
+    assert t.global_step == 4 and est.result is not None and est.result["steps_per_sec"] > 0
