@@ -71,13 +71,13 @@ def normal_(t: torch.Tensor, std: float, gen: torch.Generator | None = None):
 
 class _EmbeddingFn(Function):
     @staticmethod
-    def forward(ctx, ids, w, v0, v1):
+    def forward(ctx, ids, w, v0, v1, sharded):
         ctx.save_for_backward(ids)
         ctx.v = (v0, v1)
         ctx.wshape = w.shape
         ctx.w = w
         local = ids - v0
-        if v0 != 0 or v1 != w.shape[0]:  # vocab-sharded: zero rows owned by other ranks
+        if sharded:  # vocab-sharded: rows owned by other ranks contribute zeros
             mask = (ids >= v0) & (ids < v1)
             local = torch.where(mask, local, torch.zeros_like(local))
             out = torch.nn.functional.embedding(local, w)
@@ -92,7 +92,7 @@ class _EmbeddingFn(Function):
         w = ctx.w
         v0, v1 = ctx.v
         if not ctx.needs_input_grad[1]:
-            return None, None, None, None
+            return None, None, None, None, None
         mask = (ids >= v0) & (ids < v1)
         local = (ids - v0).masked_fill(~mask, 0).reshape(-1)
         g2 = (g * mask.unsqueeze(-1).to(g.dtype)).reshape(-1, g.shape[-1])
@@ -100,12 +100,12 @@ class _EmbeddingFn(Function):
         if mg is None:
             dw = torch.zeros(ctx.wshape, dtype=g.dtype, device=g.device)
             dw.index_add_(0, local, g2)
-            return None, dw, None, None
+            return None, dw, None, None, None
         if not getattr(w, "grad_added", False):
             mg.zero_()
         mg.view(ctx.wshape).index_add_(0, local, g2.to(mg.dtype))
         w.grad_added = True
-        return None, None, None, None
+        return None, None, None, None, None
 
 
 class VocabParallelEmbedding(nn.Module):
@@ -122,7 +122,7 @@ class VocabParallelEmbedding(nn.Module):
         self.weight = nn.Parameter(torch.empty(per, hidden_size, dtype=dtype, device=device))
 
     def forward(self, ids_sb: torch.Tensor) -> torch.Tensor:
-        out = _EmbeddingFn.apply(ids_sb, self.weight, self.v0, self.v1)
+        out = _EmbeddingFn.apply(ids_sb, self.weight, self.v0, self.v1, self.pc.tp)
         if self.pc.tp:
             out = tpl.scatter_seq(out, self.pc.tp_group)
         return out

@@ -22,9 +22,9 @@ from ..ops.native import lib, use_native
 
 def _combine_lse(lse_local: torch.Tensor, group) -> torch.Tensor:
     n = dist.get_world_size(group)
-    allv = torch.empty((n, *lse_local.shape), dtype=lse_local.dtype, device=lse_local.device)
+    allv = torch.empty(n * lse_local.numel(), dtype=lse_local.dtype, device=lse_local.device)
     dist.all_gather_into_tensor(allv, lse_local.contiguous(), group=group)
-    return torch.logsumexp(allv, dim=0)
+    return torch.logsumexp(allv.view(n, -1), dim=0)
 
 
 def _local_stats(lg, lab, v0, ignore_index, native):

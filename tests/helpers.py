@@ -46,8 +46,11 @@ def _entry(rank, world, port, fn, args, q):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import io
         res = fn(rank, world, *args)
-        q.put((rank, "ok", res))
+        buf = io.BytesIO()
+        torch.save(res, buf)  # plain bytes: no shared-memory handles outliving this process
+        q.put((rank, "ok", buf.getvalue()))
     except Exception as e:  # noqa: BLE001
         import traceback
         q.put((rank, "err", traceback.format_exc()))
@@ -69,7 +72,8 @@ def run_gloo(fn, world=2, args=(), timeout=240):
             rank, status, res = q.get(timeout=timeout)
             if status != "ok":
                 raise AssertionError(f"rank {rank} failed:\n{res}")
-            out[rank] = res
+            import io
+            out[rank] = torch.load(io.BytesIO(res), weights_only=True)
     finally:
         for p in procs:
             p.join(timeout=30)
