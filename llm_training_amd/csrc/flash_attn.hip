@@ -26,6 +26,8 @@
 //  * query blocks are scheduled heaviest-first (reverse order) so the causal triangle load-balances.
 #include "common.h"
 
+#include <initializer_list>
+
 namespace llmt {
 
 typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
@@ -84,13 +86,27 @@ __device__ __forceinline__ bfv8 acc_as_b(const f32v16& a, int s) {
 // 16-byte buffer load; rows past the descriptor's num_records come back as zeros (no selects).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// The descriptor words must stay scalar, or hipcc wraps every buffer op in a readfirstlane/saveexec
+// waterfall loop (cdna guide T20). Build it from kernel-argument / blockIdx values with plain integer
+// ops only: HIP's min<int64_t> (lowered through f64) or a readfirstlane round trip both pushed the
+// descriptor into VGPRs and produced the waterfall in every K/V load.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)min<int64_t>(bytes, 0x7fffffff),
-                                           0x00020000);
+  const int n = (int)(bytes > 0x7fffffffLL ? 0x7fffffffLL : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, n, 0x00020000);
 }
 __device__ __forceinline__ bfv8 bload8(__amdgpu_buffer_rsrc_t r, int off) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
   return __builtin_bit_cast(bfv8, v);
+}
+
+// one-time fragment loads (outside the tile loops): plain global loads, zero rows past the end
+__device__ __forceinline__ bfv8 gload8(const bf16* p, bool ok) {
+  bfv8 v = *reinterpret_cast<const bfv8*>(p);  // callers clamp p to a valid row
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (__bf16)0.f;
+  }
+  return v;
 }
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -148,9 +164,9 @@ struct AttnArgs {
   float* dk_part;
   float* dv_part;
   int B, S, Hq, Hkv;
-  int64_t q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh;
-  int64_t d_sb, d_ss, d_sh;    // dout strides
-  int64_t dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
+  int q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh;  // element strides (host-checked < 2^31)
+  int d_sb, d_ss, d_sh;    // dout strides
+  int dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
   float scale;
   int causal, window;
 };
@@ -174,17 +190,17 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
   const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
   const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
-  const bf16* qp = a.q + b * a.q_sb + h * a.q_sh;
-  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + b * a.k_sb + hk * a.k_sh, (int64_t)S * a.k_ss * 2);
-  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + b * a.v_sb + hk * a.v_sh, (int64_t)S * a.v_ss * 2);
-  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(qp, (int64_t)S * a.q_ss * 2);
+  const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
   const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
   const int sq = (seg && qrow < S) ? seg[qrow] : 0;
   const float sl2 = a.scale * kLog2e;
 
   bfv8 qf[G::NKK];
 #pragma unroll
-  for (int kk = 0; kk < G::NKK; ++kk) qf[kk] = bload8(qrs, (int)(qrow * a.q_ss + kk * 16 + hh * 8) * 2);
+  for (int kk = 0; kk < G::NKK; ++kk)
+    qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
 
   f32v16 ot[G::NDT];
 #pragma unroll
@@ -199,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
 
   bfv8 kst[NV], vst[NV];
   int sst = 0;
-  auto load_tile = [&](int n0) {
+  auto load_tile = [&, krs, vrs](int n0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, kr = n0 + row;
@@ -315,7 +331,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (qrow < S) {
-    bf16* op = a.out + b * a.o_sb + (int64_t)qrow * a.o_ss + h * a.o_sh;
+    bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
 #pragma unroll
     for (int dt = 0; dt < G::NDT; ++dt)
 #pragma unroll
@@ -327,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
       }
     if (hh == 0) {
       const float muse = (m == -INFINITY) ? 0.f : m;
-      a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (muse + __log2f(lt)) * kLn2 : -INFINITY;
+      a.lse[((int64_t)(int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (muse + __log2f(lt)) * kLn2 : -INFINITY;
     }
   }
 }
@@ -341,8 +357,8 @@ __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(AttnArgs a) {
     const int64_t bs = row / a.Hq;
     const int64_t sidx = bs % a.S;
     const int64_t b = bs / a.S;
-    const bf16x8* op = reinterpret_cast<const bf16x8*>(a.o + b * a.o_sb + sidx * a.o_ss + h * a.o_sh);
-    const bf16x8* dp = reinterpret_cast<const bf16x8*>(a.dout + b * a.d_sb + sidx * a.d_ss + h * a.d_sh);
+    const bf16x8* op = reinterpret_cast<const bf16x8*>(a.o + (int64_t)b * a.o_sb + sidx * a.o_ss + (int64_t)h * a.o_sh);
+    const bf16x8* dp = reinterpret_cast<const bf16x8*>(a.dout + (int64_t)b * a.d_sb + sidx * a.d_ss + (int64_t)h * a.d_sh);
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < D / 8; ++c) {
@@ -352,7 +368,7 @@ __global__ __launch_bounds__(256) void fa_bwd_delta_kernel(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) s += x[i] * y[i];
     }
-    ((float*)a.delta)[(b * a.Hq + h) * a.S + sidx] = s;
+    ((float*)a.delta)[((int64_t)b * a.Hq + h) * a.S + sidx] = s;
   }
 }
 
@@ -374,22 +390,22 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
   const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
   const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
-  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(a.q + b * a.q_sb + h * a.q_sh, (int64_t)S * a.q_ss * 2);
-  const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.dout + b * a.d_sb + h * a.d_sh, (int64_t)S * a.d_ss * 2);
-  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + b * a.k_sb + hk * a.k_sh, (int64_t)S * a.k_ss * 2);
-  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + b * a.v_sb + hk * a.v_sh, (int64_t)S * a.v_ss * 2);
+  const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
+  const bf16* dop = a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
   const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
   const int sq = (seg && qrow < S) ? seg[qrow] : 0;
   const float sl2 = a.scale * kLog2e;
-  const int64_t lrow = ((int64_t)b * a.Hq + h) * S + qrow;
+  const int64_t lrow = ((int64_t)(int64_t)b * a.Hq + h) * S + qrow;
   const float lse2 = qrow < S ? a.lse[lrow] * kLog2e : INFINITY;
   const float dlt = qrow < S ? a.delta[lrow] : 0.f;
 
   bfv8 qf[G::NKK], df[G::NKK];
 #pragma unroll
   for (int kk = 0; kk < G::NKK; ++kk) {
-    qf[kk] = bload8(qrs, (int)(qrow * a.q_ss + kk * 16 + hh * 8) * 2);
-    df[kk] = bload8(drs, (int)(qrow * a.d_ss + kk * 16 + hh * 8) * 2);
+    qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+    df[kk] = gload8(dop + (int64_t)min(qrow, S - 1) * a.d_ss + kk * 16 + hh * 8, qrow < S);
   }
   f32v16 dqt[G::NDT];
 #pragma unroll
@@ -403,7 +419,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
 
   bfv8 kst[NV], vst[NV];
   int sst = 0;
-  auto load_tile = [&](int n0) {
+  auto load_tile = [&, krs, vrs](int n0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, kr = n0 + row;
@@ -483,7 +499,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
     __syncthreads();
   }
   if (qrow < S) {
-    bf16* dqp = a.out + b * a.dq_sb + (int64_t)qrow * a.dq_ss + h * a.dq_sh;
+    bf16* dqp = a.out + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * a.dq_sh;
 #pragma unroll
     for (int dt = 0; dt < G::NDT; ++dt)
 #pragma unroll
@@ -514,12 +530,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
   const int h = blockIdx.y, b = blockIdx.z, hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
   const int ks = kb * 128, kw = ks + wid * 32, kr = kw + r;
-  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(a.q + b * a.q_sb + h * a.q_sh, (int64_t)S * a.q_ss * 2);
-  const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.dout + b * a.d_sb + h * a.d_sh, (int64_t)S * a.d_ss * 2);
-  const __amdgpu_buffer_rsrc_t krs = make_rsrc(a.k + b * a.k_sb + hk * a.k_sh, (int64_t)S * a.k_ss * 2);
-  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(a.v + b * a.v_sb + hk * a.v_sh, (int64_t)S * a.v_ss * 2);
-  const float* lsep = a.lse + ((int64_t)b * a.Hq + h) * S;
-  const float* dlp = a.delta + ((int64_t)b * a.Hq + h) * S;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh, (int64_t)S * a.q_ss * 2);
+  const __amdgpu_buffer_rsrc_t drs = make_rsrc(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh, (int64_t)S * a.d_ss * 2);
+  const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
+  const bf16* vp = a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh;
+  const float* lsep = a.lse + ((int64_t)(int64_t)b * a.Hq + h) * S;
+  const float* dlp = a.delta + ((int64_t)(int64_t)b * a.Hq + h) * S;
   const int* seg = a.seg ? a.seg + (int64_t)b * S : nullptr;
   const int sk = (seg && kr < S) ? seg[kr] : 0;
   const float sl2 = a.scale * kLog2e;
@@ -527,8 +543,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
   bfv8 kf[G::NKK], vf[G::NKK];
 #pragma unroll
   for (int kk = 0; kk < G::NKK; ++kk) {
-    kf[kk] = bload8(krs, (int)(kr * a.k_ss + kk * 16 + hh * 8) * 2);
-    vf[kk] = bload8(vrs, (int)(kr * a.v_ss + kk * 16 + hh * 8) * 2);
+    kf[kk] = gload8(kp + (int64_t)min(kr, S - 1) * a.k_ss + kk * 16 + hh * 8, kr < S);
+    vf[kk] = gload8(vp + (int64_t)min(kr, S - 1) * a.v_ss + kk * 16 + hh * 8, kr < S);
   }
   f32v16 dkt[G::NDT], dvt[G::NDT];
 #pragma unroll
@@ -546,7 +562,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
   bfv8 qst[NV], dst_[NV];
   float lst = 0.f, dls = 0.f;
   int sst = 0;
-  auto load_tile = [&](int q0) {
+  auto load_tile = [&, qrs, drs](int q0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = tid + 256 * i, row = e / G::V8, c8 = e % G::V8, qi = q0 + row;
@@ -655,8 +671,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
               make_float4(dvt[dt][4 * c], dvt[dt][4 * c + 1], dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
         }
     } else {
-      bf16* dkp = a.dk + b * a.dk_sb + (int64_t)kr * a.dk_ss + hk * a.dk_sh;
-      bf16* dvp = a.dv + b * a.dv_sb + (int64_t)kr * a.dv_ss + hk * a.dv_sh;
+      bf16* dkp = a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh;
+      bf16* dvp = a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh;
 #pragma unroll
       for (int dt = 0; dt < G::NDT; ++dt)
 #pragma unroll
@@ -699,8 +715,8 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
     wk.y = pack_bf16x2(sk.z, sk.w);
     wv.x = pack_bf16x2(sv.x, sv.y);
     wv.y = pack_bf16x2(sv.z, sv.w);
-    *reinterpret_cast<uint2*>(a.dk + b * a.dk_sb + (int64_t)s * a.dk_ss + hk * a.dk_sh + c4 * 4) = wk;
-    *reinterpret_cast<uint2*>(a.dv + b * a.dv_sb + (int64_t)s * a.dv_ss + hk * a.dv_sh + c4 * 4) = wv;
+    *reinterpret_cast<uint2*>(a.dk + (int64_t)b * a.dk_sb + (int64_t)s * a.dk_ss + (int64_t)hk * a.dk_sh + c4 * 4) = wk;
+    *reinterpret_cast<uint2*>(a.dv + (int64_t)b * a.dv_sb + (int64_t)s * a.dv_ss + (int64_t)hk * a.dv_sh + c4 * 4) = wv;
   }
 }
 
@@ -710,6 +726,11 @@ using namespace llmt;
 
 // buffer-load offsets are 32-bit: every row of one (batch, head) slice must be addressable
 static bool fits32(int64_t S, int64_t row_stride) { return S * row_stride * 2 < 0x7fffffffLL; }
+static bool strides32(std::initializer_list<int64_t> xs) {
+  for (int64_t x : xs)
+    if (x < 0 || x >= 0x7fffffffLL) return false;
+  return true;
+}
 
 static bool aligned16(const void* p, int64_t s0, int64_t s1, int64_t s2) {
   return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (s0 % 8 == 0) && (s1 % 8 == 0) && (s2 % 8 == 0);
@@ -726,6 +747,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
     return hipErrorInvalidValue;
   if (B == 0 || S == 0) return hipSuccess;
   if (!fits32(S, q_ss) || !fits32(S, k_ss) || !fits32(S, v_ss)) return hipErrorInvalidValue;
+  if (!strides32({q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh})) return hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.out = (bf16*)o; a.lse = lse; a.seg = seg;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv;
@@ -757,6 +779,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     return hipErrorInvalidValue;
   if (B == 0 || S == 0) return hipSuccess;
   if (!fits32(S, q_ss) || !fits32(S, k_ss) || !fits32(S, v_ss) || !fits32(S, o_ss)) return hipErrorInvalidValue;
+  if (!strides32({q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh, dq_sb, dq_ss, dq_sh, dk_sb,
+                  dk_ss, dk_sh, dv_sb, dv_ss, dv_sh}))
+    return hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (const bf16*)o;
   a.dout = (const bf16*)dout; a.out = (bf16*)dq; a.lse = (float*)lse; a.delta = delta; a.seg = seg;
