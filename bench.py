@@ -92,7 +92,6 @@ def main():
         engine.begin_step(1)
         engine.zero_grad()
         engine.begin_micro(0)
-        engine.wait_params()
         loss, _, _ = lm.training_step(batch)
         loss.backward()
         engine.finish_backward()

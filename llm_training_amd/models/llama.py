@@ -196,7 +196,9 @@ class Llama(BaseModel):
                     e.weight[pad - e.v0].zero_()
 
     def fsdp_units(self):
-        return [self.embed_tokens, *self.layers, nn.ModuleList([m for m in (self.norm, self.lm_head) if m is not None])]
+        # last unit: final norm + lm_head, hooked on the norm (called first)
+        tail = [m for m in (self.norm, self.lm_head) if m is not None]
+        return [self.embed_tokens, *self.layers, (self.norm, tail)]
 
     # ------------------------------------------------------------------ forward
     def _runtime(self, input_ids, position_ids, segment_ids, device, S, B):

@@ -69,6 +69,7 @@ class _Unit:
     rs_event: object = None
     hook_handles: list = field(default_factory=list)
     replicated: bool = False
+    keep_gathered: bool = False     # stage 3: params used outside the hooked module's forward
 
     @property
     def shard_numel(self):
@@ -105,6 +106,9 @@ class DataParallelEngine:
         self.units: list[_Unit] = []
         self._build_units()
         self._install_hooks()
+        # units whose module is never called in forward cannot wait for their own parameter
+        # all-gather in a pre-forward hook: then the whole comm stream is awaited at step start
+        self.global_wait = any(u.module is not None and not _hookable(u.module) for u in self.units)
         self.grad_norm = None
         self._gscale = torch.ones(1, device=dev, dtype=torch.float32)
 
@@ -113,10 +117,19 @@ class DataParallelEngine:
         seen: set[int] = set()
         mods = self.model.fsdp_units() if hasattr(self.model, "fsdp_units") else [self.model]
         groups: list[tuple[nn.Module, list[nn.Parameter], bool]] = []
+        multi: set[int] = set()
         rep: list[nn.Parameter] = []
         for m in mods:
+            # a unit is a module, or (hook_module, [modules...]) when its parameters live in several
+            # modules and the first one called in forward carries the hooks (e.g. final norm + lm_head)
+            if isinstance(m, tuple):
+                m, srcs = m
+                plist = [p for s in srcs for p in s.parameters()]
+                multi.add(len(groups))
+            else:
+                plist = list(m.parameters())
             params = []
-            for p in m.parameters():
+            for p in plist:
                 if id(p) in seen or not p.requires_grad:
                     continue
                 seen.add(id(p))
@@ -129,6 +142,7 @@ class DataParallelEngine:
             groups.append((None, rep, True))
         for i, (m, params, replicated) in enumerate(groups):
             self.units.append(self._make_unit(i, m, params, replicated))
+            self.units[-1].keep_gathered = i in multi or i == len(groups) - 1
         nparams = sum(p.numel() for u in self.units for p in u.params)
         logger.info("engine: %d units, %.3f B trainable params (local), zero stage %d, dp %d, tp %d",
                     len(self.units), nparams / 1e9, self.stage, self.dp, self.pc.tp_size)
@@ -214,7 +228,7 @@ class DataParallelEngine:
 
     def _make_post_fwd(self, u: _Unit):
         def hook(mod, args, out):
-            if self.reshard_after_forward and u.idx != len(self.units) - 1:
+            if self.reshard_after_forward and not u.keep_gathered:
                 self._release_unit(u)
             # re-gather before this unit's backward: hook the unit's output gradient
             if torch.is_grad_enabled():
@@ -307,6 +321,8 @@ class DataParallelEngine:
     def begin_step(self, accumulate_grad_batches: int = 1):
         self.accum = max(1, int(accumulate_grad_batches))
         self.micro = 0
+        if self.global_wait:
+            self.wait_params()
 
     def begin_micro(self, i: int):
         self.micro = i
@@ -397,12 +413,10 @@ class DataParallelEngine:
                 _adamw_ref(u.master, u.exp_avg, u.exp_avg_sq, g.float() * self._gscale, lr, b1, b2, self.eps,
                            self.weight_decay, self.step_count)
                 pout.copy_(u.master)
-        # refresh the full bf16 parameters (stage 1/2): in-place all-gather of the updated shards
-        if self.stage in (1, 2) and dp > 1:
-            for u in self.units:
-                if u.replicated:
-                    continue
-                sn = u.numel // dp
+            # stage 1/2: refresh this unit's full bf16 parameters with an in-place all-gather of the
+            # updated shards on the comm stream right away, so it overlaps the remaining units' AdamW
+            # and the next forward (which waits per unit in its pre-forward hook)
+            if self.stage in (1, 2) and dp > 1 and not u.replicated:
                 shard = u.pflat[r * sn:(r + 1) * sn]
                 if self.comm_stream is not None:
                     ev = torch.cuda.Event()
@@ -494,6 +508,13 @@ class DataParallelEngine:
                 return False
 
         return _Ctx()
+
+
+def _hookable(m: nn.Module) -> bool:
+    """True if ``m`` is invoked as a module in forward (so its forward pre-hook fires)."""
+    if isinstance(m, (nn.ModuleList, nn.ModuleDict, nn.ParameterList)):
+        return False
+    return type(m).forward is not nn.Module.forward
 
 
 def _adamw_ref(p, m, v, g, lr, b1, b2, eps, wd, step):

@@ -232,8 +232,6 @@ class Trainer:
         counters: dict[str, Any] = {}
         for i, b in enumerate(batches):
             eng.begin_micro(i)
-            if i == 0:
-                eng.wait_params()
             b = self.to_device(b)
             loss, metrics, cnt = lm.training_step(b, self.state.batch_idx + i)
             loss.backward()
