@@ -34,6 +34,7 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
                                int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh,
                                int64_t o_sb, int64_t o_ss, int64_t o_sh, float scale, int causal, int window,
                                hipStream_t stream);
+int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D);
 hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                                const float* lse, float* delta, const int* seg, void* dq, void* dk, void* dv,
                                float* work, int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss,
@@ -297,10 +298,10 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == B * Hq * S, "flash_attn_bwd: lse");
   const int* sp = nullptr;
   if (seg.has_value() && seg->defined()) sp = seg->data_ptr<int>();
-  auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  auto delta = at::empty({llmt_flash_attn_bwd_ws((int)B, (int)S, (int)Hq, (int)D)}, q.options().dtype(at::kFloat));
   TORCH_CHECK(dout.strides() == o.strides(), "flash_attn_bwd: dout must share O's layout");
   at::Tensor work;  // fp32 per-q-head dK/dV partials, only needed for GQA
-  if (Hq != Hkv) work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
+  if (Hq != Hkv && D != 128) work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
   check(llmt_flash_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                             lse.data_ptr<float>(), delta.data_ptr<float>(), sp, dq.data_ptr(), dk.data_ptr(),
                             dv.data_ptr(), work.defined() ? work.data_ptr<float>() : nullptr, (int)B, (int)S, (int)Hq, (int)Hkv, (int)D,

@@ -720,6 +720,310 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
   }
 }
 
+// ============================================================================ backward, D = 128 pipeline
+// The D = 128 backward (every Llama-family model) runs a software-pipelined pair of kernels built
+// for one wave per SIMD (512 registers per lane):
+//  * Q / dO (dK/dV pass) tiles arrive by LDS-DMA (`buffer_load ... lds`, zero-filled past the end) into
+//    a ring of NS slots, several tiles ahead, behind counted `s_waitcnt vmcnt` and a raw barrier — the
+//    loads no longer stall every iteration (the v2 kernels waited on a one-tile-ahead register stage).
+//  * per-row constants are folded into the MFMA accumulators' initial values: S' = Q.K^T - lse/scale,
+//    dP' = dO.V^T - delta, so P = exp2(S' * scale * log2e) and dS = P * dP' need no subtraction; rows
+//    that must not contribute (past S, masked) start at -inf, so only diagonal / window / packed tiles
+//    pay for a mask and it is applied once, to the initial values.
+//  * each iteration overlaps the S/dP MFMAs of tile t with the softmax VALU and transposed LDS reads of
+//    tile t-1, and the dV/dK MFMAs of tile t-1 with the row reads of tile t+1.
+//  * the dK/dV workgroup loops over every query head of its kv-head group, so GQA needs no fp32
+//    partials and no reduction kernel; blocks are ordered kv-head-fastest (an XCD per kv head at
+//    Hkv = 8), heaviest key blocks first.
+// Per-row constants, packed per 32-row tile for the DMA:
+//   ld[((b*Hq + h)*nT + t)*128 + {0..31: -lse/scale | 32..63: -delta | 64..95: segment id}]
+constexpr int kLdTile = 128;
+
+__global__ __launch_bounds__(256) void fa_bwd_prep128_kernel(AttnArgs a, float* ld) {
+  constexpr int D = 128;
+  const int nT = (a.S + 31) / 32;
+  const int64_t nrows = (int64_t)a.B * a.Hq * nT * 32;
+  const float inv_scale = 1.f / a.scale;
+  for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < nrows; row += (int64_t)gridDim.x * 256) {
+    const int i = (int)(row & 31);
+    const int64_t tt = row >> 5;
+    const int t = (int)(tt % nT);
+    const int64_t bh = tt / nT;
+    const int h = (int)(bh % a.Hq);
+    const int b = (int)(bh / a.Hq);
+    const int s = t * 32 + i;
+    float dl = 0.f, ls = -INFINITY;
+    int sg = -1;
+    if (s < a.S) {
+      const bf16x8* op = reinterpret_cast<const bf16x8*>(a.o + (int64_t)b * a.o_sb + (int64_t)s * a.o_ss + (int64_t)h * a.o_sh);
+      const bf16x8* dp = reinterpret_cast<const bf16x8*>(a.dout + (int64_t)b * a.d_sb + (int64_t)s * a.d_ss + (int64_t)h * a.d_sh);
+#pragma unroll
+      for (int c = 0; c < D / 8; ++c) {
+        float x[8], y[8];
+        unpack8(op[c], x);
+        unpack8(dp[c], y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dl += x[j] * y[j];
+      }
+      const int64_t lr = ((int64_t)b * a.Hq + h) * a.S + s;
+      ((float*)a.delta)[lr] = dl;
+      const float l = a.lse[lr];
+      ls = (l == -INFINITY) ? -INFINITY : -l * inv_scale;
+      sg = a.seg ? a.seg[(int64_t)b * a.S + s] : 0;
+    }
+    float* blk = ld + (bh * nT + t) * kLdTile;
+    blk[i] = ls;
+    blk[32 + i] = -dl;
+    reinterpret_cast<int*>(blk)[64 + i] = sg;
+    blk[96 + i] = 0.f;
+  }
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// LDS-DMA issued from inline asm: hipcc cannot see these as LDS writes, so it does not put a
+// `vmcnt(0)` in front of every ds_read that follows one (it did with the builtin form, draining the
+// ring each iteration); the ring's counted waits below are the only synchronisation.
+struct Rsrc {
+  u32x4 w;
+};
+__device__ __forceinline__ Rsrc make_rsrc4(const void* base, int64_t bytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  Rsrc r;
+  r.w[0] = (uint32_t)p;
+  r.w[1] = (uint32_t)(p >> 32) & 0xffffu;
+  r.w[2] = (uint32_t)(bytes > 0x7fffffffLL ? 0x7fffffffLL : bytes);
+  r.w[3] = 0x00020000u;
+  return r;
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(lds_ptr_t)(const_cast<char*>(p));
+}
+__device__ __forceinline__ void dma16(const Rsrc& r, const char* lds, int voff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(lds_addr(lds)), "v"(voff), "s"(r.w) : "memory");
+}
+__device__ __forceinline__ void dma4(const Rsrc& r, const char* lds, int voff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(lds_addr(lds)), "v"(voff), "s"(r.w) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// every wave's LDS reads retired, then a barrier that does NOT drain the DMA ring (no vmcnt(0))
+__device__ __forceinline__ void ring_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// grid: ceil(S/128) * Hkv * B blocks (1-D), 4 waves x 32 keys; query tiles of 32 rows over all q heads of
+// the kv group; NS-slot LDS-DMA ring.
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, const float* ld) {
+  constexpr int D = 128, BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
+  constexpr int NDMA = 5;  // DMA instructions per wave per tile: Q 2, dO 2, row constants 1
+  using QI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases go to M0
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  const int b = L % a.B;
+  const int kb = L / a.B;
+  const int ks = kb * 128, kw = ks + wid * 32, kr = kw + r;
+  const int nT = (S + 31) / 32;
+  const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
+  const bf16* vp = a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh;
+  const int sk = (a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;
+  const float sl2 = a.scale * kLog2e;
+
+  bfv8 kf[8], vf[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    kf[kk] = gload8(kp + (int64_t)min(kr, S - 1) * a.k_ss + kk * 16 + hh * 8, kr < S);
+    vf[kk] = gload8(vp + (int64_t)min(kr, S - 1) * a.v_ss + kk * 16 + hh * 8, kr < S);
+  }
+  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
+  f32v16 dkt[4], dvt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      dkt[dt][i] = 0.f;
+      dvt[dt][i] = 0.f;
+    }
+
+  const int q_beg = a.causal ? ks : 0;  // multiple of 32
+  const int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+  const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
+  const int T = nq * grp;
+
+  if (T > 0) {
+    // ---- DMA of tile t (data of tile min(t, T-1)) into slot t % NS
+    auto issue = [&](int t) {
+      char* slot = smem + (t % NS) * SLOT;
+      const int tc = min(t, T - 1);
+      const int g = tc / nq;
+      const int q0 = q_beg + (tc - g * nq) * BM;
+      const int h = hk * grp + g;
+      const Rsrc qrs = make_rsrc4(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh, (int64_t)S * a.q_ss * 2);
+      const Rsrc drs = make_rsrc4(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh, (int64_t)S * a.d_ss * 2);
+      const Rsrc lrs = make_rsrc4(ld + ((int64_t)b * a.Hq + h) * nT * kLdTile, (int64_t)nT * kLdTile * 4);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int row0 = 8 * wid + 4 * n, row = row0 + (lane >> 4);
+        const int ch = (lane & 15) ^ QI::swz(row);
+        dma16(qrs, slot + row0 * 256, ((q0 + row) * a.q_ss + ch * 8) * 2);
+        dma16(drs, slot + IMG + row0 * 256, ((q0 + row) * a.d_ss + ch * 8) * 2);
+      }
+      // row constants: waves 0/2 fetch floats 0..63, waves 1/3 floats 64..127 (same bytes twice)
+      dma4(lrs, slot + 2 * IMG + (wid & 1) * 256, ((q0 >> 5) * kLdTile + (wid & 1) * 64 + lane) * 4);
+    };
+    auto tile_q0 = [&](int t) {
+      const int tc = min(t, T - 1);
+      const int g = tc / nq;
+      return q_beg + (tc - g * nq) * BM;
+    };
+    // initial accumulator values of tile t: -lse/scale and -delta per query row, -inf where masked
+    auto init = [&](int t, f32v16& si, f32v16& di) {
+      const char* slot = smem + (t % NS) * SLOT;
+      const float* Ls = reinterpret_cast<const float*>(slot + 2 * IMG);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 l4 = *reinterpret_cast<const float4*>(Ls + 8 * c + 4 * hh);
+        const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
+        si[4 * c] = l4.x; si[4 * c + 1] = l4.y; si[4 * c + 2] = l4.z; si[4 * c + 3] = l4.w;
+        di[4 * c] = d4.x; di[4 * c + 1] = d4.y; di[4 * c + 2] = d4.z; di[4 * c + 3] = d4.w;
+      }
+      const int q0 = tile_q0(t);
+      const bool need = a.seg || (a.causal && kw + 31 > q0) || (a.window >= 0 && q0 + 31 - a.window > kw);
+      if (need) {
+        const int* Sg = reinterpret_cast<const int*>(Ls + 64);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int4 s4 = make_int4(sk, sk, sk, sk);
+          if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int qi = q0 + 8 * c + 4 * hh + j;
+            bool ok = true;
+            if (a.causal) ok = ok && (kr <= qi);
+            if (a.window >= 0) ok = ok && (qi - kr <= a.window);
+            if (a.seg) ok = ok && ((&s4.x)[j] == sk);
+            si[4 * c + j] = ok ? si[4 * c + j] : -INFINITY;
+          }
+        }
+      }
+    };
+    auto rows = [&](int t, bfv8* qr, bfv8* dr) {
+      const char* slot = smem + (t % NS) * SLOT;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        qr[kk] = QI::row_read(slot, r, 2 * kk + hh);
+        dr[kk] = QI::row_read(slot + IMG, r, 2 * kk + hh);
+      }
+    };
+
+    // prologue: tiles 0..NS-2 in flight, wait for 0..2
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t) issue(t);
+    wait_vm<NDMA * (NS - 4)>();
+    ring_barrier();
+
+    bfv8 qr[8], dr[8];
+    f32v16 sacc, dacc;
+    rows(0, qr, dr);
+    init(0, sacc, dacc);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      sacc = mfma32(qr[kk], kf[kk], sacc);
+      dacc = mfma32(dr[kk], vf[kk], dacc);
+    }
+    rows(1, qr, dr);
+
+    for (int t = 1; t <= T; ++t) {
+      issue(t + NS - 2);
+      // ---- region A: S/dP of tile t  ||  softmax of tile t-1 + its transposed reads
+      f32v16 sn, dn;
+      init(t, sn, dn);
+      const char* pslot = smem + ((t - 1) % NS) * SLOT;
+      bfv8 trd[2][4], trq[2][4];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          trd[s2][dt] = QI::trA(pslot + IMG, BM, 16 * s2, dt * 32, lane);
+          trq[s2][dt] = QI::trA(pslot, BM, 16 * s2, dt * 32, lane);
+        }
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        sn = mfma32(qr[kk], kf[kk], sn);
+        dn = mfma32(dr[kk], vf[kk], dn);
+      }
+      bfv8 pb[2], db[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = fexp2(sacc[8 * s2 + j] * sl2);
+          pb[s2][j] = (__bf16)p;
+          db[s2][j] = (__bf16)(p * dacc[8 * s2 + j]);
+        }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+      }
+      // pin the S/dP chains of tile t inside region A (IR passes otherwise sink them into region B)
+      asm volatile("" : "+v"(sn), "+v"(dn));
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- region B: dV/dK of tile t-1  ||  row reads of tile t+1
+      rows(t + 1, qr, dr);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dvt[dt] = mfma32(trd[s2][dt], pb[s2], dvt[dt]);
+          dkt[dt] = mfma32(trq[s2][dt], db[s2], dkt[dt]);
+        }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // DS read
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      sacc = sn;
+      dacc = dn;
+      wait_vm<NDMA * (NS - 4)>();
+      ring_barrier();
+    }
+    wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+  }
+
+  if (kr < S) {
+    bf16* dkp = a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh;
+    bf16* dvp = a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int d = dt * 32 + 8 * c + 4 * hh;
+        uint2 wk, wv;
+        wk.x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
+        wk.y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
+        wv.x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
+        wv.y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
+        *reinterpret_cast<uint2*>(dkp + d) = wk;
+        *reinterpret_cast<uint2*>(dvp + d) = wv;
+      }
+  }
+}
+
 }  // namespace llmt
 
 using namespace llmt;
@@ -764,6 +1068,12 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   return hipGetLastError();
 }
 
+// floats of the `delta` workspace llmt_flash_attn_bwd needs
+extern "C" int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D) {
+  const int64_t n = (int64_t)B * Hq * S;
+  return D == 128 ? n + (int64_t)B * Hq * ((S + 31) / 32) * kLdTile : n;
+}
+
 extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
                                           const void* dout, const float* lse, float* delta, const int* seg, void* dq,
                                           void* dk, void* dv, float* work, int B, int S, int Hq, int Hkv, int D,
@@ -796,10 +1106,19 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   a.dv_sb = dv_sb; a.dv_ss = dv_ss; a.dv_sh = dv_sh;
   a.scale = scale; a.causal = causal; a.window = window;
   const bool gqa = Hq != Hkv;
-  if (gqa && !work) return hipErrorInvalidValue;
   const int64_t nrows = (int64_t)B * S * Hq;
   dim3 grid((S + 127) / 128, Hq, B);
   const int dgrid = stream_grid(nrows, 256);
+  if (D == 128) {
+    // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws)
+    float* ld = delta + nrows;
+    const int64_t nT = (S + 31) / 32;
+    fa_bwd_prep128_kernel<<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
+    fa_bwd_dq_kernel<128><<<grid, 256, 0, stream>>>(a);
+    fa_bwd_dkdv128_kernel<<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    return hipGetLastError();
+  }
+  if (gqa && !work) return hipErrorInvalidValue;
 #define LLMT_BWD(DD)                                                                              \
   fa_bwd_delta_kernel<DD><<<dgrid, 256, 0, stream>>>(a);                                          \
   fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                              \

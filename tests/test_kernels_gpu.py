@@ -197,6 +197,20 @@ def test_flash_attention_window():
     _attn_case(1, 512, 4, 4, 96, window=100)
 
 
+@pytest.mark.parametrize("causal,window", [(True, 100), (False, -1), (True, -1)])
+def test_flash_attention_d128_pipeline(causal, window):
+    # D = 128 backward runs the LDS-DMA ring kernels: long enough for several ring wraps and GQA head loops
+    _attn_case(2, 1100, 8, 2, 128, causal=causal, window=window)
+
+
+def test_flash_attention_d128_segments_gqa():
+    B, S = 1, 777
+    seg = torch.zeros(B, S, dtype=torch.int32, device=DEV)
+    seg[0, 200:500] = 1
+    seg[0, 500:] = 2
+    _attn_case(B, S, 8, 1, 128, seg=seg)
+
+
 def test_rope_attention_fused_matches_reference():
     torch.manual_seed(0)
     S, B, nq, nkv, D = 256, 2, 8, 2, 128
