@@ -26,6 +26,7 @@
 //  * query blocks are scheduled heaviest-first (reverse order) so the causal triangle load-balances.
 #include "common.h"
 
+#include <cstdlib>
 #include <initializer_list>
 
 namespace llmt {
@@ -818,6 +819,7 @@ __device__ __forceinline__ void ring_barrier() { asm volatile("s_waitcnt lgkmcnt
 
 // grid: ceil(S/128) * Hkv * B blocks (1-D), 4 waves x 32 keys; query tiles of 32 rows over all q heads of
 // the kv group; NS-slot LDS-DMA ring.
+template <int V>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, const float* ld) {
   constexpr int D = 128, BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
   constexpr int NDMA = 5;  // DMA instructions per wave per tile: Q 2, dO 2, row constants 1
@@ -973,15 +975,17 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
           pb[s2][j] = (__bf16)p;
           db[s2][j] = (__bf16)(p * dacc[8 * s2 + j]);
         }
+      if constexpr (V == 0) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+        for (int g = 0; g < 16; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+        }
+        // pin the S/dP chains of tile t inside region A (IR passes otherwise sink them into region B)
+        asm volatile("" : "+v"(sn), "+v"(dn));
+        __builtin_amdgcn_sched_barrier(0);
       }
-      // pin the S/dP chains of tile t inside region A (IR passes otherwise sink them into region B)
-      asm volatile("" : "+v"(sn), "+v"(dn));
-      __builtin_amdgcn_sched_barrier(0);
       // ---- region B: dV/dK of tile t-1  ||  row reads of tile t+1
       rows(t + 1, qr, dr);
 #pragma unroll
@@ -991,12 +995,14 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
           dvt[dt] = mfma32(trd[s2][dt], pb[s2], dvt[dt]);
           dkt[dt] = mfma32(trq[s2][dt], db[s2], dkt[dt]);
         }
+      if constexpr (V == 0) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // DS read
+        for (int g = 0; g < 16; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // DS read
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
       sacc = sn;
       dacc = dn;
       wait_vm<NDMA * (NS - 4)>();
@@ -1020,6 +1026,185 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
         wv.y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
         *reinterpret_cast<uint2*>(dkp + d) = wk;
         *reinterpret_cast<uint2*>(dvp + d) = wv;
+      }
+  }
+}
+
+// grid: ceil(S/128) * Hq * B blocks (1-D: the query heads of one kv head on one XCD at Hkv = 8,
+// heaviest query blocks first), 4 waves x 32 queries. Key tiles of 64 rows (K dual image, V row
+// image, segment ids) arrive in a 4-slot LDS-DMA ring; each tile is processed as two 32-key half
+// steps: half h runs the S^T/dP^T MFMAs of h beside the dS VALU + K^T reads of h-1, then the dQ MFMAs
+// of h-1 beside the row reads of h+1 (registers, one half ahead). One barrier per tile.
+__global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const float* ld) {
+  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256, NS = 4;
+  constexpr int NDMA = 9;  // per wave per tile: K 4, V 4, segment ids 1
+  using KI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  const int nqb = (S + 127) / 128;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  const int h = hk * grp + L % grp;
+  L /= grp;
+  const int b = L % a.B;
+  const int mb = nqb - 1 - L / a.B;  // heaviest (last) query blocks first
+  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const int nT = (S + 31) / 32;
+  const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
+  const bf16* dop = a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh;
+  const float sl2 = a.scale * kLog2e;
+  // this lane's query: -lse/scale, -delta, segment id (from the packed per-tile constants)
+  const float* blk = ld + (((int64_t)b * a.Hq + h) * nT + (min(qrow, S - 1) >> 5)) * kLdTile;
+  float lsn = qrow < S ? blk[qrow & 31] : -INFINITY;
+  float ndl = qrow < S ? blk[32 + (qrow & 31)] : 0.f;
+  int sq = qrow < S ? reinterpret_cast<const int*>(blk)[64 + (qrow & 31)] : -2;
+
+  bfv8 qf[8], df[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+    df[kk] = gload8(dop + (int64_t)min(qrow, S - 1) * a.d_ss + kk * 16 + hh * 8, qrow < S);
+  }
+  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
+  asm volatile("" : "+v"(lsn), "+v"(ndl), "+v"(sq));
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(df[kk]));
+  f32v16 dqt[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dqt[dt][i] = 0.f;
+
+  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = kv_beg / BN * BN;
+  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+
+  if (T > 0) {
+    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
+    const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
+    auto issue = [&](int t) {
+      const char* slot = smem + (t % NS) * SLOT;
+      const int n0 = kv_beg + min(t, T - 1) * BN;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int row0 = 16 * wid + 4 * n, row = row0 + (lane >> 4);
+        const int ch = (lane & 15) ^ KI::swz(row);
+        dma16(krs, slot + row0 * 256, ((n0 + row) * a.k_ss + ch * 8) * 2);
+        dma16(vrs, slot + IMG + row0 * 256, ((n0 + row) * a.v_ss + ch * 8) * 2);
+      }
+      dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);  // all waves write the same 256 B
+    };
+    // half step hs = 2 t + u covers keys n0(t) + 32 u ..
+    auto hslot = [&](int hs) { return smem + ((hs >> 1) % NS) * SLOT; };
+    auto hkey0 = [&](int hs) { return kv_beg + min(hs >> 1, T - 1) * BN + 32 * (hs & 1); };
+    auto rows = [&](int hs, bfv8* kr_, bfv8* vr_) {
+      const char* slot = hslot(hs);
+      const int u = hs & 1;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        kr_[kk] = KI::row_read(slot, 32 * u + r, 2 * kk + hh);
+        vr_[kk] = KI::row_read(slot + IMG, 32 * u + r, 2 * kk + hh);
+      }
+    };
+    // initial S^T / dP^T accumulators of half hs: -lse/scale (-inf where masked) and -delta
+    auto init = [&](int hs, f32v16& si, f32v16& di) {
+      const int k0 = hkey0(hs);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        si[i] = lsn;
+        di[i] = ndl;
+      }
+      const bool need = a.seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
+                        (a.window >= 0 && k0 < qw + 31 - a.window);
+      if (need) {
+        const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int4 s4 = make_int4(sq, sq, sq, sq);
+          if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kx = k0 + 8 * c + 4 * hh + j;
+            bool ok = kx < S;
+            if (a.causal) ok = ok && (kx <= qrow);
+            if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
+            if (a.seg) ok = ok && ((&s4.x)[j] == sq);
+            si[4 * c + j] = ok ? lsn : -INFINITY;
+          }
+        }
+      }
+    };
+
+    bfv8 kr_[8], vr_[8];
+    f32v16 sp, dp;
+    // one half step: S^T/dP^T of hs (rows already in kr_/vr_) || dS of hs-1; dQ of hs-1 || rows of hs+1
+    auto half = [&](int hs) {
+      f32v16 sn, dn;
+      init(hs, sn, dn);
+      const char* pslot = hslot(hs - 1);
+      const int pu = (hs - 1) & 1;
+      bfv8 trk[2][4];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) trk[s2][dt] = KI::trA(pslot, BN, 32 * pu + 16 * s2, dt * 32, lane);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        sn = mfma32(kr_[kk], qf[kk], sn);
+        dn = mfma32(vr_[kk], df[kk], dn);
+      }
+      bfv8 dsb[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsb[s2][j] = (__bf16)(fexp2(sp[8 * s2 + j] * sl2) * dp[8 * s2 + j]);
+      rows(hs + 1, kr_, vr_);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dqt[dt] = mfma32(trk[s2][dt], dsb[s2], dqt[dt]);
+      sp = sn;
+      dp = dn;
+    };
+
+#pragma unroll
+    for (int t = 0; t < NS; ++t) issue(t);
+    wait_vm<2 * NDMA>();  // tiles 0 and 1 landed
+    ring_barrier();
+    rows(0, kr_, vr_);
+    init(0, sp, dp);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      sp = mfma32(kr_[kk], qf[kk], sp);
+      dp = mfma32(vr_[kk], df[kk], dp);
+    }
+    rows(1, kr_, vr_);
+    for (int t = 0; t < T; ++t) {
+      half(2 * t + 1);
+      half(2 * t + 2);
+      wait_vm<NDMA>();  // tile t+2 landed (t+3 may stay in flight)
+      ring_barrier();
+      issue(t + NS);    // into tile t's slot, free after the barrier
+    }
+    wait_vm<0>();
+  }
+
+  if (qrow < S) {
+    bf16* dqp = a.out + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * a.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint2 w;
+        w.x = pack_bf16x2(dqt[dt][4 * c] * a.scale, dqt[dt][4 * c + 1] * a.scale);
+        w.y = pack_bf16x2(dqt[dt][4 * c + 2] * a.scale, dqt[dt][4 * c + 3] * a.scale);
+        *reinterpret_cast<uint2*>(dqp + dt * 32 + 8 * c + 4 * hh) = w;
       }
   }
 }
@@ -1114,8 +1299,15 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     float* ld = delta + nrows;
     const int64_t nT = (S + 31) / 32;
     fa_bwd_prep128_kernel<<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
-    fa_bwd_dq_kernel<128><<<grid, 256, 0, stream>>>(a);
-    fa_bwd_dkdv128_kernel<<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    fa_bwd_dq128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a, ld);
+    static const int variant = [] {
+      const char* e = getenv("LLMT_FA_BWD_VARIANT");
+      return e ? atoi(e) : 1;
+    }();
+    if (variant == 1)
+      fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else
+      fa_bwd_dkdv128_kernel<0><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     return hipGetLastError();
   }
   if (gqa && !work) return hipErrorInvalidValue;
