@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--attn", default="flash", choices=["flash", "sdpa", "eager"])
     ap.add_argument("--ckpt", action="store_true", help="full activation checkpointing")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
+                    help="hipBLASLt solution selection (default: shipped TunableOp results)")
     args = ap.parse_args()
 
     from llm_training_amd.lms.clm import CLM
@@ -60,8 +62,10 @@ def main():
     from llm_training_amd.ops.native import lib
     from llm_training_amd.parallel.context import ParallelContext, init_distributed
     from llm_training_amd.parallel.engine import DataParallelEngine
+    from llm_training_amd.runtime.gemm_tuning import setup_gemm_tuning
 
     rank, local, world, device = init_distributed()
+    gemm_mode = setup_gemm_tuning(args.gemm_tuning)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     lib()  # fail loudly if the HIP extension is missing
@@ -133,7 +137,7 @@ def main():
             "config": {"model": "Llama-3-8B" if not args.layers else f"Llama-3-8B-{args.layers}L(INVALID-debug)",
                        "global_batch": pc.dp_size * B, "seq_len": S, "parallelism": par, "zero_stage": stage,
                        "attn": args.attn, "activation_checkpointing": args.ckpt, "optimizer": "fused AdamW fp32 master",
-                       "grad_clip": 1.0},
+                       "grad_clip": 1.0, "gemm_tuning": gemm_mode},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "mfu": round(tps / world * fpt / 2.5e15, 4),
             "tflops_per_gpu": round(tps / world * fpt / 1e12, 1),

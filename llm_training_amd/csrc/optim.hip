@@ -62,6 +62,46 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
   }
 }
 
+// bf16-gradient form, 8 elements per thread: every access is 16 bytes (grad and bf16 param copy were
+// 8-byte accesses in the 4-wide form); the fp32 state streams are written non-temporally.
+__global__ __launch_bounds__(256) void adamw8_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                     float* __restrict__ v, const bf16* __restrict__ g,
+                                                     bf16* __restrict__ pout, int64_t n8, float lr, float b1,
+                                                     float b2, float eps, float wd, float step_size,
+                                                     float inv_sqrt_bc2, const float* __restrict__ gscale) {
+  const float sc = gscale ? gscale[0] : 1.f;
+  const float decay = 1.f - lr * wd;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float gg[8];
+    unpack8(reinterpret_cast<const bf16x8*>(g)[i], gg);
+    float4 pp[2], mm[2], vv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pp[h] = reinterpret_cast<const float4*>(p)[2 * i + h];
+      mm[h] = reinterpret_cast<const float4*>(m)[2 * i + h];
+      vv[h] = reinterpret_cast<const float4*>(v)[2 * i + h];
+    }
+    float* pf = reinterpret_cast<float*>(pp);
+    float* mf = reinterpret_cast<float*>(mm);
+    float* vf = reinterpret_cast<float*>(vv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gk = gg[k] * sc;
+      mf[k] = b1 * mf[k] + (1.f - b1) * gk;
+      vf[k] = b2 * vf[k] + (1.f - b2) * gk * gk;
+      const float denom = sqrtf(vf[k]) * inv_sqrt_bc2 + eps;
+      pf[k] = pf[k] * decay - step_size * mf[k] / denom;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_nontemporal_store(pp[h], reinterpret_cast<float4*>(p) + 2 * i + h);
+      __builtin_nontemporal_store(mm[h], reinterpret_cast<float4*>(m) + 2 * i + h);
+      __builtin_nontemporal_store(vv[h], reinterpret_cast<float4*>(v) + 2 * i + h);
+    }
+    if (pout) reinterpret_cast<bf16x8*>(pout)[i] = pack8(pf);
+  }
+}
+
 // out[0] += sum(x^2) over n elements (n % 4 == 0); one atomic per block.
 template <typename T>
 __global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, int64_t n4, float* __restrict__ out) {
@@ -90,6 +130,12 @@ extern "C" hipError_t llmt_adamw(float* p, float* m, float* v, const void* g, in
   const double bc2 = 1.0 - pow((double)b2, (double)step);
   const float step_size = (float)(lr / bc1);
   const float inv_sqrt_bc2 = (float)(1.0 / sqrt(bc2));
+  if (!grad_is_fp32 && n % 8 == 0) {
+    const int64_t n8 = n / 8;
+    adamw8_kernel<<<stream_grid(n8, 256), 256, 0, stream>>>(p, m, v, (const bf16*)g, (bf16*)pout, n8, lr, b1, b2, eps,
+                                                            wd, step_size, inv_sqrt_bc2, gscale);
+    return hipGetLastError();
+  }
   const int grid = stream_grid(n4, 256);
   if (grad_is_fp32)
     adamw_kernel<float><<<grid, 256, 0, stream>>>(p, m, v, (const float*)g, (bf16*)pout, n4, lr, b1, b2, eps, wd,

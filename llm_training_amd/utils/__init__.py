@@ -1,3 +1,4 @@
 from .imports import import_object, normalize_path
+from .misc import ContextManagers, StrEnum, copy_method_signature
 
-__all__ = ["import_object", "normalize_path"]
+__all__ = ["import_object", "normalize_path", "ContextManagers", "StrEnum", "copy_method_signature"]
