@@ -102,8 +102,16 @@ class LlamaAttention(nn.Module):
     def forward(self, h, rt):
         S, B, _ = h.shape
         qkv = self.qkv_proj(h).view(S, B, self.nq + 2 * self.nkv, self.hd)
-        a = F_.rope_attention(qkv, rt["positions"], rt["cos"], rt["sin"], self.nq, self.nkv, causal=True,
-                              segment_ids=rt["segment_ids"], window=rt.get("window", -1), impl=rt["impl"])
+        def core(t):
+            return F_.rope_attention(t, rt["positions"], rt["cos"], rt["sin"], self.nq, self.nkv, causal=True,
+                                     segment_ids=rt["segment_ids"], window=rt.get("window", -1), impl=rt["impl"])
+
+        if rt.get("selective") and rt["impl"] != "flash" and self.training and torch.is_grad_enabled():
+            # selective recompute (reference llama_model.py:506-534): keep only the attention inputs and
+            # recompute the score matrix in backward. The flash kernels never store it, so they skip this.
+            a = ckpt.checkpoint(core, qkv, use_reentrant=False)
+        else:
+            a = core(qkv)
         return self.o_proj(a.reshape(S, B, self.nq * self.hd))
 
 
@@ -208,7 +216,9 @@ class Llama(BaseModel):
             position_ids = position_ids.to(device).long().expand(B, S)
         cos, sin = self.rope.get(device, S)
         impl = self.config.resolved_attn_implementation(device.type)
-        return {"positions": position_ids, "cos": cos, "sin": sin, "segment_ids": segment_ids, "impl": impl}
+        selective = self.gradient_checkpointing and self.config.recompute_granularity == "selective"
+        return {"positions": position_ids, "cos": cos, "sin": sin, "segment_ids": segment_ids, "impl": impl,
+                "selective": selective}
 
     def hidden_states(self, input_ids=None, position_ids=None, segment_ids=None, inputs_embeds=None,
                       gather_sequence: bool = True, embed_hook=None):
@@ -228,7 +238,8 @@ class Llama(BaseModel):
         rt = self._runtime(input_ids, position_ids, segment_ids, device, S, B)
         residual = None
         for layer in self.layers:
-            if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
+            if (self.gradient_checkpointing and self.config.recompute_granularity == "full" and self.training
+                    and torch.is_grad_enabled()):
                 if residual is None:
                     x, residual = ckpt.checkpoint(lambda a, lay=layer: lay(a, None, rt), x, use_reentrant=False)
                 else:

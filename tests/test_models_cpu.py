@@ -184,3 +184,25 @@ def test_orpo_loss_matches_formula():
     or_loss = -(0.1 * torch.nn.functional.logsigmoid(lo)).mean()
     ce = -cs.sum() / cn.sum()
     assert abs(loss.item() - (or_loss + ce).item()) < 1e-4
+
+
+@pytest.mark.parametrize("granularity", ["full", "selective"])
+def test_activation_checkpointing_matches(granularity):
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    from tests.helpers import tiny_llama_cfg
+    torch.manual_seed(0)
+    ids = torch.randint(0, 128, (2, 12))
+    grads = []
+    for ck in (False, True):
+        cfg = tiny_llama_cfg(enable_gradient_checkpointing=ck, recompute_granularity=granularity,
+                             attn_implementation="eager")
+        m = Llama(cfg, ParallelContext.single(), dtype=torch.float32)
+        m.init_weights(3)
+        m.train()
+        out = m(ids).logits
+        out.float().square().mean().backward()
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys()
+    for k in grads[0]:
+        assert torch.allclose(grads[0][k], grads[1][k], atol=1e-6), k
