@@ -30,8 +30,36 @@ def env_rank_info() -> tuple[int, int, int]:
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
         os.environ.setdefault("LOCAL_RANK", str(local))
+        host = first_slurm_host(os.environ.get("SLURM_JOB_NODELIST", os.environ.get("SLURM_NODELIST", "")))
+        if host:
+            os.environ.setdefault("MASTER_ADDR", host)
+        jid = os.environ.get("SLURM_JOB_ID")
+        if jid and jid.isdigit():
+            os.environ.setdefault("MASTER_PORT", str(20000 + int(jid) % 20000))
         return rank, local, world
     return 0, 0, 1
+
+
+def first_slurm_host(nodelist: str) -> str | None:
+    """First host of a SLURM node list ("gpu[03-05,9],cpu1" -> "gpu03") without calling scontrol."""
+    nodelist = nodelist.strip()
+    if not nodelist:
+        return None
+    head, depth = [], 0
+    for ch in nodelist:  # first top-level comma-separated item
+        if ch == "[":
+            depth += 1
+        elif ch == "]":
+            depth -= 1
+        elif ch == "," and depth == 0:
+            break
+        head.append(ch)
+    item = "".join(head)
+    if "[" not in item:
+        return item
+    prefix, rng = item.split("[", 1)
+    first = rng.rstrip("]").split(",")[0].split("-")[0]
+    return prefix + first
 
 
 def init_distributed(backend: str | None = None, timeout_minutes: float = 30.0, device_type: str | None = None):

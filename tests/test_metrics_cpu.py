@@ -97,3 +97,11 @@ def test_utils_parity():
     with init_on_device("cpu", include_buffers=True):
         lin2 = nn.Linear(2, 2)
     assert lin2.weight.device.type == "cpu"
+
+
+def test_slurm_nodelist_first_host():
+    from llm_training_amd.parallel.context import first_slurm_host
+    assert first_slurm_host("gpu[03-05,9],cpu1") == "gpu03"
+    assert first_slurm_host("nodeA,nodeB") == "nodeA"
+    assert first_slurm_host("mi355x-017") == "mi355x-017"
+    assert first_slurm_host("") is None
