@@ -238,14 +238,23 @@ class _RopeFlashAttnFn(Function):
         nq, nkv, causal, window, scale = ctx.cfg
         L = lib()
         do = do.transpose(0, 1)
-        if do.stride() != o.stride():
+        if not _same_layout(do, o):
             do = torch.empty_like(o).copy_(do)
+        elif do.stride() != o.stride():
+            do = do.as_strided(o.shape, o.stride())  # differs only in the strides of size-1 dims
         dqkv = torch.empty_like(qkv)
         x, dx = qkv.transpose(0, 1), dqkv.transpose(0, 1)
         L.flash_attn_bwd(x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:], o, do, lse, seg, dx[:, :, :nq],
                          dx[:, :, nq:nq + nkv], dx[:, :, nq + nkv:], scale, causal, window)
         L.rope_(dqkv, pos, cos, sin, nq + nkv, True)
         return dqkv, None, None, None, None, None, None, None, None, None
+
+
+def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same shape and the same element -> memory mapping (strides of size-1 dims do not matter)."""
+    if a.shape != b.shape:
+        return False
+    return all(n == 1 or sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()))
 
 
 class _FlashAttnFn(Function):
@@ -263,7 +272,11 @@ class _FlashAttnFn(Function):
         q, k, v, o, lse, seg = ctx.saved_tensors
         causal, window, scale = ctx.cfg
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        lib().flash_attn_bwd(q, k, v, o, do.contiguous(), lse, seg, dq, dk, dv, scale, causal, window)
+        if not _same_layout(do, o):
+            do = torch.empty_like(o).copy_(do)
+        elif do.stride() != o.stride():
+            do = do.as_strided(o.shape, o.stride())
+        lib().flash_attn_bwd(q, k, v, o, do, lse, seg, dq, dk, dv, scale, causal, window)
         return dq, dk, dv, None, None, None, None
 
 
