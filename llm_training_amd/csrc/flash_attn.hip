@@ -1209,6 +1209,191 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const 
   }
 }
 
+// ============================================================================ forward, D = 128 pipeline
+// grid: ceil(S/128) * Hq * B blocks (1-D, kv-head-major, heaviest query blocks first), 4 waves x 32
+// queries (query on the lane: S^T = K.Q^T). K/V tiles of 64 keys arrive by LDS-DMA in a 4-slot ring
+// (two tiles in flight); each tile runs as two 32-key half steps: the S^T MFMA chain of half h beside
+// the online-softmax VALU, V^T reads and O^T += V^T.P^T MFMAs of half h-1. One barrier per tile.
+__global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
+  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256, NS = 4;
+  constexpr int NDMA = 9;  // per wave per tile: K 4, V 4, segment ids 1
+  using KI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  const int nqb = (S + 127) / 128;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  const int h = hk * grp + L % grp;
+  L /= grp;
+  const int b = L % a.B;
+  const int mb = nqb - 1 - L / a.B;
+  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
+  const float sl2 = a.scale * kLog2e;
+  int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
+
+  bfv8 qf[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
+  asm volatile("" : "+v"(sq));
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(qf[kk]));
+  f32v16 ot[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = kv_beg / BN * BN;
+  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+
+  if (T > 0) {
+    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
+    const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
+    auto issue = [&](int t) {
+      const char* slot = smem + (t % NS) * SLOT;
+      const int n0 = kv_beg + min(t, T - 1) * BN;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int row0 = 16 * wid + 4 * n, row = row0 + (lane >> 4);
+        const int ch = (lane & 15) ^ KI::swz(row);
+        dma16(krs, slot + row0 * 256, ((n0 + row) * a.k_ss + ch * 8) * 2);
+        dma16(vrs, slot + IMG + row0 * 256, ((n0 + row) * a.v_ss + ch * 8) * 2);
+      }
+      dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
+    };
+    auto hslot = [&](int hs) { return smem + ((hs >> 1) % NS) * SLOT; };
+    auto hkey0 = [&](int hs) { return kv_beg + min(hs >> 1, T - 1) * BN + 32 * (hs & 1); };
+    auto rows = [&](int hs, bfv8* kr_) {
+      const char* slot = hslot(hs);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) kr_[kk] = KI::row_read(slot, 32 * (hs & 1) + r, 2 * kk + hh);
+    };
+    // initial S^T accumulator of half hs: 0, or -inf where the key is not visible
+    auto init = [&](int hs, f32v16& si) {
+      const int k0 = hkey0(hs);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) si[i] = 0.f;
+      const bool need = a.seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
+                        (a.window >= 0 && k0 < qw + 31 - a.window);
+      if (need) {
+        const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int4 s4 = make_int4(sq, sq, sq, sq);
+          if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kx = k0 + 8 * c + 4 * hh + j;
+            bool ok = kx < S && qrow < S;
+            if (a.causal) ok = ok && (kx <= qrow);
+            if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
+            if (a.seg) ok = ok && ((&s4.x)[j] == sq);
+            si[4 * c + j] = ok ? 0.f : -INFINITY;
+          }
+        }
+      }
+    };
+
+    bfv8 kr_[8];
+    f32v16 sp;
+    auto half = [&](int hs) {
+      f32v16 sn;
+      init(hs, sn);
+      const char* pslot = hslot(hs - 1);
+      const int pu = (hs - 1) & 1;
+      bfv8 trv[2][4];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) trv[s2][dt] = KI::trA(pslot + IMG, BN, 32 * pu + 16 * s2, dt * 32, lane);
+      // online softmax of half hs-1 (deferred rescale: keep the running max unless a row grew > kThr)
+      float smax = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        sp[i] *= sl2;
+        smax = fmaxf(smax, sp[i]);
+      }
+      smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
+      if (__any(smax > m + kThr)) {
+        const float mnew = fmaxf(m, smax);
+        const float alpha = (mnew == -INFINITY) ? 1.f : fexp2(m - mnew);
+        m = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
+      }
+      const float muse = (m == -INFINITY) ? 0.f : m;
+      // one basic block from here: S^T chain of half hs || exp of half hs-1, then P.V of hs-1
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) sn = mfma32(kr_[kk], qf[kk], sn);
+      bfv8 pb[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = fexp2(sp[8 * s2 + j] - muse);
+          l += p;
+          pb[s2][j] = (__bf16)p;
+        }
+      rows(hs + 1, kr_);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) ot[dt] = mfma32(trv[s2][dt], pb[s2], ot[dt]);
+      sp = sn;
+    };
+
+#pragma unroll
+    for (int t = 0; t < NS; ++t) issue(t);
+    wait_vm<2 * NDMA>();  // tiles 0 and 1 landed
+    ring_barrier();
+    rows(0, kr_);
+    init(0, sp);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) sp = mfma32(kr_[kk], qf[kk], sp);
+    rows(1, kr_);
+    for (int t = 0; t < T; ++t) {
+      half(2 * t + 1);
+      half(2 * t + 2);
+      wait_vm<NDMA>();
+      ring_barrier();
+      issue(t + NS);
+    }
+    wait_vm<0>();
+  }
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < S) {
+    bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint2 w;
+        w.x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
+        w.y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
+        *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
+      }
+    if (hh == 0) {
+      const float muse = (m == -INFINITY) ? 0.f : m;
+      a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (muse + __log2f(lt)) * kLn2 : -INFINITY;
+    }
+  }
+}
+
 }  // namespace llmt
 
 using namespace llmt;
@@ -1247,7 +1432,16 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   switch (D) {
     case 64: fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a); break;
     case 96: fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a); break;
-    case 128: fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a); break;
+    case 128: {
+      static const int variant = [] {
+        const char* e = getenv("LLMT_FA_FWD_VARIANT");
+        return e ? atoi(e) : 1;
+      }();
+      if (variant == 1)
+        fa_fwd128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else
+        fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
+    } break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -92,11 +92,12 @@ __global__ __launch_bounds__(256) void adamw8_kernel(float* __restrict__ p, floa
       const float denom = sqrtf(vf[k]) * inv_sqrt_bc2 + eps;
       pf[k] = pf[k] * decay - step_size * mf[k] / denom;
     }
+    typedef float f4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      __builtin_nontemporal_store(pp[h], reinterpret_cast<float4*>(p) + 2 * i + h);
-      __builtin_nontemporal_store(mm[h], reinterpret_cast<float4*>(m) + 2 * i + h);
-      __builtin_nontemporal_store(vv[h], reinterpret_cast<float4*>(v) + 2 * i + h);
+      __builtin_nontemporal_store(__builtin_bit_cast(f4, pp[h]), reinterpret_cast<f4*>(p) + 2 * i + h);
+      __builtin_nontemporal_store(__builtin_bit_cast(f4, mm[h]), reinterpret_cast<f4*>(m) + 2 * i + h);
+      __builtin_nontemporal_store(__builtin_bit_cast(f4, vv[h]), reinterpret_cast<f4*>(v) + 2 * i + h);
     }
     if (pout) reinterpret_cast<bf16x8*>(pout)[i] = pack8(pf);
   }
