@@ -68,6 +68,7 @@ class _Unit:
     ag_event: object = None
     rs_event: object = None
     hook_handles: list = field(default_factory=list)
+    opt_event: object = None        # async AdamW of this unit done (stage 3 shard update)
     replicated: bool = False
     keep_gathered: bool = False     # stage 3: params used outside the hooked module's forward
 
@@ -80,7 +81,7 @@ class DataParallelEngine:
     def __init__(self, model: nn.Module, pc: ParallelContext, zero_stage: int = 2, *, lr: float = 1e-5,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01,
                  grad_dtype: torch.dtype | None = None, reduce_dtype: torch.dtype | None = None,
-                 reshard_after_forward: bool = True, overlap_comm: bool = True):
+                 reshard_after_forward: bool = True, overlap_comm: bool = True, overlap_step: bool = True):
         self.model = model
         self.pc = pc
         self.stage = int(zero_stage)
@@ -97,6 +98,10 @@ class DataParallelEngine:
         self.cuda = dev.type == "cuda"
         self.native = self.cuda and use_native(torch.empty(0, device=dev))
         self.comm_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.overlap) else None
+        # AdamW runs on its own stream: unit i's update overlaps the next step's forward of units < i
+        # (memory-bound optimizer beside compute-bound GEMMs); each unit's forward waits for its own
+        # update through the same per-unit event the stage-1/2 all-gather uses
+        self.opt_stream = torch.cuda.Stream(device=dev) if (self.cuda and overlap_step) else None
         # models built from our fused ops write weight grads straight into the flat buffers; others
         # (transformers modules) leave ordinary .grad tensors that are absorbed after backward
         self.autograd_grads = not getattr(model, "writes_main_grad", True)
@@ -264,6 +269,9 @@ class DataParallelEngine:
             return
         self._alloc_full(u)
         sn = u.numel // self.dp
+        if self.cuda and u.opt_event is not None:
+            torch.cuda.current_stream().wait_event(u.opt_event)  # updated shard (async AdamW)
+            u.opt_event = None
         if self.cuda and self.comm_stream is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
@@ -323,6 +331,11 @@ class DataParallelEngine:
         self.micro = 0
         if self.global_wait:
             self.wait_params()
+        elif self.cuda:
+            for u in self.units:  # units without a forward hook (TP-replicated norms): wait here
+                if u.module is None and u.ag_event is not None:
+                    torch.cuda.current_stream().wait_event(u.ag_event)
+                    u.ag_event = None
 
     def begin_micro(self, i: int):
         self.micro = i
@@ -364,6 +377,8 @@ class DataParallelEngine:
 
     def clip_and_scale(self, max_norm: float | None):
         """Global grad norm computed on device; returns the device scalar scale used by the optimizer."""
+        if self.opt_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.opt_stream)
         denom = float(self.dp * self.accum)
         need_norm = max_norm is not None and max_norm > 0
         sumsq = torch.zeros(1, device=self.device, dtype=torch.float32)
@@ -395,8 +410,20 @@ class DataParallelEngine:
     @torch.no_grad()
     def step(self, lr: float):
         self.step_count += 1
+        if self.opt_stream is None:
+            self._step_units(lr)
+            return
+        start = torch.cuda.Event()
+        start.record(torch.cuda.current_stream())
+        self._gscale.record_stream(self.opt_stream)
+        with torch.cuda.stream(self.opt_stream):
+            self.opt_stream.wait_event(start)
+            self._step_units(lr)
+
+    def _step_units(self, lr: float):
         b1, b2 = self.betas
         dp, r = self.dp, self.pc.dp_rank
+        cur = torch.cuda.current_stream() if self.cuda else None
         for u in self.units:
             g = self._grad_shard(u)
             st, udp = self._ustage(u), self._udp(u)
@@ -413,6 +440,10 @@ class DataParallelEngine:
                 _adamw_ref(u.master, u.exp_avg, u.exp_avg_sq, g.float() * self._gscale, lr, b1, b2, self.eps,
                            self.weight_decay, self.step_count)
                 pout.copy_(u.master)
+            done = None
+            if self.cuda and self.opt_stream is not None:
+                done = torch.cuda.Event()
+                done.record(cur)
             # stage 1/2: refresh this unit's full bf16 parameters with an in-place all-gather of the
             # updated shards on the comm stream right away, so it overlaps the remaining units' AdamW
             # and the next forward (which waits per unit in its pre-forward hook)
@@ -420,28 +451,39 @@ class DataParallelEngine:
                 shard = u.pflat[r * sn:(r + 1) * sn]
                 if self.comm_stream is not None:
                     ev = torch.cuda.Event()
-                    ev.record(torch.cuda.current_stream())
+                    ev.record(cur)
                     with torch.cuda.stream(self.comm_stream):
                         self.comm_stream.wait_event(ev)
                         dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
                         done = torch.cuda.Event()
                         done.record(self.comm_stream)
-                    u.ag_event = done
                 else:
                     dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
+                    if done is not None:
+                        done = torch.cuda.Event()
+                        done.record(cur)
+            if st >= 3 and udp > 1:
+                u.opt_event = done
+            else:
+                u.ag_event = done
         if self.stage >= 3 and dp > 1:
             for u in self.units:
                 if u.gathered and not u.replicated:
                     self._release_unit(u)
 
     def wait_params(self):
+        """Make the current stream wait for every pending update / parameter all-gather."""
+        if self.opt_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.opt_stream)
         if self.comm_stream is not None:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
         for u in self.units:
             u.ag_event = None
+            u.opt_event = None
 
     # ------------------------------------------------------------------ state (checkpointing)
     def optimizer_state(self) -> dict:
+        self.wait_params()
         return {
             "step": self.step_count,
             "units": [{"master": u.master, "exp_avg": u.exp_avg, "exp_avg_sq": u.exp_avg_sq} for u in self.units],
@@ -451,6 +493,7 @@ class DataParallelEngine:
 
     @torch.no_grad()
     def load_optimizer_state(self, st: dict):
+        self.wait_params()
         self.step_count = int(st["step"])
         for u, s in zip(self.units, st["units"]):
             u.master.copy_(s["master"])
@@ -461,6 +504,7 @@ class DataParallelEngine:
     @torch.no_grad()
     def sync_params_from_master(self):
         """Write bf16 params from the fp32 masters (after loading weights / optimizer state)."""
+        self.wait_params()
         for u in self.units:
             dp, st = self._udp(u), self._ustage(u)
             r = self.pc.dp_rank if dp > 1 else 0
@@ -477,6 +521,7 @@ class DataParallelEngine:
     @torch.no_grad()
     def sync_master_from_params(self):
         """Re-derive fp32 masters from the (freshly loaded) bf16/fp32 params."""
+        self.wait_params()
         for u in self.units:
             dp, st = self._udp(u), self._ustage(u)
             r = self.pc.dp_rank if dp > 1 else 0
@@ -494,6 +539,7 @@ class DataParallelEngine:
 
         class _Ctx:
             def __enter__(self_):
+                eng.wait_params()
                 if eng.stage >= 3 and eng.dp > 1:
                     for u in eng.units:
                         if not u.replicated:
