@@ -9,9 +9,14 @@ MI355X (gfx950, this ROCm image) and loads it read-only at start-up: every GEMM 
 dispatches the measured-fastest solution, shapes not listed fall back to the default heuristic.
 
 Modes (``LLMT_GEMM_TUNING`` env var or ``Trainer(gemm_tuning=...)``):
-  * ``use``  (default) — load the shipped results file if it exists, never tune.
+  * ``use``  — load the shipped results file if it exists, never tune.
   * ``tune`` — benchmark every new GEMM shape's candidate solutions and write the file.
-  * ``off``  — library default heuristic.
+  * ``off``  (default) — library default heuristic.
+
+Measured on the bench (6 steps, 1x MI355X): ``use`` 16,474 tok/s vs ``off`` 16,521 tok/s — the shipped
+partial results (TunableOp times its candidates on constant data, which reads high; random-data
+timings in gpurun benchmarks/bench_gemm_layouts.py put every projection at 1.2-1.3 PF/s for fwd+dgrad+
+wgrad whatever the weight layout) do not move the end-to-end number, so the default stays ``off``.
 """
 from __future__ import annotations
 
@@ -29,7 +34,7 @@ _state = {"mode": None}
 
 def setup_gemm_tuning(mode: str | None = None, results: str | os.PathLike | None = None) -> str:
     """Configure TunableOp once per process; returns the active mode."""
-    mode = (mode or os.environ.get("LLMT_GEMM_TUNING", "use")).lower()
+    mode = (mode or os.environ.get("LLMT_GEMM_TUNING", "off")).lower()
     if _state["mode"] is not None:
         return _state["mode"]
     if mode not in ("use", "tune", "off"):
