@@ -865,34 +865,62 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
   const int T = nq * grp;
 
   if (T > 0) {
-    // ---- DMA of tile t (data of tile min(t, T-1)) into slot t % NS
+    // ---- DMA of the next tile (tiles past T-1 repeat the last one) into slot t % NS. The tile
+    // sequence is walked with scalar counters; lane offsets are loop constants and the buffer
+    // descriptor starts at the tile's first row (rows past S fall outside it and read as zeros).
+    int dq_off[2], dd_off[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int row = 8 * wid + 4 * n + (lane >> 4);
+      const int ch = (lane & 15) ^ QI::swz(row);
+      dq_off[n] = (row * a.q_ss + ch * 8) * 2;
+      dd_off[n] = (row * a.d_ss + ch * 8) * 2;
+    }
+    const int ld_off = ((wid & 1) * 64 + lane) * 4;
+    asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]));
+    // slot base as ONE scalar: hipcc otherwise folds (t % NS) * SLOT into every LDS address as two adds
+    auto sl = [&](int t) -> const char* { return smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT); };
+    int iss_g = 0, iss_q = 0, iss_n = 0;  // head within the group, tile within the head, tiles issued
     auto issue = [&](int t) {
-      char* slot = smem + (t % NS) * SLOT;
-      const int tc = min(t, T - 1);
-      const int g = tc / nq;
-      const int q0 = q_beg + (tc - g * nq) * BM;
-      const int h = hk * grp + g;
-      const Rsrc qrs = make_rsrc4(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh, (int64_t)S * a.q_ss * 2);
-      const Rsrc drs = make_rsrc4(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh, (int64_t)S * a.d_ss * 2);
-      const Rsrc lrs = make_rsrc4(ld + ((int64_t)b * a.Hq + h) * nT * kLdTile, (int64_t)nT * kLdTile * 4);
+      const char* slot = sl(t);
+      const int q0 = q_beg + iss_q * BM;
+      const int h = hk * grp + iss_g;
+      const int64_t rows_left = S - q0;
+      const Rsrc qrs = make_rsrc4(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_ss,
+                                  rows_left * a.q_ss * 2);
+      const Rsrc drs = make_rsrc4(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh + (int64_t)q0 * a.d_ss,
+                                  rows_left * a.d_ss * 2);
+      const Rsrc lrs = make_rsrc4(ld + (((int64_t)b * a.Hq + h) * nT + (q0 >> 5)) * kLdTile, kLdTile * 4);
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        const int row0 = 8 * wid + 4 * n, row = row0 + (lane >> 4);
-        const int ch = (lane & 15) ^ QI::swz(row);
-        dma16(qrs, slot + row0 * 256, ((q0 + row) * a.q_ss + ch * 8) * 2);
-        dma16(drs, slot + IMG + row0 * 256, ((q0 + row) * a.d_ss + ch * 8) * 2);
+        const int row0 = 8 * wid + 4 * n;
+        dma16(qrs, slot + row0 * 256, dq_off[n]);
+        dma16(drs, slot + IMG + row0 * 256, dd_off[n]);
       }
       // row constants: waves 0/2 fetch floats 0..63, waves 1/3 floats 64..127 (same bytes twice)
-      dma4(lrs, slot + 2 * IMG + (wid & 1) * 256, ((q0 >> 5) * kLdTile + (wid & 1) * 64 + lane) * 4);
+      dma4(lrs, slot + 2 * IMG + (wid & 1) * 256, ld_off);
+      if (++iss_n < T) {
+        if (++iss_q == nq) {
+          iss_q = 0;
+          ++iss_g;
+        }
+      }
     };
+    int ini_g = 0, ini_q = 0, ini_n = 0;  // the same walk for init(), one tile at a time
     auto tile_q0 = [&](int t) {
-      const int tc = min(t, T - 1);
-      const int g = tc / nq;
-      return q_beg + (tc - g * nq) * BM;
+      (void)t;
+      const int q0 = q_beg + ini_q * BM;
+      if (++ini_n < T) {
+        if (++ini_q == nq) {
+          ini_q = 0;
+          ++ini_g;
+        }
+      }
+      return q0;
     };
     // initial accumulator values of tile t: -lse/scale and -delta per query row, -inf where masked
     auto init = [&](int t, f32v16& si, f32v16& di) {
-      const char* slot = smem + (t % NS) * SLOT;
+      const char* slot = sl(t);
       const float* Ls = reinterpret_cast<const float*>(slot + 2 * IMG);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -921,12 +949,47 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
         }
       }
     };
+    // lane-constant LDS byte offsets inside a 32-row image, computed once and kept opaque so hipcc
+    // does not re-derive the swizzle for every read inside the loop (it did: ~5 VALU per read)
+    int ro[8], to[4][2];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) ro[kk] = QI::roff(r, 2 * kk + hh);
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        to[dt][0] = QI::toff(BM, row, dt * 32 + col);
+        to[dt][1] = QI::toff(BM, row + 8, dt * 32 + col);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(ro[kk]));
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
     auto rows = [&](int t, bfv8* qr, bfv8* dr) {
-      const char* slot = smem + (t % NS) * SLOT;
+      const char* slot = sl(t);
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        qr[kk] = QI::row_read(slot, r, 2 * kk + hh);
-        dr[kk] = QI::row_read(slot + IMG, r, 2 * kk + hh);
+        const char* p = slot + ro[kk];  // one VGPR address; the dO image is an immediate offset away
+        qr[kk] = lds_b128(p);
+        dr[kk] = lds_b128(p + IMG);
+      }
+    };
+    // A operands of the accumulator-as-B products from tile image pair `slot`: rows 16*s2..,
+    // columns 32*dt.. of Q (dK) and dO (dV); 8 VGPR addresses per tile, everything else immediates
+    auto trA2 = [&](const char* slot, bfv8 (&tq)[2][4], bfv8 (&td)[2][4]) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const char* p0 = slot + to[dt][0];
+        const char* p1 = slot + to[dt][1];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const s16v4 ql = lds_tr(p0 + 4096 * s2), qh = lds_tr(p1 + 4096 * s2);
+          const s16v4 dl = lds_tr(p0 + IMG + 4096 * s2), dh = lds_tr(p1 + IMG + 4096 * s2);
+          tq[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(ql, qh, 0, 1, 2, 3, 4, 5, 6, 7));
+          td[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(dl, dh, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
       }
     };
 
@@ -952,15 +1015,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
       // ---- region A: S/dP of tile t  ||  softmax of tile t-1 + its transposed reads
       f32v16 sn, dn;
       init(t, sn, dn);
-      const char* pslot = smem + ((t - 1) % NS) * SLOT;
+      const char* pslot = sl(t - 1);
       bfv8 trd[2][4], trq[2][4];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          trd[s2][dt] = QI::trA(pslot + IMG, BM, 16 * s2, dt * 32, lane);
-          trq[s2][dt] = QI::trA(pslot, BM, 16 * s2, dt * 32, lane);
-        }
+      trA2(pslot, trq, trd);
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
         sn = mfma32(qr[kk], kf[kk], sn);
@@ -1089,7 +1146,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const 
     const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
     const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
     auto issue = [&](int t) {
-      const char* slot = smem + (t % NS) * SLOT;
+      const char* slot = smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT);
       const int n0 = kv_beg + min(t, T - 1) * BN;
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
@@ -1101,43 +1158,80 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const 
       dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);  // all waves write the same 256 B
     };
     // half step hs = 2 t + u covers keys n0(t) + 32 u ..
-    auto hslot = [&](int hs) { return smem + ((hs >> 1) % NS) * SLOT; };
+    // slot base as ONE scalar (see the dK/dV kernel) and loop-constant lane offsets
+    auto hslot = [&](int hs) -> const char* {
+      return smem + __builtin_amdgcn_readfirstlane(((hs >> 1) % NS) * SLOT);
+    };
+    int ro[8], to[4][2];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        to[dt][0] = KI::toff(BN, row, dt * 32 + col);
+        to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(ro[kk]));
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
     auto hkey0 = [&](int hs) { return kv_beg + min(hs >> 1, T - 1) * BN + 32 * (hs & 1); };
     auto rows = [&](int hs, bfv8* kr_, bfv8* vr_) {
-      const char* slot = hslot(hs);
-      const int u = hs & 1;
+      // rows 32*u.. of the half: +8192 B when u = 1 (swizzle depends on row & 15 only)
+      const char* slot = hslot(hs) + 8192 * (hs & 1);
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        kr_[kk] = KI::row_read(slot, 32 * u + r, 2 * kk + hh);
-        vr_[kk] = KI::row_read(slot + IMG, 32 * u + r, 2 * kk + hh);
+        const char* p = slot + ro[kk];
+        kr_[kk] = lds_b128(p);
+        vr_[kk] = lds_b128(p + IMG);
       }
     };
-    // initial S^T / dP^T accumulators of half hs: -lse/scale (-inf where masked) and -delta
-    auto init = [&](int hs, f32v16& si, f32v16& di) {
+    // initial S^T / dP^T accumulators: loop-constant -lse/scale and -delta vectors used directly as the
+    // first MFMA's C operand; a half that needs a mask builds a -inf-patched copy instead
+    f32v16 sic, dic;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      sic[i] = lsn;
+      dic[i] = ndl;
+    }
+    auto need_mask = [&](int hs) {
       const int k0 = hkey0(hs);
+      return a.seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) || (a.window >= 0 && k0 < qw + 31 - a.window);
+    };
+    auto masked_init = [&](int hs) {
+      const int k0 = hkey0(hs);
+      f32v16 si;
+      const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        si[i] = lsn;
-        di[i] = ndl;
-      }
-      const bool need = a.seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
-                        (a.window >= 0 && k0 < qw + 31 - a.window);
-      if (need) {
-        const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
+      for (int c = 0; c < 4; ++c) {
+        int4 s4 = make_int4(sq, sq, sq, sq);
+        if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          int4 s4 = make_int4(sq, sq, sq, sq);
-          if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int kx = k0 + 8 * c + 4 * hh + j;
-            bool ok = kx < S;
-            if (a.causal) ok = ok && (kx <= qrow);
-            if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
-            if (a.seg) ok = ok && ((&s4.x)[j] == sq);
-            si[4 * c + j] = ok ? lsn : -INFINITY;
-          }
+        for (int j = 0; j < 4; ++j) {
+          const int kx = k0 + 8 * c + 4 * hh + j;
+          bool ok = kx < S;
+          if (a.causal) ok = ok && (kx <= qrow);
+          if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
+          if (a.seg) ok = ok && ((&s4.x)[j] == sq);
+          si[4 * c + j] = ok ? lsn : -INFINITY;
         }
+      }
+      return si;
+    };
+    // S^T and dP^T of half hs from the rows in kr_/vr_
+    auto sdp = [&](int hs, const bfv8* kr_, const bfv8* vr_, f32v16& sn, f32v16& dn) {
+      if (need_mask(hs))
+        sn = mfma32(kr_[0], qf[0], masked_init(hs));
+      else
+        sn = mfma32(kr_[0], qf[0], sic);
+      dn = mfma32(vr_[0], df[0], dic);
+#pragma unroll
+      for (int kk = 1; kk < 8; ++kk) {
+        sn = mfma32(kr_[kk], qf[kk], sn);
+        dn = mfma32(vr_[kk], df[kk], dn);
       }
     };
 
@@ -1146,19 +1240,23 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const 
     // one half step: S^T/dP^T of hs (rows already in kr_/vr_) || dS of hs-1; dQ of hs-1 || rows of hs+1
     auto half = [&](int hs) {
       f32v16 sn, dn;
-      init(hs, sn, dn);
       const char* pslot = hslot(hs - 1);
       const int pu = (hs - 1) & 1;
       bfv8 trk[2][4];
+      {
+        const char* base = pslot + 8192 * pu;  // rows 32*pu..
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int dt = 0; dt < 4; ++dt) {
+          const char* p0 = base + to[dt][0];
+          const char* p1 = base + to[dt][1];
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) trk[s2][dt] = KI::trA(pslot, BN, 32 * pu + 16 * s2, dt * 32, lane);
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        sn = mfma32(kr_[kk], qf[kk], sn);
-        dn = mfma32(vr_[kk], df[kk], dn);
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const s16v4 lo = lds_tr(p0 + 4096 * s2), hi = lds_tr(p1 + 4096 * s2);
+            trk[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+        }
       }
+      sdp(hs, kr_, vr_, sn, dn);
       bfv8 dsb[2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -1178,12 +1276,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const 
     wait_vm<2 * NDMA>();  // tiles 0 and 1 landed
     ring_barrier();
     rows(0, kr_, vr_);
-    init(0, sp, dp);
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      sp = mfma32(kr_[kk], qf[kk], sp);
-      dp = mfma32(vr_[kk], df[kk], dp);
-    }
+    sdp(0, kr_, vr_, sp, dp);
     rows(1, kr_, vr_);
     for (int t = 0; t < T; ++t) {
       half(2 * t + 1);
