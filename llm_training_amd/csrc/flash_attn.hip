@@ -1353,7 +1353,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
     const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
     const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
     auto issue = [&](int t) {
-      const char* slot = smem + (t % NS) * SLOT;
+      const char* slot = smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT);
       const int n0 = kv_beg + min(t, T - 1) * BN;
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
@@ -1364,12 +1364,30 @@ __global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
       }
       dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
     };
-    auto hslot = [&](int hs) { return smem + ((hs >> 1) % NS) * SLOT; };
+    auto hslot = [&](int hs) -> const char* {
+      return smem + __builtin_amdgcn_readfirstlane(((hs >> 1) % NS) * SLOT);
+    };
+    int ro[8], to[4][2];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        to[dt][0] = KI::toff(BN, row, dt * 32 + col);
+        to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(ro[kk]));
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
     auto hkey0 = [&](int hs) { return kv_beg + min(hs >> 1, T - 1) * BN + 32 * (hs & 1); };
     auto rows = [&](int hs, bfv8* kr_) {
-      const char* slot = hslot(hs);
+      const char* slot = hslot(hs) + 8192 * (hs & 1);
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) kr_[kk] = KI::row_read(slot, 32 * (hs & 1) + r, 2 * kk + hh);
+      for (int kk = 0; kk < 8; ++kk) kr_[kk] = lds_b128(slot + ro[kk]);
     };
     // initial S^T accumulator of half hs: 0, or -inf where the key is not visible
     auto init = [&](int hs, f32v16& si) {
@@ -1405,10 +1423,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
       const char* pslot = hslot(hs - 1);
       const int pu = (hs - 1) & 1;
       bfv8 trv[2][4];
+      {
+        const char* base = pslot + IMG + 8192 * pu;
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int dt = 0; dt < 4; ++dt) {
+          const char* p0 = base + to[dt][0];
+          const char* p1 = base + to[dt][1];
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) trv[s2][dt] = KI::trA(pslot + IMG, BN, 32 * pu + 16 * s2, dt * 32, lane);
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const s16v4 lo = lds_tr(p0 + 4096 * s2), hi = lds_tr(p1 + 4096 * s2);
+            trv[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+        }
+      }
       // online softmax of half hs-1 (deferred rescale: keep the running max unless a row grew > kThr)
       float smax = -INFINITY;
 #pragma unroll

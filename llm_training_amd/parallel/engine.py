@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import re
 from dataclasses import dataclass, field
 
@@ -101,6 +102,7 @@ class DataParallelEngine:
         # AdamW runs on its own stream: unit i's update overlaps the next step's forward of units < i
         # (memory-bound optimizer beside compute-bound GEMMs); each unit's forward waits for its own
         # update through the same per-unit event the stage-1/2 all-gather uses
+        overlap_step = overlap_step and os.environ.get("LLMT_OVERLAP_STEP", "1") != "0"
         self.opt_stream = torch.cuda.Stream(device=dev) if (self.cuda and overlap_step) else None
         # models built from our fused ops write weight grads straight into the flat buffers; others
         # (transformers modules) leave ordinary .grad tensors that are absorbed after backward
