@@ -119,7 +119,16 @@ class Trainer:
 
     @property
     def param_dtype(self):
-        return PRECISIONS.get(self.precision, torch.bfloat16)
+        dt = PRECISIONS.get(self.precision, torch.bfloat16)
+        if dt == torch.float16 and torch.cuda.is_available():
+            # the reference's fp16 modes need a GradScaler; on MI355X bf16 runs the MFMAs at the same
+            # rate with fp32's exponent range, and the HIP kernels are bf16-only: run fp16 configs in bf16
+            if not getattr(self, "_fp16_warned", False):
+                logger.warning("precision %s: training in bf16 (same MFMA rate, no loss scaling needed)",
+                               self.precision)
+                self._fp16_warned = True
+            return torch.bfloat16
+        return dt
 
     # ------------------------------------------------------------------ setup
     def setup(self, lm, datamodule, ckpt_path: str | None = None):
