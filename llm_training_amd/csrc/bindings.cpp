@@ -28,7 +28,7 @@ hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const 
 hipError_t llmt_adamw(float* p, float* m, float* v, const void* g, int grad_is_fp32, void* pout, int64_t n,
                       float lr, float b1, float b2, float eps, float wd, int64_t step, const float* gscale,
                       hipStream_t stream);
-hipError_t llmt_sumsq(const void* x, int is_fp32, int64_t n, float* out, hipStream_t stream);
+hipError_t llmt_sumsq(const void* x, int is_fp32, int64_t n, float* out, float* ws, hipStream_t stream);
 hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* seg,
                                int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss, int64_t q_sh,
                                int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh,
@@ -247,7 +247,9 @@ void sumsq_(const at::Tensor& x, at::Tensor out) {
   TORCH_CHECK(x.is_contiguous() && x.numel() % 4 == 0, "sumsq: contiguous, numel % 4 == 0");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "sumsq dtype");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "sumsq out");
-  check(llmt_sumsq(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), out.data_ptr<float>(), cur_stream()),
+  auto ws = at::empty({1024}, out.options());
+  check(llmt_sumsq(x.data_ptr(), x.scalar_type() == at::kFloat, x.numel(), out.data_ptr<float>(),
+                   ws.data_ptr<float>(), cur_stream()),
         "sumsq");
 }
 

@@ -103,9 +103,11 @@ __global__ __launch_bounds__(256) void adamw8_kernel(float* __restrict__ p, floa
   }
 }
 
-// out[0] += sum(x^2) over n elements (n % 4 == 0); one atomic per block.
+// Deterministic sum of squares (the clipping norm must not depend on atomic ordering, so two runs of
+// the same step produce the same update): pass 1 writes one partial per block, pass 2 adds the
+// partials in a fixed order and accumulates into out[0] (units are summed in launch order).
 template <typename T>
-__global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, int64_t n4, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, int64_t n4, float* __restrict__ part) {
   __shared__ float red[4];
   float s = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
@@ -114,7 +116,15 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, int
     s += f[0] * f[0] + f[1] * f[1] + f[2] * f[2] + f[3] * f[3];
   }
   s = block_sum<4>(s, red);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) out[0] += s;
 }
 
 }  // namespace llmt
@@ -147,14 +157,16 @@ extern "C" hipError_t llmt_adamw(float* p, float* m, float* v, const void* g, in
   return hipGetLastError();
 }
 
-extern "C" hipError_t llmt_sumsq(const void* x, int is_fp32, int64_t n, float* out, hipStream_t stream) {
+// ws: >= 1024 floats of scratch
+extern "C" hipError_t llmt_sumsq(const void* x, int is_fp32, int64_t n, float* out, float* ws, hipStream_t stream) {
   if (n % 4) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
   if (n4 == 0) return hipSuccess;
   const int grid = stream_grid(n4, 256) > 1024 ? 1024 : stream_grid(n4, 256);
   if (is_fp32)
-    sumsq_kernel<float><<<grid, 256, 0, stream>>>((const float*)x, n4, out);
+    sumsq_kernel<float><<<grid, 256, 0, stream>>>((const float*)x, n4, ws);
   else
-    sumsq_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x, n4, out);
+    sumsq_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)x, n4, ws);
+  sum_partials_kernel<<<1, 256, 0, stream>>>(ws, grid, out);
   return hipGetLastError();
 }

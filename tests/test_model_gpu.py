@@ -81,3 +81,111 @@ def test_random_tokens_loss_stays_near_uniform():
         losses.append(loss.item())
     import math
     assert min(losses) > 0.8 * math.log(cfg.vocab_size), losses
+
+
+def _hip_vs_cpu(model_cls, cfg, ids, seg=None, tol_loss=2e-2, tol_grad=0.08):
+    torch.manual_seed(0)
+    cpu = model_cls(cfg, ParallelContext.single(), dtype=torch.float32)
+    cpu.init_weights(7)
+    dev = torch.device("cuda", 0)
+    gpu = model_cls(cfg, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
+    gpu.load_state_dict({k: v.to(torch.bfloat16) for k, v in cpu.state_dict().items()})
+    cpu.load_state_dict({k: v.to(torch.bfloat16).float() for k, v in cpu.state_dict().items()})
+    lc, gc = _loss_and_grads(cpu, ids, seg)
+    lg, gg = _loss_and_grads(gpu, ids.to(dev), seg.to(dev) if seg is not None else None)
+    assert abs(lc.item() - lg.item()) < tol_loss, (lc, lg)
+    for n in gc:
+        rel = ((gg[n] - gc[n]).norm() / (gc[n].norm() + 1e-12)).item()
+        assert rel < tol_grad, (n, rel)
+
+
+@pytest.mark.parametrize("window", [None, 96])
+def test_phi3_head_dim96_hip_matches_cpu_reference(window):
+    """Phi-3 geometry (head_dim 96, fused qkv / gate_up, LongRoPE tables, optional sliding window) on
+    the D=96 HIP kernels against the fp32 torch path."""
+    from llm_training_amd.models.phi3 import Phi3, Phi3Config
+    factors = [1.0 + 0.05 * i for i in range(48)]
+    cfg = Phi3Config(vocab_size=2048, hidden_size=384, intermediate_size=768, num_hidden_layers=2,
+                     num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=2048,
+                     original_max_position_embeddings=256, sliding_window=window,
+                     rope_scaling={"type": "longrope", "short_factor": factors, "long_factor": factors})
+    ids = torch.randint(0, cfg.vocab_size, (2, 384))
+    _hip_vs_cpu(Phi3, cfg, ids)
+
+
+def test_async_optimizer_stream_matches_synchronous():
+    """AdamW on its own stream (overlapping the next forward) must train exactly like the synchronous
+    update up to the run-to-run noise of atomics (embedding backward): a read-before-update race would
+    show up as a full learning-rate step of difference."""
+    dev = torch.device("cuda", 0)
+    cfg = _cfg(num_hidden_layers=2)
+    outs = []
+    for overlap in (False, False, True):
+        torch.manual_seed(0)
+        m = Llama(cfg, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
+        m.init_weights(5)
+        eng = DataParallelEngine(m, ParallelContext.single(dev), 0, lr=1e-3, overlap_step=overlap)
+        lm = CLM({"model": None})
+        lm.model = m
+        g = torch.Generator(device=dev).manual_seed(11)
+        losses = []
+        for _ in range(4):
+            ids = torch.randint(0, cfg.vocab_size, (1, 512), device=dev, generator=g)
+            eng.begin_step(1)
+            eng.zero_grad()
+            loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+            loss.backward()
+            eng.finish_backward()
+            eng.clip_and_scale(1.0)
+            eng.step(1e-3)
+            losses.append(loss.item())
+        eng.wait_params()
+        outs.append((losses, {k: v.float().cpu() for k, v in m.state_dict().items()}))
+    for a, b in zip(outs[0][0], outs[2][0]):
+        assert abs(a - b) < 1e-4 * abs(a), (outs[0][0], outs[2][0])
+    num_a = num_n = den = 0.0
+    for k in outs[0][1]:
+        ref, again, asy = outs[0][1][k], outs[1][1][k], outs[2][1][k]
+        num_n += (again - ref).norm().item() ** 2  # sync vs sync: atomics (embedding backward) + Adam
+        num_a += (asy - ref).norm().item() ** 2
+        den += ref.norm().item() ** 2
+    noise, rel = (num_n / den) ** 0.5, (num_a / den) ** 0.5
+    assert rel <= 3 * noise + 1e-4, (rel, noise)
+
+
+def test_dpo_orpo_hip_match_cpu_reference():
+    from llm_training_amd.lms.preference import DPO, ORPO
+    torch.manual_seed(0)
+    cfg = _cfg(num_hidden_layers=2)
+    dev = torch.device("cuda", 0)
+    B, S = 2, 256
+    ids = torch.randint(0, cfg.vocab_size, (2 * B, S))
+    labels = ids.clone()
+    labels[:, :40] = -100
+    batch = {"chosen_input_ids": ids[:B], "chosen_labels": labels[:B], "rejected_input_ids": ids[B:],
+             "rejected_labels": labels[B:], "chosen_attention_mask": torch.ones(B, S, dtype=torch.long),
+             "rejected_attention_mask": torch.ones(B, S, dtype=torch.long)}
+    src = Llama(cfg, ParallelContext.single(), dtype=torch.float32)
+    src.init_weights(9)
+    sd = {k: v.to(torch.bfloat16) for k, v in src.state_dict().items()}
+    for cls in (DPO, ORPO):
+        res = []
+        for device in ("cpu", "cuda"):
+            d = torch.device(device, 0) if device == "cuda" else torch.device("cpu")
+            dtype = torch.bfloat16 if device == "cuda" else torch.float32
+            m = Llama(cfg, ParallelContext.single(d), dtype=dtype, device=d)
+            m.load_state_dict({k: v.to(dtype) for k, v in sd.items()})
+            lm = cls({"model": None, "beta": 0.1})
+            lm.model = m
+            if cls is DPO:
+                lm.ref_model = copy.deepcopy(m).eval()
+                for p in lm.ref_model.parameters():
+                    p.requires_grad_(False)
+            b = {k: v.to(d) for k, v in batch.items()}
+            loss, metrics, _ = lm.training_step(b)
+            loss.backward()
+            gn = torch.sqrt(sum((p.grad.float() ** 2).sum() for p in m.parameters() if p.grad is not None))
+            res.append((loss.item(), gn.item()))
+        (lc, gc), (lg, gg) = res
+        assert abs(lc - lg) < 3e-2, (cls.__name__, lc, lg)
+        assert abs(gc - gg) / gc < 0.1, (cls.__name__, gc, gg)
