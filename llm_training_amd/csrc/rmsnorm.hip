@@ -213,8 +213,11 @@ extern "C" hipError_t llmt_rmsnorm_fwd(const void* x, const void* res, const voi
 
 // dw_part must hold nblocks*H floats where nblocks = llmt_rmsnorm_bwd_nblocks(T).
 extern "C" int llmt_rmsnorm_bwd_nblocks(int T) {
-  int nblk = (T + 31) / 32;  // >= 32 rows per block so partial traffic stays << activation traffic
-  if (nblk > 256) nblk = 256;
+  // >= 16 rows per block and 2 blocks per CU: one block per CU (the old 256 cap) left the
+  // memory pipe under-filled (1.8 TB/s at T=8192, H=4096); the fp32 partials (nblk*H*4 B) stay well
+  // below the activation traffic (3*T*H*2 B)
+  int nblk = (T + 15) / 16;
+  if (nblk > 512) nblk = 512;
   if (nblk < 1) nblk = 1;
   return nblk;
 }
