@@ -34,6 +34,8 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
                                int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh,
                                int64_t o_sb, int64_t o_ss, int64_t o_sh, float scale, int causal, int window,
                                hipStream_t stream);
+hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N, int K,
+                     int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream);
 int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D);
 hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                                const float* lse, float* delta, const int* seg, void* dq, void* dk, void* dv,
@@ -253,6 +255,40 @@ void sumsq_(const at::Tensor& x, at::Tensor out) {
         "sumsq");
 }
 
+// ---------------------------------------------------------------- GEMM
+// c (+)= X . Y^T with X = a ([M, K], or [K, M] when a_mn) and Y = b ([N, K], or [K, N] when b_mn);
+// bf16 operands, c bf16 or fp32 [M, N] with unit column stride.
+inline int64_t row_ld(const at::Tensor& t) {
+  // a single row's stride is arbitrary in torch: any multiple of 8 covering the row works
+  return t.size(0) > 1 ? t.stride(0) : (t.size(1) + 7) / 8 * 8;
+}
+
+void gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool a_mn, bool b_mn, bool accumulate) {
+  check_bf16_cuda(a, "a");
+  check_bf16_cuda(b, "b");
+  TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
+              "gemm: c must be a bf16 or fp32 GPU tensor");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm: operands must be 2-D");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm: unit column stride required");
+  const int64_t M = a_mn ? a.size(1) : a.size(0), K = a_mn ? a.size(0) : a.size(1);
+  const int64_t N = b_mn ? b.size(1) : b.size(0), Kb = b_mn ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm: contraction sizes differ (", K, " vs ", Kb, ")");
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: output must be [", M, ", ", N, "]");
+  TORCH_CHECK(K > 0 && K % 32 == 0, "gemm: K must be a positive multiple of 32");
+  TORCH_CHECK(N % 4 == 0, "gemm: N must be a multiple of 4");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm: dimension too large");
+  const int64_t lda = row_ld(a), ldb = row_ld(b), ldc = c.size(0) > 1 ? c.stride(0) : (N + 3) / 4 * 4;
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0, "gemm: leading dimensions must be 16-byte multiples");
+  TORCH_CHECK(256 * lda * 2 < 0x7fffffffLL && 256 * ldb * 2 < 0x7fffffffLL, "gemm: leading dimension too large");
+  for (const at::Tensor* t : {&a, &b, static_cast<const at::Tensor*>(&c)})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "gemm: operands must be 16-byte aligned");
+  const int out_mode = c.scalar_type() == at::kFloat ? (accumulate ? 2 : 1) : (accumulate ? 3 : 0);
+  if (M == 0 || N == 0) return;
+  check(llmt_gemm(a.data_ptr(), b.data_ptr(), c.data_ptr(), a_mn ? 1 : 0, b_mn ? 1 : 0, out_mode, (int)M, (int)N,
+                  (int)K, lda, ldb, ldc, cur_stream()),
+        "gemm");
+}
+
 // ---------------------------------------------------------------- flash attention
 // q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (any batch/seq/head strides, unit stride on D).
 // seg: optional int32 [B, S] segment ids (0 = padding): attention is restricted to equal ids.
@@ -331,6 +367,7 @@ TORCH_LIBRARY(llmt, m) {
       "adamw_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? pout, float lr, float b1, float b2, "
       "float eps, float wd, int step, Tensor? gscale) -> ()");
   m.def("sumsq_(Tensor x, Tensor(a!) out) -> ()");
+  m.def("gemm_(Tensor a, Tensor b, Tensor(a!) c, bool a_mn, bool b_mn, bool accumulate) -> ()");
   m.def(
       "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window) -> (Tensor, "
       "Tensor)");
@@ -348,6 +385,7 @@ TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("cross_entropy_", &cross_entropy_);
   m.impl("adamw_", &adamw_);
   m.impl("sumsq_", &sumsq_);
+  m.impl("gemm_", &gemm_);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
 }

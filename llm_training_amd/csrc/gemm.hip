@@ -1,0 +1,357 @@
+// bf16 GEMM for gfx950 (CDNA4) with fp32 accumulation, in all three layouts of a linear layer:
+//
+//   C[M, N] (+)= X . Y^T,   X(m, k) and Y(n, k) read from row-major bf16 matrices, each either
+//   K-major (element (i, k) at P[i * ld + k]) or MN-major (element (i, k) at P[k * ld + i]).
+//
+//   forward  y  = x . W^T   : X = x  [T, K]  K-major,   Y = W [N, K]   K-major
+//   dgrad    dx = dy . W    : X = dy [T, N]  K-major,   Y = W [N, K]   MN-major (contraction = W's rows)
+//   wgrad    dW = dy^T . x  : X = dy [T, N]  MN-major,  Y = x [T, K]   MN-major (contraction = tokens)
+//
+// The projections and the lm_head of the models are these GEMMs. hipBLASLt's default
+// solutions reach 1.0 (forward), 1.37 (dgrad) and 1.5 (wgrad) PF/s on the Llama-3-8B shapes
+// (profiles/r1_llama8b_1gpu_v2_kernel_stats.md, profiles/r1_gemm_layouts_random_data.jsonl).
+//
+// Structure (one 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N), 256 x 256 output tile):
+//  * K advances in 32-deep stages. Each stage's X and Y tiles (16 KB each) arrive by LDS-DMA
+//    (`buffer_load_dwordx4 ... lds`, one 1-KB piece per wave-instruction) into a ring of kNS LDS slots,
+//    kNS-1 stages ahead of the MFMAs, behind a counted `s_waitcnt vmcnt` and ONE raw barrier per stage:
+//    the loads never drain inside the loop.
+//  * fragments are software-pipelined one stage ahead: after the barrier that publishes stage t+1 the
+//    wave issues its LDS reads of stage t+1, then runs the 32 MFMAs of stage t on the registers read one
+//    iteration earlier, so LDS latency and the DMA issue hide under the MFMAs.
+//  * LDS images are lane-linear (the DMA writes base + 16 * lane); bank conflicts are removed by
+//    permuting the SOURCE address and reading through the same involution:
+//      K-major image [256 rows][32 k] (64-B rows): 16-B chunk c of row r at chunk c ^ (-(r >> 2) & 3);
+//        fragments by ds_read_b128, every 16-lane group on 16 distinct bank slots.
+//      MN-major image [32 k][256 mn] (512-B rows): 32-B unit u of k-row k at unit u ^ ((k & 3) | (k >> 1 & 4));
+//        fragments by two ds_read_b64_tr_b16 (hardware transpose: 4 k-rows x 16 columns per 16 lanes),
+//        the 8 k-rows read by each 32-lane half land on 8 distinct 32-B bank units.
+//  * MFMA v_mfma_f32_16x16x32_bf16 with the operands swapped (Y as the MFMA A operand), so each lane's
+//    accumulator holds 4 consecutive OUTPUT COLUMNS of one row: 8-byte row stores, no transpose.
+//  * blockIdx -> tile: bijective XCD remap (blocks b and b+8 share an XCD, so each XCD gets a contiguous
+//    run of tiles), then a grouped order of kGM row tiles: the 32 workgroups resident on one XCD share
+//    4 X panels and 8 Y panels through that XCD's L2.
+//  * the stage base is rebased every stage (scalar descriptor), so only offsets inside one stage's
+//    window must fit 32 bits; reads past the end of an operand come back as zeros (descriptor range
+//    check). K must be a multiple of 32; rows / columns past M / N are computed on padding and not stored.
+#include "common.h"
+
+namespace llmt {
+namespace {
+
+typedef __bf16 gbf8 __attribute__((ext_vector_type(8)));
+typedef short gs4 __attribute__((ext_vector_type(4)));
+typedef float gf4 __attribute__((ext_vector_type(4)));
+typedef unsigned int gu4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 256, kBN = 256, kBK = 32, kNS = 5, kThreads = 512;
+constexpr int kImg = kBM * kBK * 2;  // 16 KB: one operand's image of one stage
+constexpr int kSlot = 2 * kImg;      // X image + Y image
+constexpr int kDmaPerStage = 4;      // DMA instructions per wave per stage
+constexpr int kGM = 4;               // row tiles per group of the tile order
+
+__device__ __forceinline__ int kswz(int r) { return (-(r >> 2)) & 3; }
+__device__ __forceinline__ int mswz(int k) { return (k & 3) | ((k >> 1) & 4); }
+
+struct GRsrc {
+  gu4 w;
+};
+
+// Raw buffer descriptor (no swizzle, range-checked): loads past `bytes` return zeros. Offsets never
+// exceed one stage's window, so clamping a larger extent to 2^31 - 1 cuts nothing that is read.
+__device__ __forceinline__ GRsrc g_rsrc(const char* base, int64_t bytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  GRsrc r;
+  r.w[0] = (uint32_t)p;
+  r.w[1] = (uint32_t)(p >> 32) & 0xffffu;
+  r.w[2] = (uint32_t)(bytes > 0x7fffffffLL ? 0x7fffffffLL : (bytes < 0 ? 0 : bytes));
+  r.w[3] = 0x00020000u;
+  return r;
+}
+
+__device__ __forceinline__ uint32_t g_lds(const char* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(const_cast<char*>(p));
+}
+
+// 16 bytes per lane global -> LDS (lds_base + 16 * lane). Issued from inline asm so hipcc does not treat
+// it as an LDS write it must drain before every ds_read; the counted waits below order it.
+__device__ __forceinline__ void g_dma16(const GRsrc& r, uint32_t lds_base, int voff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "s"(lds_base), "v"(voff), "s"(r.w)
+               : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void g_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `stages` later stages' DMAs of this wave are outstanding
+__device__ __forceinline__ void g_wait_stages(int stages) {
+  static_assert(kNS - 2 <= 3, "extend the switch");
+  if (stages >= 3)
+    g_wait_vm<3 * kDmaPerStage>();
+  else if (stages == 2)
+    g_wait_vm<2 * kDmaPerStage>();
+  else if (stages == 1)
+    g_wait_vm<kDmaPerStage>();
+  else
+    g_wait_vm<0>();
+}
+
+// This wave's LDS reads retired, then a barrier that leaves the DMA ring in flight (no vmcnt(0)). The
+// lgkmcnt(0) is the builtin (vmcnt/expcnt fields at their maxima) so hipcc's wait bookkeeping knows
+// every earlier fragment read has landed and does not stall the next MFMAs on the reads issued after
+// the barrier; the barrier itself is asm with a memory clobber so no LDS access moves across it.
+__device__ __forceinline__ void g_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
+  asm volatile("s_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ gs4 lds_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) gs4*)(p));
+}
+
+// One operand (X or Y): where this lane's two DMA pieces of a stage come from, how the stage base
+// advances, and how MFMA fragments are read back from the stage image.
+template <bool MN>
+struct Opnd {
+  const char* base;  // stage 0 tile origin
+  int64_t extent;    // readable bytes from `base`
+  int64_t step;      // bytes per stage
+  int off0, off1;    // this lane's source byte offsets of its wave's two 1-KB pieces
+  int frag_off;      // lane-constant part of the fragment read address
+
+  // P: row-major matrix with leading dimension ld; rows = its row count; cols = its column count
+  // (K-major: rows = output rows/cols of C, cols = K; MN-major: rows = K, cols = output rows/cols).
+  __device__ __forceinline__ void init(const bf16* P, int64_t ld, int64_t rows, int64_t cols, int tile0, int w,
+                                       int lane) {
+    if constexpr (!MN) {
+      base = reinterpret_cast<const char*>(P + (int64_t)tile0 * ld);
+      extent = ((rows - 1 - tile0) * ld + cols) * 2;
+      step = kBK * 2;
+      const int row = w * 16 + (lane >> 2);
+      const int ch = (lane & 3) ^ kswz(row);
+      off0 = row * (int)ld * 2 + ch * 16;
+      off1 = off0 + 128 * (int)ld * 2;
+      const int fr = lane & 15;
+      frag_off = fr * 64 + (((lane >> 4) ^ kswz(fr)) * 16);
+    } else {
+      base = reinterpret_cast<const char*>(P + tile0);
+      extent = ((rows - 1) * ld + cols - tile0) * 2;
+      step = (int64_t)kBK * ld * 2;
+      const int krow = 2 * w + (lane >> 5);
+      const int pc = lane & 31;
+      const int lc = 2 * ((pc >> 1) ^ mswz(krow)) + (pc & 1);
+      off0 = krow * (int)ld * 2 + lc * 16;
+      off1 = off0 + 16 * (int)ld * 2;  // k-rows +16: same swizzle
+      const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+      frag_off = (8 * g + q) * 512 + 8 * p;  // + 32 * (unit ^ h) per fragment, h = q | (g & 1) << 2
+    }
+  }
+
+  __device__ __forceinline__ GRsrc rsrc(int t) const { return g_rsrc(base + t * step, extent - t * step); }
+
+  // fragment of the 16-row (output index) tile starting at `tile` (multiple of 16) of the stage image
+  __device__ __forceinline__ gbf8 frag(const char* img, int tile, int lane) const {
+    if constexpr (!MN) {
+      return *reinterpret_cast<const gbf8*>(img + tile * 64 + frag_off);
+    } else {
+      const int h = ((lane & 15) >> 2) | (((lane >> 4) & 1) << 2);
+      const char* p = img + frag_off + (((tile >> 4) ^ h) << 5);
+      const gs4 lo = lds_tr16(p), hi = lds_tr16(p + 4 * 512);
+      return __builtin_bit_cast(gbf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+  }
+};
+
+struct GemmArgs {
+  const bf16* x;
+  const bf16* y;
+  void* c;
+  int M, N, K;
+  int64_t ldx, ldy, ldc;
+};
+
+__device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
+  const int nbm = (M + kBM - 1) / kBM, nbn = (N + kBN - 1) / kBN, nwg = nbm * nbn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  const int per = kGM * nbn;
+  const int g = wg / per;
+  const int first = g * kGM;
+  const int gsz = min(nbm - first, kGM);
+  const int in = wg - g * per;
+  tm = first + in % gsz;
+  tn = in / gsz;
+}
+
+// OUT: 0 = bf16 store, 1 = fp32 store, 2 = fp32 accumulate, 3 = bf16 accumulate (C = bf16(C + X.Y^T))
+template <bool XMN, bool YMN, int OUT>
+__global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[kNS * kSlot];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases live in SGPRs
+  int tm, tn;
+  tile_coords(g.M, g.N, tm, tn);
+  const int row0 = tm * kBM, col0 = tn * kBN;
+
+  Opnd<XMN> X;
+  Opnd<YMN> Y;
+  if constexpr (!XMN)
+    X.init(g.x, g.ldx, g.M, g.K, row0, w, lane);
+  else
+    X.init(g.x, g.ldx, g.K, g.M, row0, w, lane);
+  if constexpr (!YMN)
+    Y.init(g.y, g.ldy, g.N, g.K, col0, w, lane);
+  else
+    Y.init(g.y, g.ldy, g.K, g.N, col0, w, lane);
+  const uint32_t lbase = g_lds(smem);
+
+  auto issue = [&](int t, int slot) {
+    const uint32_t s = lbase + (uint32_t)(slot * kSlot);
+    const GRsrc rx = X.rsrc(t), ry = Y.rsrc(t);
+    g_dma16(rx, s + w * 1024, X.off0);
+    g_dma16(rx, s + (w + 8) * 1024, X.off1);
+    g_dma16(ry, s + kImg + w * 1024, Y.off0);
+    g_dma16(ry, s + kImg + (w + 8) * 1024, Y.off1);
+  };
+
+  const int wm = w >> 2, wn = w & 3;
+  struct Frags {
+    gbf8 y[4];  // MFMA A operand: output columns
+    gbf8 x[8];  // MFMA B operand: output rows
+  };
+  auto read_frags = [&](Frags& f, const char* slot) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.y[j] = Y.frag(slot + kImg, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f.x[i] = X.frag(slot, wm * 128 + i * 16, lane);
+  };
+
+  gf4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = gf4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const Frags& f) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.y[j], f.x[i], acc[i][j], 0, 0, 0);
+  };
+
+  const int nk = g.K / kBK;
+  // prologue: stages 0 .. kNS-2 in flight, stage 0's fragments in registers
+#pragma unroll
+  for (int s = 0; s < kNS - 1; ++s)
+    if (s < nk) issue(s, s);
+  g_wait_stages(min(nk - 1, kNS - 2));
+  g_barrier();
+  Frags f0, f1;
+  read_frags(f0, smem);
+
+  int slot_next = 1;         // slot of stage t+1
+  int slot_issue = kNS - 1;  // slot of stage t+kNS-1 (= the slot stage t-1 used)
+  // Iteration t: publish stage t+1 (its reads of the previous slot user retired before this barrier),
+  // refill the ring with stage t+kNS-1, read stage t+1's fragments, MFMA stage t.
+  // (every body reads the next stage unconditionally, so hipcc's lgkmcnt ladder before the MFMAs counts
+  // the just-issued reads as outstanding; the last stage is peeled off below)
+  auto body = [&](int t, Frags& cur, Frags& nxt) {
+    g_wait_stages(min(nk - 1, t + kNS - 2) - (t + 1));
+    g_barrier();
+    if (t + kNS - 1 < nk) issue(t + kNS - 1, slot_issue);
+    read_frags(nxt, smem + slot_next * kSlot);
+    slot_next = slot_next + 1 == kNS ? 0 : slot_next + 1;
+    slot_issue = slot_issue + 1 == kNS ? 0 : slot_issue + 1;
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs (and the register budget flat)
+    mma(cur);
+  };
+  int t = 0;
+  for (; t + 2 < nk; t += 2) {
+    body(t, f0, f1);
+    body(t + 1, f1, f0);
+  }
+  if (t + 1 < nk) {  // two stages left
+    body(t, f0, f1);
+    f0 = f1;
+  }
+  mma(f0);
+
+  // epilogue: lane holds C[m][n .. n+3], m = row (lane & 15) of m-tile i, n = 4 * (lane >> 4) of n-tile j
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = row0 + wm * 128 + i * 16 + fr;
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = col0 + wn * 64 + j * 16 + fc * 4;
+      if (n >= g.N) continue;
+      const gf4 v = acc[i][j];
+      if constexpr (OUT == 0 || OUT == 3) {
+        uint2* p = reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(g.c) + (int64_t)m * g.ldc + n);
+        float a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+        if constexpr (OUT == 3) {
+          const uint2 o = *p;
+          a0 += bf16_lo(o.x);
+          a1 += bf16_hi(o.x);
+          a2 += bf16_lo(o.y);
+          a3 += bf16_hi(o.y);
+        }
+        uint2 o;
+        o.x = pack_bf16x2(a0, a1);
+        o.y = pack_bf16x2(a2, a3);
+        *p = o;
+      } else {
+        float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.c) + (int64_t)m * g.ldc + n);
+        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+        if constexpr (OUT == 2) {
+          const float4 c = *p;
+          o.x += c.x;
+          o.y += c.y;
+          o.z += c.z;
+          o.w += c.w;
+        }
+        *p = o;
+      }
+    }
+  }
+}
+
+template <bool XMN, bool YMN>
+hipError_t launch(const GemmArgs& a, int out_mode, hipStream_t stream) {
+  const int64_t nwg = (int64_t)((a.M + kBM - 1) / kBM) * ((a.N + kBN - 1) / kBN);
+  const dim3 grid((unsigned)nwg), block(kThreads);
+  switch (out_mode) {
+    case 0: gemm_kernel<XMN, YMN, 0><<<grid, block, 0, stream>>>(a); break;
+    case 1: gemm_kernel<XMN, YMN, 1><<<grid, block, 0, stream>>>(a); break;
+    case 2: gemm_kernel<XMN, YMN, 2><<<grid, block, 0, stream>>>(a); break;
+    default: gemm_kernel<XMN, YMN, 3><<<grid, block, 0, stream>>>(a); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace llmt
+
+// Host launcher: C[M, N] (+)= X . Y^T. x_mn / y_mn select MN-major operands (x is [K, M] / y is [K, N]);
+// otherwise x is [M, K] and y is [N, K]. Preconditions (checked by the binding): K % 32 == 0, N % 4 == 0,
+// ldx / ldy % 8 == 0, ldc % 4 == 0, 16-byte aligned x / y / c, 256 * ld * 2 < 2^31.
+extern "C" hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N,
+                                int K, int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream) {
+  using namespace llmt;
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (K <= 0 || K % kBK != 0 || N % 4 != 0 || out_mode < 0 || out_mode > 3) return hipErrorInvalidValue;
+  if (ldx % 8 || ldy % 8 || ldc % 4) return hipErrorInvalidValue;
+  if (256 * ldx * 2 >= 0x7fffffffLL || 256 * ldy * 2 >= 0x7fffffffLL) return hipErrorInvalidValue;
+  GemmArgs a{reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(y), c, M, N, K, ldx, ldy, ldc};
+  if (!x_mn && !y_mn) return launch<false, false>(a, out_mode, stream);
+  if (!x_mn && y_mn) return launch<false, true>(a, out_mode, stream);
+  if (x_mn && y_mn) return launch<true, true>(a, out_mode, stream);
+  return launch<true, false>(a, out_mode, stream);
+}

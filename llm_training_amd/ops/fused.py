@@ -15,6 +15,7 @@ flash-attn calls of src/llm_training/ops/attention_op.py.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch.autograd import Function
@@ -25,9 +26,66 @@ from .native import lib, use_native
 # ----------------------------------------------------------------------------- gradient-buffer helpers
 
 
+# ----------------------------------------------------------------------------- GEMM dispatch
+# The three GEMMs of a linear layer run on the hand-written gfx950 kernel (csrc/gemm.hip) or on
+# hipBLASLt through torch.matmul. ``LLMT_GEMM`` picks per layout: "hip" (all), "blas" (none) or a comma
+# list of fwd,dgrad,wgrad. Shapes the kernel does not take (K % 32, N % 4, unaligned or strided
+# operands) always go to the library.
+_GEMM_ENV = os.environ.get("LLMT_GEMM", "hip").strip().lower()
+HIP_GEMM_LAYOUTS = ({"fwd", "dgrad", "wgrad"} if _GEMM_ENV == "hip" else
+                    set() if _GEMM_ENV in ("blas", "", "none") else {x.strip() for x in _GEMM_ENV.split(",")})
+
+
+def _gemm_operand_ok(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1
+            and (t.size(0) <= 1 or t.stride(0) % 8 == 0) and t.data_ptr() % 16 == 0)
+
+
+def _hip_gemm_ok(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> bool:
+    if layout not in HIP_GEMM_LAYOUTS or k % 32 or k == 0 or ncols % 4:
+        return False
+    return all(_gemm_operand_ok(t) for t in ts) and use_native(ts[0])
+
+
+def mm_nt(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x2 [M, K] @ w[N, K]^T -> [M, N] (forward of a linear layer)."""
+    if _hip_gemm_ok("fwd", x2.shape[1], w.shape[0], x2, w):
+        y = torch.empty(x2.shape[0], w.shape[0], device=x2.device, dtype=x2.dtype)
+        lib().gemm_(x2, w, y, False, False, False)
+        return y
+    return torch.matmul(x2, w.t())
+
+
+def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """dy2 [M, N] @ w [N, K] -> [M, K] (input gradient of a linear layer)."""
+    if _hip_gemm_ok("dgrad", dy2.shape[1], w.shape[1], dy2, w) and (out is None or _gemm_operand_ok(out)):
+        if out is None:
+            out = torch.empty(dy2.shape[0], w.shape[1], device=dy2.device, dtype=dy2.dtype)
+        lib().gemm_(dy2, w, out, False, True, False)
+        return out
+    if out is None:
+        return torch.matmul(dy2, w)
+    return torch.matmul(dy2, w, out=out)
+
+
 def _wgrad_mm(w: torch.Tensor, a_t: torch.Tensor, b: torch.Tensor):
-    """dW = a_t @ b. Writes into ``w.main_grad`` if present (returns None), else returns dW."""
+    """dW = a_t @ b. Writes into ``w.main_grad`` if present (returns None), else returns dW.
+
+    ``a_t`` is the transpose view of dy [T, N]; on the HIP path both operands are read token-major
+    (MN-major) straight from dy and x and the output is stored / accumulated in the buffer's dtype.
+    """
     mg = getattr(w, "main_grad", None)
+    a = a_t.t()
+    if (_hip_gemm_ok("wgrad", a.shape[0], b.shape[1], a, b)
+            and (mg is None or (mg.is_contiguous() and mg.dtype in (torch.bfloat16, torch.float32)))):
+        if mg is None:
+            out = torch.empty(a.shape[1], b.shape[1], device=a.device, dtype=w.dtype)
+            lib().gemm_(a, b, out, True, True, False)
+            return out
+        added = bool(getattr(w, "grad_added", False))
+        lib().gemm_(a, b, mg.view(a.shape[1], b.shape[1]), True, True, added)
+        w.grad_added = True
+        return None
     if mg is None:
         return (a_t @ b).to(w.dtype)
     mg2 = mg.view(a_t.shape[0], b.shape[1])
@@ -66,7 +124,7 @@ class _LinearFn(Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
-        y = torch.matmul(x, w.t())
+        y = mm_nt(x.reshape(-1, x.shape[-1]), w).view(*x.shape[:-1], w.shape[0])
         if b is not None:
             y = y + b
         return y
@@ -77,7 +135,7 @@ class _LinearFn(Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dy, w)
+            dx = mm_nn(dy2 if dy2.stride(-1) == 1 else dy2.contiguous(), w).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _wgrad_mm(w, dy2.t(), x.reshape(-1, x.shape[-1]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -362,7 +420,7 @@ class _FusedLinearCEFn(Function):
         grads = []
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
-            lg = torch.matmul(h[s0:s1], w.t())
+            lg = mm_nt(h[s0:s1], w)
             _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, inv_n, True)
             loss_rows[s0:s1] = lr
             grads.append(lg)
@@ -381,7 +439,7 @@ class _FusedLinearCEFn(Function):
             s0 = i * chunk
             s1 = s0 + lg.shape[0]
             if dh is not None:
-                torch.matmul(lg, w, out=dh[s0:s1])
+                mm_nn(lg, w, out=dh[s0:s1])
             if ctx.needs_input_grad[1]:
                 r = _wgrad_mm(w, lg.t(), hs[s0:s1])
                 if r is not None:
@@ -440,7 +498,7 @@ class _LinearLogpsFn(Function):
         out = torch.empty(N, device=h.device, dtype=torch.float32)
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
-            lg = torch.matmul(h[s0:s1], w.t())
+            lg = mm_nt(h[s0:s1], w)
             _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, None, False)
             out[s0:s1] = -lr
         ctx.save_for_backward(h, w, labels)
@@ -458,9 +516,9 @@ class _LinearLogpsFn(Function):
         dw_acc = None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
-            lg = torch.matmul(h[s0:s1], w.t())
+            lg = mm_nt(h[s0:s1], w)
             L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, coef[s0:s1], None, True)
-            torch.matmul(lg, w, out=dh[s0:s1])
+            mm_nn(lg, w, out=dh[s0:s1])
             if ctx.needs_input_grad[1]:
                 r = _wgrad_mm(w, lg.t(), h[s0:s1])
                 if r is not None:

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 from torch.autograd import Function
 
-from ..ops.fused import _wgrad_mm
+from ..ops.fused import _wgrad_mm, mm_nn, mm_nt
 from ..ops.native import lib, use_native
 
 
@@ -67,7 +67,7 @@ class _VPFusedCE(Function):
         lgs, lses, tgts = [], [], []
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
-            lg = torch.matmul(h[s0:s1], w.t())
+            lg = mm_nt(h[s0:s1], w)
             lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
             lgs.append(lg)
             lses.append(lse)
@@ -95,7 +95,7 @@ class _VPFusedCE(Function):
         for i, lg in enumerate(lgs):
             s0 = i * chunk
             s1 = s0 + lg.shape[0]
-            torch.matmul(lg, w, out=dh[s0:s1])
+            mm_nn(lg, w, out=dh[s0:s1])
             r = _wgrad_mm(w, lg.t(), hs[s0:s1])
             if r is not None:
                 dw = r if dw is None else dw + r
@@ -111,7 +111,7 @@ class _VPLogps(Function):
         lses, tgts = [], []
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
-            lg = torch.matmul(h[s0:s1], w.t())
+            lg = mm_nt(h[s0:s1], w)
             lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
             lses.append(lse)
             tgts.append(tgt)
@@ -134,9 +134,9 @@ class _VPLogps(Function):
         dw = None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
-            lg = torch.matmul(h[s0:s1], w.t())
+            lg = mm_nt(h[s0:s1], w)
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), coef[s0:s1], None, native)
-            torch.matmul(lg, w, out=dh[s0:s1])
+            mm_nn(lg, w, out=dh[s0:s1])
             r = _wgrad_mm(w, lg.t(), h[s0:s1])
             if r is not None:
                 dw = r if dw is None else dw + r

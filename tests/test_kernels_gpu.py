@@ -226,3 +226,54 @@ def test_rope_attention_fused_matches_reference():
     (orf * do.float()).sum().backward()
     assert _rel(o, orf) < 2e-2
     assert _rel(qkv.grad, qr.grad) < 4e-2
+
+
+# ----------------------------------------------------------------------------- GEMM (csrc/gemm.hip)
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("out", ["bf16", "bf16_acc", "fp32", "fp32_acc"])
+@pytest.mark.parametrize("M,N,K", [(520, 776, 352), (64, 128, 32), (8, 264, 96), (1024, 512, 4096)])
+def test_gemm_layouts(layout, out, M, N, K):
+    # nt = forward (x . W^T), nn = dgrad (dy . W), tn = wgrad (dy^T . x); partial tiles on every edge
+    torch.manual_seed(0)
+    xb = torch.randn(M, K, device=DEV).bfloat16()
+    yb = torch.randn(N, K, device=DEV).bfloat16()
+    a = xb.t().contiguous() if layout == "tn" else xb
+    b = yb if layout == "nt" else yb.t().contiguous()
+    dt = torch.float32 if out.startswith("fp32") else torch.bfloat16
+    acc = out.endswith("acc")
+    c0 = torch.randn(M, N, device=DEV).to(dt)
+    c = c0.clone()
+    lib().gemm_(a, b, c, layout == "tn", layout != "nt", acc)
+    want = xb.float() @ yb.float().t() + (c0.float() if acc else 0.0)
+    assert _rel(c, want) < (1e-4 if dt == torch.float32 else 1e-2)
+
+
+def test_gemm_strided_operands():
+    # row-strided views (leading dimension > row length), as the fused CE heads and TP slices pass them
+    torch.manual_seed(0)
+    M, N, K = 300, 200, 160
+    xw = torch.randn(M, K + 64, device=DEV).bfloat16()
+    yw = torch.randn(N, K + 32, device=DEV).bfloat16()
+    cw = torch.zeros(M, N + 40, device=DEV, dtype=torch.bfloat16)
+    x, y, c = xw[:, :K], yw[:, 8:K + 8], cw[:, :N]
+    lib().gemm_(x, y, c, False, False, False)
+    assert _rel(c, x.float() @ y.float().t()) < 1e-2
+    assert cw[:, N:].abs().max().item() == 0
+
+
+def test_linear_hip_gemm_grads_into_grad_buffer():
+    torch.manual_seed(0)
+    T, K, N = 320, 256, 384
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16().requires_grad_(True)
+    w.main_grad = torch.zeros(N, K, device=DEV, dtype=torch.float32)
+    w.grad_added = False
+    xs = [torch.randn(T, K, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(2)]
+    dys = [torch.randn(T, N, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+    for x, dy in zip(xs, dys):
+        y = F_.linear(x, w)
+        assert _rel(y, x.float() @ w.float().t()) < 1e-2
+        y.backward(dy)
+    assert w.grad is None
+    assert _rel(w.main_grad, sum(dy.float().t() @ x.float() for x, dy in zip(xs, dys))) < 1e-3
+    for x, dy in zip(xs, dys):
+        assert _rel(x.grad, dy.float() @ w.float()) < 1e-2
