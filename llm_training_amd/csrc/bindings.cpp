@@ -273,6 +273,7 @@ void gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool a_mn, bo
   const int64_t M = a_mn ? a.size(1) : a.size(0), K = a_mn ? a.size(0) : a.size(1);
   const int64_t N = b_mn ? b.size(1) : b.size(0), Kb = b_mn ? b.size(0) : b.size(1);
   TORCH_CHECK(K == Kb, "gemm: contraction sizes differ (", K, " vs ", Kb, ")");
+  TORCH_CHECK(b_mn || !a_mn, "gemm: an MN-major a needs an MN-major b");
   TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: output must be [", M, ", ", N, "]");
   TORCH_CHECK(K > 0 && K % 32 == 0, "gemm: K must be a positive multiple of 32");
   TORCH_CHECK(N % 4 == 0, "gemm: N must be a multiple of 4");

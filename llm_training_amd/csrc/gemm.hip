@@ -44,10 +44,10 @@ typedef short gs4 __attribute__((ext_vector_type(4)));
 typedef float gf4 __attribute__((ext_vector_type(4)));
 typedef unsigned int gu4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 256, kBN = 256, kBK = 32, kNS = 5, kThreads = 512;
+constexpr int kBM = 256, kBN = 256, kBK = 32, kNS = 5;
 constexpr int kImg = kBM * kBK * 2;  // 16 KB: one operand's image of one stage
 constexpr int kSlot = 2 * kImg;      // X image + Y image
-constexpr int kDmaPerStage = 4;      // DMA instructions per wave per stage
+constexpr int kPieces = 2 * kBM * kBK * 2 / 1024;  // 1-KB DMA pieces per stage (both operands)
 constexpr int kGM = 4;               // row tiles per group of the tile order
 
 __device__ __forceinline__ int kswz(int r) { return (-(r >> 2)) & 3; }
@@ -88,15 +88,16 @@ __device__ __forceinline__ void g_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// wait until at most `stages` later stages' DMAs of this wave are outstanding
+// wait until at most `stages` later stages' DMAs of this wave (D per stage) are outstanding
+template <int D>
 __device__ __forceinline__ void g_wait_stages(int stages) {
-  static_assert(kNS - 2 <= 3, "extend the switch");
+  static_assert(kNS - 2 <= 3 && 3 * D <= 63, "extend the switch / vmcnt range");
   if (stages >= 3)
-    g_wait_vm<3 * kDmaPerStage>();
+    g_wait_vm<3 * D>();
   else if (stages == 2)
-    g_wait_vm<2 * kDmaPerStage>();
+    g_wait_vm<2 * D>();
   else if (stages == 1)
-    g_wait_vm<kDmaPerStage>();
+    g_wait_vm<D>();
   else
     g_wait_vm<0>();
 }
@@ -114,14 +115,16 @@ __device__ __forceinline__ gs4 lds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) gs4*)(p));
 }
 
-// One operand (X or Y): where this lane's two DMA pieces of a stage come from, how the stage base
-// advances, and how MFMA fragments are read back from the stage image.
-template <bool MN>
+// One operand (X or Y): where this lane's DMA pieces of a stage come from, how the stage base
+// advances, and how MFMA fragments are read back from the stage image. The operand's stage image is
+// 16 pieces of 1 KB; with NW waves, wave w loads pieces w, w + NW, ... (NP = 16 / NW of them).
+template <bool MN, int NW>
 struct Opnd {
+  static constexpr int NP = 16 / NW;
   const char* base;  // stage 0 tile origin
   int64_t extent;    // readable bytes from `base`
   int64_t step;      // bytes per stage
-  int off0, off1;    // this lane's source byte offsets of its wave's two 1-KB pieces
+  int off[NP];       // this lane's source byte offsets of its wave's pieces
   int frag_off;      // lane-constant part of the fragment read address
 
   // P: row-major matrix with leading dimension ld; rows = its row count; cols = its column count
@@ -132,21 +135,25 @@ struct Opnd {
       base = reinterpret_cast<const char*>(P + (int64_t)tile0 * ld);
       extent = ((rows - 1 - tile0) * ld + cols) * 2;
       step = kBK * 2;
-      const int row = w * 16 + (lane >> 2);
-      const int ch = (lane & 3) ^ kswz(row);
-      off0 = row * (int)ld * 2 + ch * 16;
-      off1 = off0 + 128 * (int)ld * 2;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {  // piece j = rows 16j .. 16j+15
+        const int row = (w + NW * i) * 16 + (lane >> 2);
+        const int ch = (lane & 3) ^ kswz(row);
+        off[i] = row * (int)ld * 2 + ch * 16;
+      }
       const int fr = lane & 15;
       frag_off = fr * 64 + (((lane >> 4) ^ kswz(fr)) * 16);
     } else {
       base = reinterpret_cast<const char*>(P + tile0);
       extent = ((rows - 1) * ld + cols - tile0) * 2;
       step = (int64_t)kBK * ld * 2;
-      const int krow = 2 * w + (lane >> 5);
-      const int pc = lane & 31;
-      const int lc = 2 * ((pc >> 1) ^ mswz(krow)) + (pc & 1);
-      off0 = krow * (int)ld * 2 + lc * 16;
-      off1 = off0 + 16 * (int)ld * 2;  // k-rows +16: same swizzle
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {  // piece j = k-rows 2j, 2j+1
+        const int krow = 2 * (w + NW * i) + (lane >> 5);
+        const int pc = lane & 31;
+        const int lc = 2 * ((pc >> 1) ^ mswz(krow)) + (pc & 1);
+        off[i] = krow * (int)ld * 2 + lc * 16;
+      }
       const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
       frag_off = (8 * g + q) * 512 + 8 * p;  // + 32 * (unit ^ h) per fragment, h = q | (g & 1) << 2
     }
@@ -191,8 +198,12 @@ __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
 }
 
 // OUT: 0 = bf16 store, 1 = fp32 store, 2 = fp32 accumulate, 3 = bf16 accumulate (C = bf16(C + X.Y^T))
-template <bool XMN, bool YMN, int OUT>
-__global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
+// NW: waves per workgroup, as 2 (M) x NW/2 (N); wave tile 128 x (512 / NW): NW = 8 -> 128 x 64 (two
+// waves per SIMD), NW = 4 -> 128 x 128 (one wave per SIMD, 256 accumulators in AGPRs, half the LDS
+// fragment traffic per MFMA).
+template <bool XMN, bool YMN, int OUT, int NW>
+__global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs g) {
+  constexpr int WTN = 512 / NW, NJ = WTN / 16, DMA = kPieces / NW;
   __shared__ __attribute__((aligned(16))) char smem[kNS * kSlot];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases live in SGPRs
@@ -200,8 +211,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
   tile_coords(g.M, g.N, tm, tn);
   const int row0 = tm * kBM, col0 = tn * kBN;
 
-  Opnd<XMN> X;
-  Opnd<YMN> Y;
+  Opnd<XMN, NW> X;
+  Opnd<YMN, NW> Y;
   if constexpr (!XMN)
     X.init(g.x, g.ldx, g.M, g.K, row0, w, lane);
   else
@@ -215,34 +226,34 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
   auto issue = [&](int t, int slot) {
     const uint32_t s = lbase + (uint32_t)(slot * kSlot);
     const GRsrc rx = X.rsrc(t), ry = Y.rsrc(t);
-    g_dma16(rx, s + w * 1024, X.off0);
-    g_dma16(rx, s + (w + 8) * 1024, X.off1);
-    g_dma16(ry, s + kImg + w * 1024, Y.off0);
-    g_dma16(ry, s + kImg + (w + 8) * 1024, Y.off1);
+#pragma unroll
+    for (int i = 0; i < 16 / NW; ++i) g_dma16(rx, s + (w + NW * i) * 1024, X.off[i]);
+#pragma unroll
+    for (int i = 0; i < 16 / NW; ++i) g_dma16(ry, s + kImg + (w + NW * i) * 1024, Y.off[i]);
   };
 
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / (NW / 2), wn = w % (NW / 2);
   struct Frags {
-    gbf8 y[4];  // MFMA A operand: output columns
+    gbf8 y[NJ];  // MFMA A operand: output columns
     gbf8 x[8];  // MFMA B operand: output rows
   };
   auto read_frags = [&](Frags& f, const char* slot) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) f.y[j] = Y.frag(slot + kImg, wn * 64 + j * 16, lane);
+    for (int j = 0; j < NJ; ++j) f.y[j] = Y.frag(slot + kImg, wn * WTN + j * 16, lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) f.x[i] = X.frag(slot, wm * 128 + i * 16, lane);
   };
 
-  gf4 acc[8][4];
+  gf4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = gf4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = gf4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](const Frags& f) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.y[j], f.x[i], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.y[j], f.x[i], acc[i][j], 0, 0, 0);
   };
 
   const int nk = g.K / kBK;
@@ -250,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
 #pragma unroll
   for (int s = 0; s < kNS - 1; ++s)
     if (s < nk) issue(s, s);
-  g_wait_stages(min(nk - 1, kNS - 2));
+  g_wait_stages<DMA>(min(nk - 1, kNS - 2));
   g_barrier();
   Frags f0, f1;
   read_frags(f0, smem);
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
   // (every body reads the next stage unconditionally, so hipcc's lgkmcnt ladder before the MFMAs counts
   // the just-issued reads as outstanding; the last stage is peeled off below)
   auto body = [&](int t, Frags& cur, Frags& nxt) {
-    g_wait_stages(min(nk - 1, t + kNS - 2) - (t + 1));
+    g_wait_stages<DMA>(min(nk - 1, t + kNS - 2) - (t + 1));
     g_barrier();
     if (t + kNS - 1 < nk) issue(t + kNS - 1, slot_issue);
     read_frags(nxt, smem + slot_next * kSlot);
@@ -289,8 +300,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
     const int m = row0 + wm * 128 + i * 16 + fr;
     if (m >= g.M) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = col0 + wn * 64 + j * 16 + fc * 4;
+    for (int j = 0; j < NJ; ++j) {
+      const int n = col0 + wn * WTN + j * 16 + fc * 4;
       if (n >= g.N) continue;
       const gf4 v = acc[i][j];
       if constexpr (OUT == 0 || OUT == 3) {
@@ -323,17 +334,31 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs g) {
   }
 }
 
-template <bool XMN, bool YMN>
-hipError_t launch(const GemmArgs& a, int out_mode, hipStream_t stream) {
+template <bool XMN, bool YMN, int NW>
+hipError_t launch_nw(const GemmArgs& a, int out_mode, hipStream_t stream) {
   const int64_t nwg = (int64_t)((a.M + kBM - 1) / kBM) * ((a.N + kBN - 1) / kBN);
-  const dim3 grid((unsigned)nwg), block(kThreads);
+  const dim3 grid((unsigned)nwg), block(NW * 64);
   switch (out_mode) {
-    case 0: gemm_kernel<XMN, YMN, 0><<<grid, block, 0, stream>>>(a); break;
-    case 1: gemm_kernel<XMN, YMN, 1><<<grid, block, 0, stream>>>(a); break;
-    case 2: gemm_kernel<XMN, YMN, 2><<<grid, block, 0, stream>>>(a); break;
-    default: gemm_kernel<XMN, YMN, 3><<<grid, block, 0, stream>>>(a); break;
+    case 0: gemm_kernel<XMN, YMN, 0, NW><<<grid, block, 0, stream>>>(a); break;
+    case 1: gemm_kernel<XMN, YMN, 1, NW><<<grid, block, 0, stream>>>(a); break;
+    case 2: gemm_kernel<XMN, YMN, 2, NW><<<grid, block, 0, stream>>>(a); break;
+    default: gemm_kernel<XMN, YMN, 3, NW><<<grid, block, 0, stream>>>(a); break;
   }
   return hipGetLastError();
+}
+
+// LLMT_GEMM_WAVES=4|8 (read once): workgroup shape, see gemm_kernel
+inline int gemm_waves() {
+  static const int nw = [] {
+    const char* e = getenv("LLMT_GEMM_WAVES");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
+  return nw;
+}
+
+template <bool XMN, bool YMN>
+hipError_t launch(const GemmArgs& a, int out_mode, hipStream_t stream) {
+  return gemm_waves() == 8 ? launch_nw<XMN, YMN, 8>(a, out_mode, stream) : launch_nw<XMN, YMN, 4>(a, out_mode, stream);
 }
 
 }  // namespace
@@ -353,5 +378,5 @@ extern "C" hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn,
   if (!x_mn && !y_mn) return launch<false, false>(a, out_mode, stream);
   if (!x_mn && y_mn) return launch<false, true>(a, out_mode, stream);
   if (x_mn && y_mn) return launch<true, true>(a, out_mode, stream);
-  return launch<true, false>(a, out_mode, stream);
+  return hipErrorInvalidValue;  // X MN-major with Y K-major: no linear-layer GEMM has this layout
 }

@@ -23,8 +23,11 @@ import torch
 import torch.distributed as dist
 
 from ..optim import resolve_optimizer
+from ..parallel import debug as collective_debug
 from ..parallel.context import ParallelContext, init_distributed
 from ..parallel.engine import DataParallelEngine, freeze_modules
+from .monitor import (StallWatchdog, StepProfiler, ThroughputMeter, find_last_checkpoint, model_flops_per_token,
+                      record_failure)
 from .strategies import Strategy, resolve_strategy
 
 logger = logging.getLogger("llm_training")
@@ -95,6 +98,11 @@ class Trainer:
         self._log_buffer: list[tuple[int, dict]] = []
         self.last_metrics: dict[str, float] = {}
         self.step_times: list[float] = []
+        self.meter: ThroughputMeter | None = None
+        self.profiler: StepProfiler | None = None
+        self.watchdog: StallWatchdog | None = None
+        self.collectives = None
+        self._fpt: dict[int, float] = {}
 
     # ------------------------------------------------------------------ properties used by callbacks
     @property
@@ -138,6 +146,8 @@ class Trainer:
         self.pc = ParallelContext.create(st.data_parallel_size, st.tensor_parallel_size, device)
         seed = self.seed if self.seed is not None else 42
         torch.manual_seed(seed + self.pc.dp_rank)
+        if ckpt_path == "last":
+            ckpt_path = self.resolve_last_checkpoint()
         self.lm, self.datamodule = lm, datamodule
         for cb in self.callbacks:
             _call(cb, "setup", self, lm, "fit")
@@ -163,6 +173,24 @@ class Trainer:
             load_checkpoint(self, ckpt_path)
         for lg in self.loggers:
             _call(lg, "setup", self)
+        self.meter = ThroughputMeter(self.pc.dp_size, device=device)
+        self.profiler = StepProfiler(out_dir=self.log_dir, rank=self.pc.rank)
+        self.watchdog = StallWatchdog(path=os.path.join(self.log_dir, f"stall_rank{self.pc.rank}.txt"))
+        self.collectives = collective_debug.maybe_enable_from_env()
+
+    def resolve_last_checkpoint(self) -> str | None:
+        """``ckpt_path: last``: newest complete checkpoint under the checkpoint directories (or None)."""
+        from .callbacks import ModelCheckpoint
+        roots = [cb.dirpath for cb in self.callbacks if isinstance(cb, ModelCheckpoint) and cb.dirpath]
+        roots.append(self.default_root_dir)
+        found = [c for c in (find_last_checkpoint(r) for r in roots) if c]
+        if not found:
+            logger.info("ckpt_path=last: no complete checkpoint under %s; starting from scratch", roots)
+            return None
+        from .monitor import checkpoint_step
+        best = max(found, key=checkpoint_step)
+        logger.info("ckpt_path=last: resuming from %s", best)
+        return best
 
     def train_loader(self):
         return self.datamodule.train_dataloader(self.pc.dp_rank, self.pc.dp_size,
@@ -185,6 +213,17 @@ class Trainer:
 
     # ------------------------------------------------------------------ loop
     def fit(self, lm, datamodule=None, ckpt_path: str | None = None):
+        try:
+            return self._fit(lm, datamodule, ckpt_path)
+        except Exception as e:
+            rank = self.pc.rank if self.pc is not None else int(os.environ.get("RANK", "0"))
+            record_failure(e, rank, self.log_dir)
+            raise
+        finally:
+            if self.watchdog is not None:
+                self.watchdog.close()
+
+    def _fit(self, lm, datamodule=None, ckpt_path: str | None = None):
         self.setup(lm, datamodule, ckpt_path)
         for cb in self.callbacks:
             _call(cb, "on_fit_start", self, lm)
@@ -233,6 +272,8 @@ class Trainer:
     def train_step(self, batches: list[dict]):
         eng, lm = self.engine, self.lm
         t0 = time.perf_counter()
+        self.profiler.before_step(self.state.global_step + 1)
+        self.watchdog.arm()
         for cb in self.callbacks:
             _call(cb, "on_train_batch_start", self, lm, batches[0], self.state.batch_idx)
         eng.begin_step(len(batches))
@@ -262,9 +303,25 @@ class Trainer:
         self.state.batch_idx += len(batches)
         self._log_buffer.append((self.state.global_step, metrics_acc))
         self.step_times.append(time.perf_counter() - t0)
+        self._count_tokens(batches)
+        self.profiler.after_step(self.state.global_step)
+        self.watchdog.disarm()
+        if self.collectives is not None and self.state.global_step % collective_debug.check_every() == 0:
+            self.collectives.verify()
         self._flush_logs()
         for cb in self.callbacks:
             _call(cb, "on_train_batch_end", self, lm, None, batches[-1], self.state.batch_idx)
+
+    def _count_tokens(self, batches: list[dict]):
+        ids = [b.get("input_ids") for b in batches if isinstance(b, dict)]
+        ids = [t for t in ids if isinstance(t, torch.Tensor)]
+        if not ids:
+            return
+        S = int(ids[0].shape[-1])
+        if S not in self._fpt:
+            self._fpt[S] = model_flops_per_token(getattr(self.lm.model, "config", None), S)
+        self.meter.fpt = self._fpt[S]
+        self.meter.update(sum(t.numel() for t in ids))
 
     def _flush_logs(self, force: bool = False):
         if not self._log_buffer:
@@ -288,9 +345,12 @@ class Trainer:
             t = torch.tensor([float(consumed[k]) for k in sorted(consumed)], device=self.device)
             dist.all_reduce(t, group=self.pc.dp_group)
             consumed = dict(zip(sorted(consumed), t.cpu().tolist()))
-        for (step, _), vals in zip(rows, mat):
+        rates = self.meter.metrics() if self.meter is not None else {}
+        for i, ((step, _), vals) in enumerate(zip(rows, mat)):
             d = dict(zip(keys, vals))
             d.update({k: float(v) for k, v in consumed.items()})
+            if i == len(rows) - 1:
+                d.update(rates)
             self.last_metrics = d
             if self.is_global_zero:
                 for lg in self.loggers:
@@ -298,8 +358,10 @@ class Trainer:
         if self.is_global_zero and self.enable_progress_bar:
             d = self.last_metrics
             loss = next((d[k] for k in d if k.startswith("Loss/Train") or k == "Loss/Train/Step"), float("nan"))
-            logger.info("step %d | loss %.4f | lr %.3e | grad_norm %.3f", self.state.global_step, loss,
-                        d.get("lr", float("nan")), d.get("Gradient Norm", float("nan")))
+            logger.info("step %d | loss %.4f | lr %.3e | grad_norm %.3f | %.0f tok/s | %.1f TFLOP/s/gpu",
+                        self.state.global_step, loss, d.get("lr", float("nan")), d.get("Gradient Norm", float("nan")),
+                        d.get("Throughput/tokens_per_sec", float("nan")),
+                        d.get("Throughput/tflops_per_gpu", float("nan")))
         self._log_buffer.clear()
 
     @torch.no_grad()

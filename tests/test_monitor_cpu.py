@@ -1,0 +1,137 @@
+"""Observability / failure-handling helpers (runtime/monitor.py) and the collective-consistency checker
+(parallel/debug.py). CPU only; the checker runs on 2 gloo ranks."""
+import json
+import os
+import time
+
+import pytest
+import torch
+
+from tests.helpers import run_gloo
+
+
+def test_model_flops_per_token_llama3_8b():
+    from types import SimpleNamespace
+
+    from llm_training_amd.runtime.monitor import model_flops_per_token
+    cfg = SimpleNamespace(hidden_size=4096, num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=8,
+                          intermediate_size=14336, vocab_size=128256)
+    f = model_flops_per_token(cfg, 8192)
+    # 45.03 GF matmul + 6.44 GF attention = 51.5 GF/token
+    assert abs(f / 1e9 - 51.5) < 0.2
+    assert model_flops_per_token(None, 8192) == 0.0
+
+
+def test_throughput_meter_rates():
+    from llm_training_amd.runtime.monitor import ThroughputMeter
+    m = ThroughputMeter(world_size=4, flops_per_token=1e9)
+    assert m.metrics() == {}
+    m.update(1000)
+    time.sleep(0.05)
+    m.update(1000)
+    d = m.metrics()
+    assert d["Throughput/tokens_per_sec"] == pytest.approx(4 * d["Throughput/tokens_per_sec_per_gpu"])
+    assert 0 < d["Throughput/tokens_per_sec_per_gpu"] < 2000 / 0.05
+    assert d["Throughput/tflops_per_gpu"] == pytest.approx(d["Throughput/tokens_per_sec_per_gpu"] * 1e9 / 1e12)
+    assert m.steps == 0  # reset after reporting
+
+
+def test_step_profiler_writes_trace(tmp_path):
+    from llm_training_amd.runtime.monitor import StepProfiler
+    p = StepProfiler("2-3", out_dir=str(tmp_path), rank=0)
+    assert p.enabled
+    for step in range(1, 5):
+        p.before_step(step)
+        torch.randn(64, 64) @ torch.randn(64, 64)
+        p.after_step(step)
+    assert p.trace_path is not None and os.path.isfile(p.trace_path)
+    assert not p.enabled  # one window only
+    with pytest.raises(ValueError):
+        StepProfiler("abc")
+
+
+def test_stall_watchdog_dumps_stack(tmp_path):
+    from llm_training_amd.runtime.monitor import StallWatchdog
+    path = tmp_path / "stall.txt"
+    w = StallWatchdog(timeout=0.2, path=str(path))
+    w.arm()
+    time.sleep(0.6)
+    w.close()
+    text = path.read_text()
+    assert "test_stall_watchdog_dumps_stack" in text
+    assert not StallWatchdog(timeout=0).enabled
+
+
+def _fake_ckpt(root, name, step, tp=1, complete=True):
+    d = root / name
+    d.mkdir(parents=True)
+    (d / "meta.json").write_text(json.dumps({"tp_size": tp, "trainer": {"global_step": step}}))
+    for t in range(tp if complete else tp - 1):
+        (d / f"tp{t}.safetensors").write_bytes(b"x")
+    return d
+
+
+def test_find_last_checkpoint_skips_incomplete(tmp_path):
+    from llm_training_amd.runtime.monitor import find_last_checkpoint
+    assert find_last_checkpoint(tmp_path / "missing") is None
+    _fake_ckpt(tmp_path, "epoch=0-step=10", 10)
+    best = _fake_ckpt(tmp_path, "epoch=0-step=20", 20, tp=2)
+    _fake_ckpt(tmp_path, "epoch=0-step=30", 30, tp=2, complete=False)  # crashed mid-save
+    assert find_last_checkpoint(tmp_path) == str(best)
+
+
+def test_record_failure(tmp_path):
+    from llm_training_amd.runtime.monitor import record_failure
+    try:
+        raise ValueError("boom")
+    except ValueError as e:
+        path = record_failure(e, 3, str(tmp_path))
+    assert path.endswith("failure_rank3.txt")
+    text = open(path).read()
+    assert "rank: 3" in text and "ValueError: boom" in text
+
+
+def test_trainer_resumes_from_last(tmp_path):
+    """fit(ckpt_path="last") picks the newest complete checkpoint the ModelCheckpoint callback wrote."""
+    from llm_training_amd.runtime.callbacks import ModelCheckpoint
+    from llm_training_amd.runtime.trainer import Trainer
+    ckdir = tmp_path / "ck"
+    _fake_ckpt(ckdir, "epoch=0-step=5", 5)
+    best = _fake_ckpt(ckdir, "epoch=0-step=7", 7)
+    t = Trainer(default_root_dir=str(tmp_path), callbacks=[ModelCheckpoint(dirpath=str(ckdir))])
+    assert t.resolve_last_checkpoint() == str(best)
+    t2 = Trainer(default_root_dir=str(tmp_path / "empty"))
+    assert t2.resolve_last_checkpoint() is None
+
+
+def _collective_worker(rank, world, diverge):
+    import torch.distributed as dist
+
+    from llm_training_amd.parallel.debug import CollectiveRecorder
+    rec = CollectiveRecorder().install()
+    try:
+        t = torch.ones(4)
+        dist.all_reduce(t)
+        rec.verify()  # identical so far
+        # rank 1 reduces with a different op: gloo completes it, but the sequences no longer agree
+        op = dist.ReduceOp.MAX if (diverge and rank == 1) else dist.ReduceOp.SUM
+        dist.all_reduce(torch.ones(8), op=op)
+        try:
+            rec.verify()
+            return "ok"
+        except RuntimeError as e:
+            return str(e)
+    finally:
+        rec.uninstall()
+
+
+def test_collective_checker_agrees_when_consistent():
+    out = run_gloo(_collective_worker, world=2, args=(False,))
+    assert out == {0: "ok", 1: "ok"}
+
+
+def test_collective_checker_reports_divergence():
+    out = run_gloo(_collective_worker, world=2, args=(True,))
+    for r in (0, 1):
+        assert "differs across ranks at call #0" in out[r]
+        assert "MAX" in out[r] and "SUM" in out[r]
