@@ -30,8 +30,10 @@ from .native import lib, use_native
 # The three GEMMs of a linear layer run on the hand-written gfx950 kernel (csrc/gemm.hip) or on
 # hipBLASLt through torch.matmul. ``LLMT_GEMM`` picks per layout: "hip" (all), "blas" (none) or a comma
 # list of fwd,dgrad,wgrad. Shapes the kernel does not take (K % 32, N % 4, unaligned or strided
-# operands) always go to the library.
-_GEMM_ENV = os.environ.get("LLMT_GEMM", "hip").strip().lower()
+# operands) always go to the library. Default "blas": on the Llama-3-8B step the library GEMMs are
+# faster end to end (profiles/r1_gemm_hip_v1_vs_hipblaslt.jsonl: 1.1-1.2 vs 1.2-1.6 PF/s per projection;
+# bench 16.6k tok/s blas vs 16.4k wgrad-only vs 15.7k all-hip).
+_GEMM_ENV = os.environ.get("LLMT_GEMM", "blas").strip().lower()
 HIP_GEMM_LAYOUTS = ({"fwd", "dgrad", "wgrad"} if _GEMM_ENV == "hip" else
                     set() if _GEMM_ENV in ("blas", "", "none") else {x.strip() for x in _GEMM_ENV.split(",")})
 

@@ -261,7 +261,9 @@ def test_gemm_strided_operands():
     assert cw[:, N:].abs().max().item() == 0
 
 
-def test_linear_hip_gemm_grads_into_grad_buffer():
+def test_linear_hip_gemm_grads_into_grad_buffer(monkeypatch):
+    import llm_training_amd.ops.fused as fused
+    monkeypatch.setattr(fused, "HIP_GEMM_LAYOUTS", {"fwd", "dgrad", "wgrad"})  # the library is the default
     torch.manual_seed(0)
     T, K, N = 320, 256, 384
     w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16().requires_grad_(True)
