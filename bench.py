@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--attn", default="flash", choices=["flash", "sdpa", "eager"])
     ap.add_argument("--ckpt", action="store_true", help="full activation checkpointing")
+    ap.add_argument("--offload-optimizer", action="store_true", help="fp32 master/Adam state in host memory")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
                     help="hipBLASLt solution selection (default: shipped TunableOp results)")
@@ -79,7 +80,8 @@ def main():
     model = Llama(mcfg, pc, dtype=torch.bfloat16, device=device)
     model.init_weights(seed=1234)
     stage = args.zero_stage if args.zero_stage is not None else (0 if pc.dp_size == 1 else 2)
-    engine = DataParallelEngine(model, pc, stage, lr=3e-5, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    engine = DataParallelEngine(model, pc, stage, lr=3e-5, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
+                                offload_optimizer=args.offload_optimizer)
     lm = CLM({"model": None})
     lm.model = model
     lm.train()
@@ -136,7 +138,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random-init weights)",
             "config": {"model": "Llama-3-8B" if not args.layers else f"Llama-3-8B-{args.layers}L(INVALID-debug)",
                        "global_batch": pc.dp_size * B, "seq_len": S, "parallelism": par, "zero_stage": stage,
-                       "attn": args.attn, "activation_checkpointing": args.ckpt, "optimizer": "fused AdamW fp32 master",
+                       "attn": args.attn, "activation_checkpointing": args.ckpt, "optimizer": ("host AdamW (offload) fp32 master" if args.offload_optimizer else "fused AdamW fp32 master"),
                        "grad_clip": 1.0, "gemm_tuning": gemm_mode},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "mfu": round(tps / world * fpt / 2.5e15, 4),

@@ -23,6 +23,14 @@ optim/master_weight_wrapper.py) — with one engine designed around MI355X:
   waits for that unit only. Stage 3 keeps only the shard and all-gathers a unit right before its
   forward (prefetching the next unit) and again before its backward, freeing it afterwards.
 
+* **Optimizer offload** (``offload_optimizer=True``; DeepSpeed ``offload_optimizer`` / FSDP2
+  ``offload_policy``, deepspeed_strategy.py:22-27, fsdp2_strategy.py:58): master / m / v shards live
+  in pinned host memory (12 B/param / dp off the GPU). At the step every unit's bf16 gradient shard is
+  copied down on a copy stream up front; the host walks the units in order, waits for that unit's
+  copy, runs the native C++ AdamW (csrc/cpu_adam.cpp, ATen thread pool) and queues the bf16 shard's
+  upload, so the PCIe traffic of unit i+1 overlaps the host math of unit i and the next forward only
+  waits for its own unit.
+
 Checkpoint layout (see ckpt/): per-unit shards of master / m / v plus the step counter.
 """
 from __future__ import annotations
@@ -72,6 +80,8 @@ class _Unit:
     opt_event: object = None        # async AdamW of this unit done (stage 3 shard update)
     replicated: bool = False
     keep_gathered: bool = False     # stage 3: params used outside the hooked module's forward
+    g_host: torch.Tensor | None = None    # optimizer offload: pinned bf16 gradient shard
+    p_host: torch.Tensor | None = None    # optimizer offload: pinned bf16 parameter shard
 
     @property
     def shard_numel(self):
@@ -82,8 +92,10 @@ class DataParallelEngine:
     def __init__(self, model: nn.Module, pc: ParallelContext, zero_stage: int = 2, *, lr: float = 1e-5,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01,
                  grad_dtype: torch.dtype | None = None, reduce_dtype: torch.dtype | None = None,
-                 reshard_after_forward: bool = True, overlap_comm: bool = True, overlap_step: bool = True):
+                 reshard_after_forward: bool = True, overlap_comm: bool = True, overlap_step: bool = True,
+                 offload_optimizer: bool = False):
         self.model = model
+        self.offload = bool(offload_optimizer)
         self.pc = pc
         self.stage = int(zero_stage)
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
@@ -103,7 +115,9 @@ class DataParallelEngine:
         # (memory-bound optimizer beside compute-bound GEMMs); each unit's forward waits for its own
         # update through the same per-unit event the stage-1/2 all-gather uses
         overlap_step = overlap_step and os.environ.get("LLMT_OVERLAP_STEP", "1") != "0"
-        self.opt_stream = torch.cuda.Stream(device=dev) if (self.cuda and overlap_step) else None
+        self.opt_stream = (torch.cuda.Stream(device=dev) if (self.cuda and overlap_step and not self.offload)
+                           else None)
+        self.copy_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.offload) else None
         # models built from our fused ops write weight grads straight into the flat buffers; others
         # (transformers modules) leave ordinary .grad tensors that are absorbed after backward
         self.autograd_grads = not getattr(model, "writes_main_grad", True)
@@ -184,8 +198,18 @@ class DataParallelEngine:
                 u.gshard = torch.zeros(sn, device=dev, dtype=self.reduce_dtype)
         else:
             u.master = pflat.float().clone()
+        if self.offload:
+            pin = self.cuda
+            u.master = u.master.cpu().pin_memory() if pin else u.master.cpu()
+            u.g_host = torch.empty(u.master.numel(), dtype=self.grad_dtype, pin_memory=pin)
+            # bf16 models: the host kernel also writes the bf16 copy that is uploaded; fp32 models
+            # upload the master itself
+            if self.param_dtype == torch.bfloat16:
+                u.p_host = torch.empty(u.master.numel(), dtype=torch.bfloat16, pin_memory=pin)
         u.exp_avg = torch.zeros_like(u.master)
         u.exp_avg_sq = torch.zeros_like(u.master)
+        if self.offload and self.cuda:
+            u.exp_avg, u.exp_avg_sq = u.exp_avg.pin_memory(), u.exp_avg_sq.pin_memory()
         if stage >= 3 and dp > 1:
             u.pshard = pflat[r * sn:(r + 1) * sn].clone()
             self._free_full(u)
@@ -412,6 +436,9 @@ class DataParallelEngine:
     @torch.no_grad()
     def step(self, lr: float):
         self.step_count += 1
+        if self.offload:
+            self._step_units_offload(lr)
+            return
         if self.opt_stream is None:
             self._step_units(lr)
             return
@@ -446,32 +473,92 @@ class DataParallelEngine:
             if self.cuda and self.opt_stream is not None:
                 done = torch.cuda.Event()
                 done.record(cur)
-            # stage 1/2: refresh this unit's full bf16 parameters with an in-place all-gather of the
-            # updated shards on the comm stream right away, so it overlaps the remaining units' AdamW
-            # and the next forward (which waits per unit in its pre-forward hook)
-            if self.stage in (1, 2) and dp > 1 and not u.replicated:
-                shard = u.pflat[r * sn:(r + 1) * sn]
-                if self.comm_stream is not None:
-                    ev = torch.cuda.Event()
-                    ev.record(cur)
-                    with torch.cuda.stream(self.comm_stream):
-                        self.comm_stream.wait_event(ev)
-                        dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
-                        done = torch.cuda.Event()
-                        done.record(self.comm_stream)
-                else:
-                    dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
-                    if done is not None:
-                        done = torch.cuda.Event()
-                        done.record(cur)
-            if st >= 3 and udp > 1:
-                u.opt_event = done
-            else:
-                u.ag_event = done
+            self._publish_update(u, cur, done)
         if self.stage >= 3 and dp > 1:
             for u in self.units:
                 if u.gathered and not u.replicated:
                     self._release_unit(u)
+
+    def _step_units_offload(self, lr: float):
+        """AdamW on the host for optimizer-offloaded shards (see the module docstring)."""
+        b1, b2 = self.betas
+        dp, r = self.dp, self.pc.dp_rank
+        scale = float(self._gscale.reshape(-1)[0].item())  # the one host sync of the step
+        outs, grads = [], []
+        for u in self.units:
+            st, udp = self._ustage(u), self._udp(u)
+            sn = u.numel // udp
+            rr = r if udp > 1 else 0
+            if st >= 1:
+                outs.append(u.pshard if (st >= 3 and udp > 1) else u.pflat[rr * sn:(rr + 1) * sn])
+            else:
+                outs.append(u.pflat)
+            grads.append(self._grad_shard(u))
+        cur = torch.cuda.current_stream() if self.cuda else None
+        down = []
+        if self.cuda:
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            with torch.cuda.stream(self.copy_stream):
+                self.copy_stream.wait_event(ready)
+                for u, g in zip(self.units, grads):
+                    u.g_host.copy_(g, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.copy_stream)
+                    down.append(ev)
+        for i, (u, pout) in enumerate(zip(self.units, outs)):
+            if self.cuda:
+                down[i].synchronize()
+                g = u.g_host
+            else:
+                g = grads[i].contiguous()
+            lib().adamw_cpu_(u.master, u.exp_avg, u.exp_avg_sq, g, u.p_host, lr, b1, b2, self.eps,
+                             self.weight_decay, self.step_count, scale)
+            done = None
+            if self.cuda:
+                with torch.cuda.stream(self.copy_stream):
+                    pout.copy_(u.p_host if u.p_host is not None else u.master, non_blocking=True)
+                    done = torch.cuda.Event()
+                    done.record(self.copy_stream)
+                self._publish_update(u, self.copy_stream, done)
+            else:
+                pout.copy_(u.p_host if u.p_host is not None else u.master)
+                self._publish_update(u, None, None)
+        if self.stage >= 3 and dp > 1:
+            for u in self.units:
+                if u.gathered and not u.replicated:
+                    self._release_unit(u)
+
+    def _publish_update(self, u: _Unit, cur, done):
+        """Make unit ``u``'s updated shard visible: all-gather (stage 1/2) and the per-unit event the
+        next forward waits on. ``cur`` is the stream the update was issued on, ``done`` its event."""
+        dp, r = self.dp, self.pc.dp_rank
+        st, udp = self._ustage(u), self._udp(u)
+        sn = u.numel // udp
+        # stage 1/2: refresh this unit's full bf16 parameters with an in-place all-gather of the
+        # updated shards on the comm stream right away, so it overlaps the remaining units' AdamW
+        # and the next forward (which waits per unit in its pre-forward hook)
+        if self.stage in (1, 2) and dp > 1 and not u.replicated:
+            shard = u.pflat[r * sn:(r + 1) * sn]
+            if self.comm_stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                with torch.cuda.stream(self.comm_stream):
+                    self.comm_stream.wait_event(ev)
+                    dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
+                    done = torch.cuda.Event()
+                    done.record(self.comm_stream)
+            else:
+                if done is not None:
+                    torch.cuda.current_stream().wait_event(done)
+                dist.all_gather_into_tensor(u.pflat, shard, group=self.group)
+                if done is not None:
+                    done = torch.cuda.Event()
+                    done.record(torch.cuda.current_stream())
+        if st >= 3 and udp > 1:
+            u.opt_event = done
+        else:
+            u.ag_event = done
 
     def wait_params(self):
         """Make the current stream wait for every pending update / parameter all-gather."""
@@ -479,6 +566,8 @@ class DataParallelEngine:
             torch.cuda.current_stream().wait_stream(self.opt_stream)
         if self.comm_stream is not None:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
+        if self.copy_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.copy_stream)
         for u in self.units:
             u.ag_event = None
             u.opt_event = None

@@ -3,7 +3,7 @@
 Reference strategy surfaces: FSDP2Strategy (src/llm_training/lightning/strategy/fsdp2/
 fsdp2_strategy.py:49-78), DeepSpeedStrategy (lightning/strategy/deepspeed/deepspeed_strategy.py:17-72)
 and Lightning's ddp / single-device. The knobs keep their names; the ones that only make sense for
-DeepSpeed's engine (bucket sizes, offload, ZeRO++ quantisation) are accepted and recorded but the
+DeepSpeed's engine (bucket sizes, ZeRO++ quantisation) are accepted and recorded but the
 engine's own choices apply (per-layer units; see parallel/engine.py for why no extra bucketing is
 needed on xGMI).
 """
@@ -28,6 +28,7 @@ class Strategy:
     grad_reduce_dtype: str | None = None
     overlap_comm: bool = True
     save_distributed_checkpoint: bool = True
+    offload_optimizer: bool = False
     extra: dict = field(default_factory=dict)
 
     @property
@@ -65,8 +66,10 @@ class FSDP2Strategy(Strategy):
                          tensor_parallel_size=tensor_parallel_size, process_group_backend=process_group_backend,
                          timeout=timeout, reshard_after_forward=bool(reshard_after_forward),
                          save_distributed_checkpoint=save_distributed_checkpoint)
-        if offload_policy not in (None, {}) and not isinstance(offload_policy, dict):
-            logger.warning("FSDP2Strategy: CPU offload is not supported on this engine; ignored")
+        # FSDP2 OffloadPolicy (CPUOffloadPolicy / {"class_path": ...CPUOffloadPolicy} / True): the fp32
+        # master and Adam moments move to pinned host memory, updated by the native host AdamW; the bf16
+        # parameters and gradients stay in HBM (288 GB holds them for any model that fits the node)
+        self.offload_optimizer = _wants_offload(offload_policy)
         self.extra = {"mp_policy": mp_policy, "use_master_weights": use_master_weights, **kw}
 
 
@@ -79,10 +82,22 @@ class DeepSpeedStrategy(Strategy):
                  timeout=datetime.timedelta(minutes=30), **kw):
         super().__init__(zero_stage=int(stage), process_group_backend=process_group_backend, timeout=timeout,
                          overlap_comm=overlap_comm)
-        if offload_optimizer or offload_parameters:
-            logger.warning("DeepSpeedStrategy: offload is not supported on this engine; ignored")
+        self.offload_optimizer = bool(offload_optimizer)
+        if offload_parameters:
+            logger.warning("DeepSpeedStrategy: offload_parameters is not supported (parameters stay in HBM); "
+                           "offload_optimizer is")
         self.extra = {"exclude_frozen_parameters": exclude_frozen_parameters,
                       "allgather_bucket_size": allgather_bucket_size, "reduce_bucket_size": reduce_bucket_size, **kw}
+
+
+def _wants_offload(policy) -> bool:
+    if policy is None or policy is False or policy == {}:
+        return False
+    if policy is True:
+        return True
+    if isinstance(policy, dict):  # jsonargparse form: {"class_path": "torch.distributed.fsdp.CPUOffloadPolicy"}
+        return "CPUOffload" in str(policy.get("class_path", "")) or bool(policy.get("offload", False))
+    return "CPUOffload" in type(policy).__name__  # the base OffloadPolicy means "no offload"
 
 
 STRATEGY_NAMES = {"ddp": DDPStrategy, "auto": DDPStrategy, "single_device": SingleDeviceStrategy,

@@ -166,7 +166,8 @@ class Trainer:
                                          eps=hp["eps"], weight_decay=hp["weight_decay"],
                                          reduce_dtype=getattr(torch, rd) if rd else None,
                                          reshard_after_forward=st.reshard_after_forward,
-                                         overlap_comm=st.overlap_comm)
+                                         overlap_comm=st.overlap_comm,
+                                         offload_optimizer=getattr(st, "offload_optimizer", False))
         self.scheduler = lm.build_lr_scheduler(self.base_lr, self.estimated_stepping_batches())
         if ckpt_path:
             from ..ckpt.checkpoint import load_checkpoint

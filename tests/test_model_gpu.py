@@ -113,6 +113,49 @@ def test_phi3_head_dim96_hip_matches_cpu_reference(window):
     _hip_vs_cpu(Phi3, cfg, ids)
 
 
+def _train_engine(cfg, dev, steps=4, **eng_kw):
+    torch.manual_seed(0)
+    m = Llama(cfg, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
+    m.init_weights(5)
+    eng = DataParallelEngine(m, ParallelContext.single(dev), 0, lr=1e-3, **eng_kw)
+    lm = CLM({"model": None})
+    lm.model = m
+    g = torch.Generator(device=dev).manual_seed(11)
+    losses = []
+    for _ in range(steps):
+        ids = torch.randint(0, cfg.vocab_size, (1, 512), device=dev, generator=g)
+        eng.begin_step(1)
+        eng.zero_grad()
+        loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+        loss.backward()
+        eng.finish_backward()
+        eng.clip_and_scale(1.0)
+        eng.step(1e-3)
+        losses.append(loss.item())
+    eng.wait_params()
+    return eng, losses, {k: v.float().cpu() for k, v in m.state_dict().items()}
+
+
+def test_optimizer_offload_matches_device_adamw():
+    """Optimizer offload (pinned host master/m/v, native C++ AdamW, per-unit D2H/H2D on a copy stream)
+    trains like the fused device AdamW: same losses, parameters within run-to-run noise."""
+    dev = torch.device("cuda", 0)
+    cfg = _cfg(num_hidden_layers=2)
+    _, la, pa = _train_engine(cfg, dev, overlap_step=False)
+    _, lb, pb = _train_engine(cfg, dev, overlap_step=False)
+    eng, lo, po = _train_engine(cfg, dev, offload_optimizer=True)
+    assert eng.units[0].master.device.type == "cpu" and eng.units[0].master.is_pinned()
+    for a, b in zip(la, lo):
+        assert abs(a - b) < 1e-3 * abs(a), (la, lo)
+    num_n = num_o = den = 0.0
+    for k in pa:
+        num_n += (pb[k] - pa[k]).norm().item() ** 2
+        num_o += (po[k] - pa[k]).norm().item() ** 2
+        den += pa[k].norm().item() ** 2
+    noise, rel = (num_n / den) ** 0.5, (num_o / den) ** 0.5
+    assert rel <= 3 * noise + 5e-3, (rel, noise)  # see test_async_optimizer_stream_matches_synchronous
+
+
 def test_async_optimizer_stream_matches_synchronous():
     """AdamW on its own stream (overlapping the next forward) must train exactly like the synchronous
     update up to the run-to-run noise of atomics (embedding backward): a read-before-update race would
@@ -142,7 +185,7 @@ def test_async_optimizer_stream_matches_synchronous():
         eng.wait_params()
         outs.append((losses, {k: v.float().cpu() for k, v in m.state_dict().items()}))
     for a, b in zip(outs[0][0], outs[2][0]):
-        assert abs(a - b) < 1e-4 * abs(a), (outs[0][0], outs[2][0])
+        assert abs(a - b) < 5e-4 * abs(a), (outs[0][0], outs[2][0])
     num_a = num_n = den = 0.0
     for k in outs[0][1]:
         ref, again, asy = outs[0][1][k], outs[1][1][k], outs[2][1][k]
@@ -150,7 +193,10 @@ def test_async_optimizer_stream_matches_synchronous():
         num_a += (asy - ref).norm().item() ** 2
         den += ref.norm().item() ** 2
     noise, rel = (num_n / den) ** 0.5, (num_a / den) ** 0.5
-    assert rel <= 3 * noise + 1e-4, (rel, noise)
+    # run-to-run noise (embedding-backward atomics, amplified by Adam's normalisation of near-zero grads)
+    # reaches ~3e-3 on some runs and 0 on others (scripts/async_race_probe.py); one missed update would
+    # be a full Adam step on every element (~5e-2 relative), so 5e-3 still separates the two
+    assert rel <= 3 * noise + 5e-3, (rel, noise)
 
 
 def test_dpo_orpo_hip_match_cpu_reference():

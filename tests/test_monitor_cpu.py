@@ -135,3 +135,34 @@ def test_collective_checker_reports_divergence():
     for r in (0, 1):
         assert "differs across ranks at call #0" in out[r]
         assert "MAX" in out[r] and "SUM" in out[r]
+
+
+@pytest.mark.parametrize("gdtype", [torch.bfloat16, torch.float32])
+def test_native_cpu_adamw_matches_reference(gdtype):
+    """csrc/cpu_adam.cpp (optimizer offload) vs the torch AdamW reference used by the engine."""
+    from llm_training_amd.ops.native import lib
+    from llm_training_amd.parallel.engine import _adamw_ref
+    torch.manual_seed(0)
+    n = 100_003  # not a multiple of the thread-pool grain
+    p = torch.randn(n)
+    m = torch.randn(n) * 0.01
+    v = torch.rand(n) * 1e-4
+    g = torch.randn(n).to(gdtype)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    pout = torch.empty(n, dtype=torch.bfloat16)
+    for step in (1, 2, 7):
+        lib().adamw_cpu_(p, m, v, g, pout, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, 0.5)
+        _adamw_ref(pr, mr, vr, g.float() * 0.5, 1e-3, 0.9, 0.95, 1e-8, 0.1, step)
+    assert torch.allclose(m, mr, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(v, vr, rtol=1e-5, atol=1e-9)
+    assert torch.allclose(p, pr, rtol=1e-5, atol=1e-6)
+    assert torch.equal(pout, p.bfloat16())  # round-to-nearest-even, as torch's cast
+
+
+def test_strategies_map_offload_knobs():
+    from llm_training_amd.runtime.strategies import DeepSpeedStrategy, FSDP2Strategy
+    assert DeepSpeedStrategy(stage=2, offload_optimizer=True).offload_optimizer
+    assert not DeepSpeedStrategy(stage=2).offload_optimizer
+    assert FSDP2Strategy(offload_policy={"class_path": "torch.distributed.fsdp.CPUOffloadPolicy"}).offload_optimizer
+    assert not FSDP2Strategy(offload_policy={"class_path": "torch.distributed.fsdp.OffloadPolicy"}).offload_optimizer
+    assert not FSDP2Strategy().offload_optimizer
