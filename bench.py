@@ -8,8 +8,8 @@
 One process per GPU (RCCL over xGMI between them). Every step is a full training step of the real
 Llama-3-8B architecture (h 4096, I 14336, 32 layers, 32 q / 8 kv heads, vocab 128256, random init,
 bf16 weights + fp32 master/Adam state): forward, backward, gradient reduction, norm clipping (1.0)
-and the fused AdamW update. Data is synthetic: two packed sequences of S=8192 random tokens per GPU
-per step (micro-batch 2 by default, weak scaling). W untimed warm-up steps, then exactly K timed steps between
+and the fused AdamW update. Data is synthetic: three packed sequences of S=8192 random tokens per GPU
+per step (micro-batch 3 by default, weak scaling). W untimed warm-up steps, then exactly K timed steps between
 a barrier + device synchronize on both sides; the reported time is the MAX over ranks. Rank 0
 prints one JSON line.
 """
@@ -46,7 +46,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seq", type=int, default=8192)
-    ap.add_argument("--micro-batch", type=int, default=2)
+    ap.add_argument("--micro-batch", type=int, default=3)
     ap.add_argument("--layers", type=int, default=None, help="debug only: fewer layers (result marked invalid)")
     ap.add_argument("--zero-stage", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1)
