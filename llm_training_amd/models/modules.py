@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 from torch.autograd import Function
@@ -103,9 +105,19 @@ class _EmbeddingFn(Function):
             return None, dw, None, None, None
         if not getattr(w, "grad_added", False):
             mg.zero_()
-        mg.view(ctx.wshape).index_add_(0, local, g2.to(mg.dtype))
+        if g.is_cuda and deterministic_mode():
+            # index_add_ scatters with atomics (order-dependent sums for repeated tokens); the sort-based
+            # accumulate path of index_put_ sums each row's contributions in a fixed order
+            mg.view(ctx.wshape).index_put_((local,), g2.to(mg.dtype), accumulate=True)
+        else:
+            mg.view(ctx.wshape).index_add_(0, local, g2.to(mg.dtype))
         w.grad_added = True
         return None, None, None, None, None
+
+
+def deterministic_mode() -> bool:
+    """``Trainer(deterministic=True)`` / ``LLMT_DETERMINISTIC=1``: bitwise-reproducible steps."""
+    return torch.are_deterministic_algorithms_enabled() or os.environ.get("LLMT_DETERMINISTIC", "0") == "1"
 
 
 class VocabParallelEmbedding(nn.Module):

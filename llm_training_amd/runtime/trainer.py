@@ -66,6 +66,7 @@ class Trainer:
                  default_root_dir: str = "logs", num_sanity_val_steps: int = 0, seed: int | None = None,
                  deterministic: bool = False, benchmark: Any = None, **unused):
         self.strategy: Strategy = resolve_strategy(strategy)
+        self.deterministic = bool(deterministic)
         self.precision = precision
         self.loggers = [] if logger in (None, False) else (list(logger) if isinstance(logger, list) else [logger])
         self.callbacks = list(callbacks or [])
@@ -145,6 +146,11 @@ class Trainer:
         self.device = device
         self.pc = ParallelContext.create(st.data_parallel_size, st.tensor_parallel_size, device)
         seed = self.seed if self.seed is not None else 42
+        if self.deterministic:
+            # bitwise-reproducible steps: sort-based embedding backward (models/modules.py); every HIP
+            # kernel already reduces in a fixed order (no float atomics in the backward)
+            torch.use_deterministic_algorithms(True, warn_only=True)
+            os.environ["LLMT_DETERMINISTIC"] = "1"
         torch.manual_seed(seed + self.pc.dp_rank)
         if ckpt_path == "last":
             ckpt_path = self.resolve_last_checkpoint()

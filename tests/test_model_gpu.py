@@ -136,6 +136,18 @@ def _train_engine(cfg, dev, steps=4, **eng_kw):
     return eng, losses, {k: v.float().cpu() for k, v in m.state_dict().items()}
 
 
+def test_deterministic_mode_is_bitwise_reproducible(monkeypatch):
+    """LLMT_DETERMINISTIC=1 (Trainer(deterministic=True)): two runs give identical losses and weights."""
+    monkeypatch.setenv("LLMT_DETERMINISTIC", "1")
+    dev = torch.device("cuda", 0)
+    cfg = _cfg(num_hidden_layers=2)
+    _, la, pa = _train_engine(cfg, dev)
+    _, lb, pb = _train_engine(cfg, dev)
+    assert la == lb
+    bad = [k for k in pa if not torch.equal(pa[k], pb[k])]
+    assert not bad, bad
+
+
 def test_optimizer_offload_matches_device_adamw():
     """Optimizer offload (pinned host master/m/v, native C++ AdamW, per-unit D2H/H2D on a copy stream)
     trains like the fused device AdamW: same losses, parameters within run-to-run noise."""
