@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--attn", default="flash", choices=["flash", "sdpa", "eager"])
     ap.add_argument("--ckpt", action="store_true", help="full activation checkpointing")
     ap.add_argument("--offload-optimizer", action="store_true", help="fp32 master/Adam state in host memory")
+    ap.add_argument("--loss-chunk", type=int, default=8192, help="rows per lm_head GEMM of the fused CE")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="run the dp>1 engine schedule (RCCL reduce-scatter/all-gather, comm stream) even on 1 GPU")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
                     help="hipBLASLt solution selection (default: shipped TunableOp results)")
@@ -66,6 +69,14 @@ def main():
     from llm_training_amd.runtime.gemm_tuning import setup_gemm_tuning
 
     rank, local, world, device = init_distributed()
+    if args.force_sharded and world == 1:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=device)
     gemm_mode = setup_gemm_tuning(args.gemm_tuning)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -75,13 +86,13 @@ def main():
     if args.layers:
         cfg["num_hidden_layers"] = args.layers
     mcfg = LlamaConfig(**cfg, attn_implementation=args.attn, enable_gradient_checkpointing=args.ckpt,
-                       loss_chunk_size=args.seq * args.micro_batch)
+                       loss_chunk_size=args.loss_chunk)
     torch.manual_seed(1234)
     model = Llama(mcfg, pc, dtype=torch.bfloat16, device=device)
     model.init_weights(seed=1234)
     stage = args.zero_stage if args.zero_stage is not None else (0 if pc.dp_size == 1 else 2)
     engine = DataParallelEngine(model, pc, stage, lr=3e-5, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
-                                offload_optimizer=args.offload_optimizer)
+                                offload_optimizer=args.offload_optimizer, force_sharded=args.force_sharded)
     lm = CLM({"model": None})
     lm.model = model
     lm.train()
@@ -139,7 +150,8 @@ def main():
             "config": {"model": "Llama-3-8B" if not args.layers else f"Llama-3-8B-{args.layers}L(INVALID-debug)",
                        "global_batch": pc.dp_size * B, "seq_len": S, "parallelism": par, "zero_stage": stage,
                        "attn": args.attn, "activation_checkpointing": args.ckpt, "optimizer": ("host AdamW (offload) fp32 master" if args.offload_optimizer else "fused AdamW fp32 master"),
-                       "grad_clip": 1.0, "gemm_tuning": gemm_mode},
+                       "grad_clip": 1.0, "gemm_tuning": gemm_mode,
+                       **({"force_sharded": True} if args.force_sharded else {})},
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "mfu": round(tps / world * fpt / 2.5e15, 4),
             "tflops_per_gpu": round(tps / world * fpt / 1e12, 1),
@@ -147,7 +159,7 @@ def main():
             "final_loss": round(final_loss, 4),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

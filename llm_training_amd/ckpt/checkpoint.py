@@ -1,79 +1,131 @@
-"""Sharded, resumable, reshard-able training checkpoints.
+"""Sharded, resumable, reshard-able training checkpoints: one file per rank, no full gather.
 
 Reference behaviour: Lightning checkpoint dict with state_dict / optimizer / lr scheduler / loop
-progress / config (src/llm_training/lightning/strategy/fsdp2/fsdp2_strategy.py:315-409,
-callbacks/save_config_callback.py:42-44) and the resumable data loader (data/resumable_dataloader.py).
+progress / config (src/llm_training/lightning/strategy/fsdp2/fsdp2_strategy.py:315-409 —
+FSDP2 writes DCP shards per rank; callbacks/save_config_callback.py:42-44) and the resumable data
+loader (data/resumable_dataloader.py).
 
 Layout of ``<dir>/``:
-- ``meta.json``            step / epoch / batch_idx / consumed counters / scheduler / parallel layout /
-                           the resolved YAML config (so ``convert-to-hf`` can rebuild the model)
-- ``tp{t}.safetensors``    for every tensor-parallel rank t (written by data-parallel rank 0 of that
-                           TP group): ``model.<param>`` (training dtype), ``master.<param>``,
-                           ``exp_avg.<param>``, ``exp_avg_sq.<param>`` (fp32), keyed by parameter name
-Keying by parameter name (not flat-buffer offset) makes the checkpoint independent of the
-data-parallel size and ZeRO stage: a run saved at dp=8 / stage 3 resumes at dp=2 / stage 2. A change of
-the tensor-parallel size is handled by merging the TP files with the model's shard rules.
+- ``meta.json``                      step / epoch / batch_idx / consumed counters / scheduler / parallel
+                                     layout / the resolved YAML config (so ``convert-to-hf`` can rebuild
+                                     the model). Written last by rank 0 — its presence plus every rank's
+                                     ``.done`` marker means the checkpoint is complete.
+- ``shard-tp{t}-dp{d}.safetensors``  what rank (t, d) owns: for every trainable parameter the slice of
+                                     its flattened ``master`` / ``exp_avg`` / ``exp_avg_sq`` (fp32) that
+                                     falls in this rank's range of the unit's flat buffer (its ZeRO shard;
+                                     at stage 0 the DP ranks split the replicated state so every rank
+                                     writes 1/dp), and ``model.<name>`` in full for frozen parameters.
+- ``shard-tp{t}-dp{d}.json``         index: key -> [start, end, full shape] in flattened-parameter
+                                     elements.
+- ``shard-tp{t}-dp{d}.done``         written after the rank's files are closed.
+
+Each rank moves only its own shard to the host (12 B/param / dp) and the files are written on a
+background thread (``save_checkpoint(..., async_write=True)``; the next save or ``wait_for_pending_saves``
+joins it). Loading reads, for every local parameter range of the NEW layout, only the overlapping
+pieces (safetensors ``get_slice``), so any (dp, ZeRO stage) saved layout loads into any other; a
+tensor-parallel size change assembles one full parameter at a time and re-shards it with the model's
+own TP rules. bf16 parameters are re-derived from the fp32 masters (the fused AdamW writes them from
+the master in the first place).
 """
 from __future__ import annotations
 
 import json
 import logging
 import os
+import threading
 from pathlib import Path
 
 import torch
 import torch.distributed as dist
-from safetensors.torch import load_file, save_file
+from safetensors import safe_open
+from safetensors.torch import save_file
 
 logger = logging.getLogger("llm_training")
 
-
-def _unit_full(engine, u, t: torch.Tensor) -> torch.Tensor:
-    """All-gather a unit's DP shard into the full flat tensor (no-op when not sharded)."""
-    dp = engine._udp(u)
-    if engine._ustage(u) == 0 or dp == 1:
-        return t
-    full = torch.empty(u.numel, dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(full, t.contiguous(), group=engine.group)
-    return full
+FORMAT = "llm_training_amd/v2"
+KINDS = ("master", "exp_avg", "exp_avg_sq")
+_pending: list[threading.Thread] = []
 
 
-def collect_state(trainer) -> dict[str, torch.Tensor]:
-    """Per-parameter model / master / Adam state of this TP rank (full over DP), on CPU."""
+def shard_name(tp: int, dp: int) -> str:
+    return f"shard-tp{tp}-dp{dp}"
+
+
+def wait_for_pending_saves():
+    while _pending:
+        _pending.pop(0).join()
+
+
+def _write_range(engine, u) -> tuple[int, int]:
+    """Flat range of unit ``u`` that this rank writes: its ZeRO shard, or its 1/dp part of replicated
+    state (stage 0), or everything on dp rank 0 (TP-replicated units)."""
+    dp = u.dp
+    r = engine.pc.dp_rank if dp > 1 else 0
+    sn = u.numel // dp
+    if u.replicated and engine.pc.dp_rank != 0:
+        return 0, 0
+    return r * sn, (r + 1) * sn
+
+
+def collect_shard(trainer) -> tuple[dict[str, torch.Tensor], dict[str, list]]:
+    """This rank's pieces (CPU tensors) and their index."""
     eng = trainer.engine
     model = trainer.lm.model
     names = {id(p): n for n, p in model.named_parameters()}
-    out: dict[str, torch.Tensor] = {}
-    with eng.full_params_context():
+    eng.wait_params()
+    tensors: dict[str, torch.Tensor] = {}
+    index: dict[str, list] = {}
+    for u in eng.units:
+        a, b = _write_range(eng, u)
+        if b <= a:
+            continue
+        sa, _ = eng.shard_range(u)  # where the locally held optimizer state starts in flat coords
+        for p, o in zip(u.params, u.offsets):
+            s, e = max(o, a), min(o + p.numel(), b)
+            if e <= s:
+                continue
+            n = names[id(p)]
+            for kind in KINDS:
+                src = getattr(u, kind)
+                piece = src[s - sa:e - sa]
+                tensors[f"{kind}.{n}"] = piece.detach().to("cpu", copy=True)
+                index[f"{kind}.{n}"] = [s - o, e - o, list(p.shape)]
+    if eng.pc.dp_rank == 0:  # frozen parameters are not engine units: always resident in full
         for n, p in model.named_parameters():
             if not p.requires_grad:
-                out["model." + n] = p.detach().cpu()
-        for u in eng.units:
-            fulls = {k: _unit_full(eng, u, getattr(u, k)) for k in ("master", "exp_avg", "exp_avg_sq")}
-            pflat = u.pflat if u.pflat.untyped_storage().size() else None
-            for p, o in zip(u.params, u.offsets):
-                n = names[id(p)]
-                sl = slice(o, o + p.numel())
-                out["model." + n] = (pflat[sl] if pflat is not None else fulls["master"][sl].to(p.dtype)).view(
-                    p.shape).cpu().clone()
-                for k, f in fulls.items():
-                    out[f"{k}.{n}"] = f[sl].view(p.shape).cpu().clone()
-    return out
+                tensors["model." + n] = p.detach().reshape(-1).to("cpu", copy=True)
+                index["model." + n] = [0, p.numel(), list(p.shape)]
+    return tensors, index
 
 
-def save_checkpoint(trainer, path: str):
+def _write_files(path: str, base: str, tensors: dict, index: dict):
+    save_file({k: v.contiguous() for k, v in tensors.items()}, os.path.join(path, base + ".safetensors"))
+    with open(os.path.join(path, base + ".json"), "w") as f:
+        json.dump(index, f)
+    Path(path, base + ".done").touch()
+
+
+def save_checkpoint(trainer, path: str, async_write: bool = False):
     pc = trainer.pc
-    state = collect_state(trainer)
-    if pc.dp_rank == 0:
-        os.makedirs(path, exist_ok=True)
-        save_file({k: v.contiguous() for k, v in state.items()}, os.path.join(path, f"tp{pc.tp_rank}.safetensors"))
+    wait_for_pending_saves()
+    tensors, index = collect_shard(trainer)
+    os.makedirs(path, exist_ok=True)
+    base = shard_name(pc.tp_rank, pc.dp_rank)
+    if async_write:
+        t = threading.Thread(target=_write_files, args=(path, base, tensors, index), daemon=False)
+        t.start()
+        _pending.append(t)
+    else:
+        _write_files(path, base, tensors, index)
     if pc.rank == 0:
+        eng = trainer.engine
         meta = {
-            "format": "llm_training_amd/v1",
+            "format": FORMAT,
             "trainer": trainer.state.state_dict(),
             "scheduler": trainer.scheduler.state_dict() if trainer.scheduler else None,
-            "optimizer_step": trainer.engine.step_count,
-            "tp_size": pc.tp_size, "dp_size": pc.dp_size, "zero_stage": trainer.engine.stage,
+            "optimizer_step": eng.step_count,
+            "tp_size": pc.tp_size, "dp_size": pc.dp_size, "zero_stage": eng.stage,
+            "param_dtype": str(eng.param_dtype).replace("torch.", ""),
             "config": trainer.config_dict,
             "model_class": f"{type(trainer.lm.model).__module__}.{type(trainer.lm.model).__qualname__}",
             "model_config": trainer.lm.model.config.model_dump(mode="json"),
@@ -83,7 +135,7 @@ def save_checkpoint(trainer, path: str):
     if dist.is_initialized():
         dist.barrier()
     if pc.rank == 0:
-        logger.info("saved checkpoint %s", path)
+        logger.info("saved checkpoint %s%s", path, " (files written in the background)" if async_write else "")
 
 
 def read_meta(path: str) -> dict:
@@ -91,39 +143,110 @@ def read_meta(path: str) -> dict:
         return json.load(f)
 
 
-def load_tp_state(path: str, model, tp_rank: int, tp_size: int) -> dict[str, torch.Tensor]:
-    """State of ``tp_rank`` under the current tp size (merging / re-sharding saved TP files if needed)."""
-    meta = read_meta(path)
-    saved_tp = int(meta.get("tp_size", 1))
-    if saved_tp == tp_size:
-        return load_file(os.path.join(path, f"tp{tp_rank}.safetensors"))
-    parts = [load_file(os.path.join(path, f"tp{t}.safetensors")) for t in range(saved_tp)]
-    return reshard_tp(parts, model, saved_tp)
+def is_complete(path: str | os.PathLike) -> bool:
+    p = Path(path)
+    if not (p / "meta.json").is_file():
+        return False
+    try:
+        meta = json.loads((p / "meta.json").read_text())
+    except (ValueError, OSError):
+        return False
+    tp, dp = int(meta.get("tp_size", 1)), int(meta.get("dp_size", 1))
+    return all((p / (shard_name(t, d) + ".done")).is_file() for t in range(tp) for d in range(dp))
 
 
-def reshard_tp(parts: list[dict], model, saved_tp: int) -> dict[str, torch.Tensor]:
+class ShardReader:
+    """Reads element ranges of flattened parameters from the per-rank pieces of a checkpoint."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.meta = read_meta(path)
+        self.tp = int(self.meta.get("tp_size", 1))
+        self.dp = int(self.meta.get("dp_size", 1))
+        dt = self.meta.get("param_dtype", "bfloat16")
+        self.param_dtype = getattr(torch, dt) if isinstance(dt, str) else torch.bfloat16
+        # per tp rank: key -> [(start, end, shape, file)]
+        self.pieces: list[dict[str, list]] = [dict() for _ in range(self.tp)]
+        for t in range(self.tp):
+            for d in range(self.dp):
+                base = shard_name(t, d)
+                with open(os.path.join(path, base + ".json")) as f:
+                    idx = json.load(f)
+                fn = os.path.join(path, base + ".safetensors")
+                for k, (s, e, shape) in idx.items():
+                    self.pieces[t].setdefault(k, []).append((s, e, tuple(shape), fn))
+        self._files: dict[str, object] = {}
+
+    def _file(self, fn):
+        f = self._files.get(fn)
+        if f is None:
+            f = safe_open(fn, framework="pt", device="cpu")
+            self._files[fn] = f
+        return f
+
+    def has(self, t: int, key: str) -> bool:
+        return key in self.pieces[t]
+
+    def shape(self, t: int, key: str) -> tuple:
+        return self.pieces[t][key][0][2]
+
+    def read(self, t: int, key: str, s: int, e: int) -> torch.Tensor:
+        """Elements [s, e) of the flattened tensor ``key`` of saved TP rank ``t``."""
+        out = None
+        covered = 0
+        for ps, pe, _, fn in self.pieces[t][key]:
+            a, b = max(s, ps), min(e, pe)
+            if b <= a:
+                continue
+            sl = self._file(fn).get_slice(key)[a - ps:b - ps]
+            if out is None:
+                out = torch.empty(e - s, dtype=sl.dtype)
+            out[a - s:b - s] = sl
+            covered += b - a
+        if covered != e - s:
+            raise KeyError(f"checkpoint {self.path}: {key}[{s}:{e}] not fully covered ({covered} of {e - s})")
+        return out
+
+    def full(self, t: int, key: str) -> torch.Tensor:
+        shape = self.shape(t, key)
+        n = 1
+        for x in shape:
+            n *= x
+        return self.read(t, key, 0, n).view(shape)
+
+
+def _tp_unshard(model, name: str, parts: list[torch.Tensor]) -> torch.Tensor:
     from ..parallel import tensor_parallel as tpl
-    full: dict[str, torch.Tensor] = {}
-    for key in parts[0]:
-        prefix, name = key.split(".", 1)
-        kind, sizes = model._tp_rule(name) if hasattr(model, "_tp_rule") else ("rep", None)
-        ts = [p[key] for p in parts]
-        if saved_tp == 1 or kind == "rep":
-            full[key] = ts[0]
-        elif kind == "fused":
-            full[key] = tpl.unshard_fused_rows(ts, sizes)
-        elif kind == "cols":
-            full[key] = torch.cat(ts, 1)
-        else:
-            full[key] = torch.cat(ts, 0)[: model.config.vocab_size]
-    # re-shard for this rank with the model's own rules, per state kind
-    out = {}
-    for prefix in ("model", "master", "exp_avg", "exp_avg_sq"):
-        sub = {k[len(prefix) + 1:]: v for k, v in full.items() if k.startswith(prefix + ".")}
-        if sub:
-            for k, v in model.shard_full_state_dict(sub).items():
-                out[f"{prefix}.{k}"] = v
-    return out
+    kind, sizes = model._tp_rule(name) if hasattr(model, "_tp_rule") else ("rep", None)
+    if len(parts) == 1 or kind == "rep":
+        return parts[0]
+    if kind == "fused":
+        return tpl.unshard_fused_rows(parts, sizes)
+    if kind == "cols":
+        return torch.cat(parts, 1)
+    return torch.cat(parts, 0)[: model.config.vocab_size]
+
+
+class _LocalParamSource:
+    """Element ranges of this rank's (TP-local) parameters, resharding across TP sizes if needed."""
+
+    def __init__(self, reader: ShardReader, model, tp_rank: int, tp_size: int):
+        self.r, self.model, self.tp_rank, self.tp_size = reader, model, tp_rank, tp_size
+        self.same_tp = reader.tp == tp_size
+        self._cache: tuple[str, torch.Tensor] | None = None
+
+    def has(self, key: str) -> bool:
+        return self.r.has(0, key)
+
+    def read(self, key: str, s: int, e: int) -> torch.Tensor:
+        if self.same_tp:
+            return self.r.read(self.tp_rank, key, s, e)
+        if self._cache is None or self._cache[0] != key:
+            name = key.split(".", 1)[1]
+            full = _tp_unshard(self.model, name, [self.r.full(t, key) for t in range(self.r.tp)])
+            local = (self.model.shard_full_state_dict({name: full})[name] if self.tp_size > 1 else full)
+            self._cache = (key, local.reshape(-1).contiguous())
+        return self._cache[1][s:e]
 
 
 @torch.no_grad()
@@ -132,32 +255,32 @@ def load_checkpoint(trainer, path: str, load_optimizer: bool = True):
         path = os.path.join(os.path.dirname(path), os.readlink(path))
     pc, eng = trainer.pc, trainer.engine
     model = trainer.lm.model
-    meta = read_meta(path)
-    st = load_tp_state(path, model, pc.tp_rank, pc.tp_size)
-    dev = next(model.parameters()).device
-    params = dict(model.named_parameters())
-    # parameters (frozen ones included)
-    with eng.full_params_context():
-        for n, p in params.items():
-            k = "model." + n
-            if k in st:
-                p.data.copy_(st[k].to(dev, p.dtype))
-    # optimizer state: fill full flats then take this rank's shard
+    reader = ShardReader(path)
+    meta = reader.meta
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"{path}: unsupported checkpoint format {meta.get('format')!r} (expected {FORMAT})")
+    src = _LocalParamSource(reader, model, pc.tp_rank, pc.tp_size)
+    names = {id(p): n for n, p in model.named_parameters()}
+    eng.wait_params()
+    # frozen parameters: full tensors
+    for n, p in model.named_parameters():
+        if not p.requires_grad and src.has("model." + n):
+            p.data.copy_(src.read("model." + n, 0, p.numel()).view(p.shape).to(p.device, p.dtype))
+    # trainable: this rank's range of every unit, for each optimizer-state kind
     for u in eng.units:
-        names = {id(p): n for n, p in params.items()}
-        dp, stage = eng._udp(u), eng._ustage(u)
-        r = pc.dp_rank if dp > 1 else 0
-        sn = u.numel // dp
-        for kind in ("master", "exp_avg", "exp_avg_sq"):
-            full = torch.zeros(u.numel, dtype=torch.float32, device=dev)
-            for p, o in zip(u.params, u.offsets):
-                key = f"{kind}.{names[id(p)]}"
-                if key in st and load_optimizer:
-                    full[o:o + p.numel()] = st[key].reshape(-1).to(dev, torch.float32)
-                elif kind == "master":
-                    full[o:o + p.numel()] = st["model." + names[id(p)]].reshape(-1).to(dev, torch.float32)
+        a, b = eng.shard_range(u)
+        for kind in KINDS:
+            if kind != "master" and not load_optimizer:
+                continue
             tgt = getattr(u, kind)
-            tgt.copy_(full[r * sn:(r + 1) * sn] if stage >= 1 else full)
+            for p, o in zip(u.params, u.offsets):
+                s, e = max(o, a), min(o + p.numel(), b)
+                if e <= s:
+                    continue
+                key = f"{kind}.{names[id(p)]}"
+                if not src.has(key):
+                    raise KeyError(f"checkpoint {path} has no {key}")
+                tgt[s - a:e - a].copy_(src.read(key, s - o, e - o).to(torch.float32))
     eng.sync_params_from_master()
     if load_optimizer:
         eng.step_count = int(meta.get("optimizer_step", 0))
@@ -168,10 +291,20 @@ def load_checkpoint(trainer, path: str, load_optimizer: bool = True):
         logger.info("resumed from %s (step %d)", path, trainer.state.global_step)
 
 
-def load_model_state_for_export(path: str) -> tuple[dict, dict[str, torch.Tensor]]:
-    """(meta, full unsharded model state dict) from a checkpoint dir, without any process group."""
-    meta = read_meta(path)
-    tp = int(meta.get("tp_size", 1))
-    parts = [load_file(os.path.join(path, f"tp{t}.safetensors")) for t in range(tp)]
-    parts = [{k[6:]: v for k, v in p.items() if k.startswith("model.")} for p in parts]
-    return meta, parts
+def load_model_state_for_export(path: str) -> tuple[dict, list[dict[str, torch.Tensor]]]:
+    """(meta, per-TP-rank model state dicts) from a checkpoint dir, without any process group.
+
+    Trainable parameters come from the fp32 masters cast to the training dtype (exactly what the
+    fused AdamW wrote into the bf16 parameters), frozen ones from their stored copy."""
+    reader = ShardReader(path)
+    parts = []
+    for t in range(reader.tp):
+        sd = {}
+        for key in reader.pieces[t]:
+            kind, name = key.split(".", 1)
+            if kind == "model":
+                sd[name] = reader.full(t, key)
+            elif kind == "master":
+                sd[name] = reader.full(t, key).to(reader.param_dtype)
+        parts.append(sd)
+    return reader.meta, parts

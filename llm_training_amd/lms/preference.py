@@ -78,8 +78,13 @@ class DPO(_PairMixin, BaseLM):
     def configure_model(self, pc, device, dtype, seed: int = 0, resuming: bool = False):
         super().configure_model(pc, device, dtype, seed, resuming)
         spec = self.config.ref_model
-        if spec is None:
+        if spec is None and not resuming:
             self.ref_model = copy.deepcopy(self.model)
+        elif spec is None:
+            # resuming: the policy holds trained weights (and the checkpoint does not store the frozen
+            # reference), so rebuild the reference from the pre-trained / initial weights instead
+            self.ref_model = build_model(self.config.model, pc, dtype, device)
+            self._load_or_init(self.ref_model, seed, False)
         else:
             if isinstance(spec, dict) and "model_class" in spec:
                 from .base import ModelProvider

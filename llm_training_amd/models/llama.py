@@ -371,13 +371,13 @@ class Llama(BaseModel):
         sd = {k: v.detach() for k, v in self.state_dict().items()}
         pc = self.pc
         if not pc.tp:
-            return {k: v.cpu() for k, v in sd.items()}
+            return {k: v.to("cpu", copy=True) for k, v in sd.items()}
         import torch.distributed as dist
         out = {}
         for k, v in sd.items():
             kind, sizes = self._tp_rule(k)
             if kind == "rep":
-                out[k] = v.cpu()
+                out[k] = v.to("cpu", copy=True)
                 continue
             parts = [torch.empty_like(v) for _ in range(pc.tp_size)]
             dist.all_gather(parts, v.contiguous(), group=pc.tp_group)

@@ -3,11 +3,15 @@
 GPU tensors run the hand-written gfx950 kernels of ``csrc/`` (loaded by :mod:`.native`); CPU tensors
 run :mod:`.reference`. Weight gradients support *gradient-buffer views*: when a parameter carries a
 ``main_grad`` tensor (a view into the flat per-unit gradient buffer owned by
-:class:`llm_training_amd.parallel.grad_buffer.GradBuffer`), the backward writes (first micro-batch)
+:class:`llm_training_amd.parallel.engine.DataParallelEngine`), the backward writes (first micro-batch)
 or accumulates (later micro-batches) the weight gradient straight into it and returns ``None`` to
 autograd — the same trick as fusing gradient accumulation into the weight-gradient GEMM, so there
 is no separate ``param.grad`` tensor, no ``grad += new`` pass and the ZeRO engine can reduce-scatter
 the flat buffer as soon as a unit's backward is done.
+
+The parameter itself is kept on ``ctx`` (not only in ``save_for_backward``): under non-reentrant
+activation checkpointing the saved tensors are recomputed and unpacked as DETACHED aliases, which
+carry no ``main_grad`` — the gradient would silently bypass the flat buffer.
 
 Reference parity: these replace the Liger wrappers of src/llm_training/ops/liger_kernel/*.py and
 flash-attn calls of src/llm_training/ops/attention_op.py.
@@ -22,9 +26,6 @@ from torch.autograd import Function
 
 from . import reference as ref
 from .native import lib, use_native
-
-# ----------------------------------------------------------------------------- gradient-buffer helpers
-
 
 # ----------------------------------------------------------------------------- GEMM dispatch
 # The three GEMMs of a linear layer run on the hand-written gfx950 kernel (csrc/gemm.hip) or on
@@ -124,7 +125,8 @@ def _wgrad_vec(w: torch.Tensor, g: torch.Tensor):
 class _LinearFn(Function):
     @staticmethod
     def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
+        ctx.save_for_backward(x)
+        ctx.w = w
         ctx.has_bias = b is not None
         y = mm_nt(x.reshape(-1, x.shape[-1]), w).view(*x.shape[:-1], w.shape[0])
         if b is not None:
@@ -133,7 +135,8 @@ class _LinearFn(Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        (x,) = ctx.saved_tensors
+        w = ctx.w
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -158,12 +161,14 @@ class _RMSNormFn(Function):
         L = lib()
         x = x.contiguous()
         y, _, rstd = L.rmsnorm_fwd(x, None, w, eps)
-        ctx.save_for_backward(x, w, rstd)
+        ctx.save_for_backward(x, rstd)
+        ctx.w = w
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, rstd = ctx.saved_tensors
+        x, rstd = ctx.saved_tensors
+        w = ctx.w
         L = lib()
         need_w = ctx.needs_input_grad[1]
         mg = getattr(w, "main_grad", None) if need_w else None
@@ -187,12 +192,14 @@ class _AddRMSNormFn(Function):
     def forward(ctx, x, res, w, eps):
         L = lib()
         y, s, rstd = L.rmsnorm_fwd(x.contiguous(), res.contiguous(), w, eps)
-        ctx.save_for_backward(s, w, rstd)
+        ctx.save_for_backward(s, rstd)
+        ctx.w = w
         return y, s
 
     @staticmethod
     def backward(ctx, dy, ds):
-        s, w, rstd = ctx.saved_tensors
+        s, rstd = ctx.saved_tensors
+        w = ctx.w
         L = lib()
         need_w = ctx.needs_input_grad[2]
         mg = getattr(w, "main_grad", None) if need_w else None
@@ -216,13 +223,15 @@ class _RefRMSNormFn(Function):
 
     @staticmethod
     def forward(ctx, x, w, eps):
-        ctx.save_for_backward(x, w)
+        ctx.save_for_backward(x)
+        ctx.w = w
         ctx.eps = eps
         return ref.rms_norm(x, w, eps)
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        (x,) = ctx.saved_tensors
+        w = ctx.w
         with torch.enable_grad():
             xd = x.detach().requires_grad_(True)
             wd = w.detach().requires_grad_(True)
@@ -403,13 +412,30 @@ def _ref_rope_attention(qkv, positions, cos, sin, n_q, n_kv, causal, segment_ids
 # ----------------------------------------------------------------------------- cross entropy
 
 
-class _FusedLinearCEFn(Function):
-    """loss = mean_{valid rows} CE(h @ W^T, labels), logits produced chunk by chunk.
+def _apply_weight_grad(w: torch.Tensor, dw: torch.Tensor, g: torch.Tensor):
+    """Add g * dw (g: 0-dim device scalar) into ``w.main_grad`` (returns None), or return it."""
+    mg = getattr(w, "main_grad", None)
+    gs = g.to(dw.dtype)
+    if mg is None:
+        return (dw * gs).to(w.dtype)
+    mg2 = mg.view(dw.shape)
+    if getattr(w, "grad_added", False):
+        mg2.addcmul_(dw.to(mg.dtype), gs.to(mg.dtype))
+    else:
+        torch.mul(dw, gs, out=mg2) if mg.dtype == dw.dtype else mg2.copy_(dw * gs)
+    w.grad_added = True
+    return None
 
-    Forward: per row chunk, one hipBLASLt GEMM for the bf16 logits, then the HIP CE kernel computes
-    the loss AND overwrites the logits with d loss / d logits (scaled by 1/n_valid read from device
-    memory — no host sync). Backward: dh = g * dlogits @ W and dW (+)= dlogits^T @ (g * h), written
-    straight into W's gradient buffer.
+
+class _FusedLinearCEFn(Function):
+    """loss = mean_{valid rows} CE(h @ W^T, labels), memory bounded by ONE logits chunk.
+
+    Forward, per row chunk (Liger-style gradient-in-forward): one GEMM for the bf16
+    logits, the HIP CE kernel computes the loss rows AND overwrites the logits with d loss / d logits
+    (scaled by 1/n_valid read from device memory — no host sync), then the same chunk's dh rows and its
+    dW contribution are computed right away and the chunk's logits are dropped. Only dh [N, H] and dW
+    [V, H] survive to the backward, which scales them by the incoming gradient (1 for a plain loss)
+    and accumulates dW into the weight's flat gradient buffer.
     """
 
     @staticmethod
@@ -419,36 +445,37 @@ class _FusedLinearCEFn(Function):
         valid = (labels != ignore_index).sum()
         inv_n = (1.0 / valid.clamp(min=1).float()).reshape(1)
         loss_rows = torch.empty(N, device=h.device, dtype=torch.float32)
-        grads = []
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dh = torch.empty_like(h) if need_h else None
+        dw = torch.empty(w.shape, device=w.device, dtype=w.dtype) if need_w else None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, inv_n, True)
             loss_rows[s0:s1] = lr
-            grads.append(lg)
-        ctx.save_for_backward(h, w, *grads)
-        ctx.chunk = chunk
+            if need_h:
+                mm_nn(lg, w, out=dh[s0:s1])
+            if need_w:
+                if s0 == 0:
+                    torch.mm(lg.t(), h[s0:s1], out=dw)
+                else:
+                    dw.addmm_(lg.t(), h[s0:s1])
+            del lg
+        ctx.save_for_backward(*(t for t in (dh, dw) if t is not None))
+        ctx.has = (need_h, need_w)
+        ctx.w = w
         return loss_rows.sum() * inv_n[0]
 
     @staticmethod
     def backward(ctx, g):
-        h, w, *grads = ctx.saved_tensors
-        chunk = ctx.chunk
-        dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
-        hs = h * g.to(h.dtype)
-        dw_acc = None
-        for i, lg in enumerate(grads):
-            s0 = i * chunk
-            s1 = s0 + lg.shape[0]
-            if dh is not None:
-                mm_nn(lg, w, out=dh[s0:s1])
-            if ctx.needs_input_grad[1]:
-                r = _wgrad_mm(w, lg.t(), hs[s0:s1])
-                if r is not None:
-                    dw_acc = r if dw_acc is None else dw_acc + r
+        saved = list(ctx.saved_tensors)
+        need_h, need_w = ctx.has
+        dh = saved.pop(0) if need_h else None
+        dw = saved.pop(0) if need_w else None
         if dh is not None:
-            dh.mul_(g.to(dh.dtype))
-        return dh, dw_acc, None, None, None
+            dh = dh * g.to(dh.dtype)
+        dwr = _apply_weight_grad(ctx.w, dw, g) if dw is not None else None
+        return dh, dwr, None, None, None
 
 
 def fused_linear_cross_entropy(h, w, labels, ignore_index: int = -100, chunk_size: int = 8192):
@@ -503,13 +530,15 @@ class _LinearLogpsFn(Function):
             lg = mm_nt(h[s0:s1], w)
             _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, None, False)
             out[s0:s1] = -lr
-        ctx.save_for_backward(h, w, labels)
+        ctx.save_for_backward(h, labels)
+        ctx.w = w
         ctx.cfg = (ignore_index, chunk)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        h, w, labels = ctx.saved_tensors
+        h, labels = ctx.saved_tensors
+        w = ctx.w
         ignore_index, chunk = ctx.cfg
         L = lib()
         N = h.shape[0]

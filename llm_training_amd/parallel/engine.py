@@ -2,7 +2,7 @@
 
 Replaces the reference's two strategy back-ends — DeepSpeed ZeRO (SURVEY K13/P2/P3,
 src/llm_training/lightning/strategy/deepspeed/deepspeed_strategy.py) and FSDP2 fully_shard + the
-MasterWeightsOptimizer wrapper (P4/C15, lightning/strategy/fsdp2/fsdp2_strategy.py:249-263,
+MasterWeightsOptimizer wrapper (P4/C15, lightning/strategy/fsdp2/fsdp2_strategy.py:249-263,430-442,
 optim/master_weight_wrapper.py) — with one engine designed around MI355X:
 
 * **Units.** The model declares its FSDP units (embedding, each decoder layer, final norm + lm_head).
@@ -14,6 +14,11 @@ optim/master_weight_wrapper.py) — with one engine designed around MI355X:
   see ops/fused.py), so a unit is complete when autograd produces the gradient of the unit's INPUT —
   a tensor hook on that input launches the unit's reduce-scatter (ZeRO) or all-reduce (DDP) on a
   dedicated communication stream while backward continues with the previous unit.
+* **Gradient sharding (stage >= 2).** A decoder layer's full-size gradient buffer exists only while
+  that layer's backward runs: a hook on the layer OUTPUT's gradient allocates it, the input-gradient
+  hook reduce-scatters it into the persistent 1/dp shard (accumulating across micro-batches, like
+  DeepSpeed stage 2's per-micro-batch reduction, deepspeed_strategy.py:40-44) and frees it. Resident
+  gradient memory is 2 B/param / dp plus at most a couple of in-flight layers.
 * **Optimizer.** fp32 master weights, Adam m and v exist only for this rank's shard of each unit
   (stage >= 1) — 12 B/param / dp — and are updated by ONE fused HIP AdamW launch per unit that also
   writes the bf16 parameter shard. Gradient averaging (1/dp), accumulation (1/accum) and clipping are
@@ -21,17 +26,24 @@ optim/master_weight_wrapper.py) — with one engine designed around MI355X:
 * **Parameters.** stage 0-2 keep the full bf16 parameters resident (an 8B model is 16 GB of 288 GB);
   after the step each unit's shard is all-gathered in place on the comm stream and the next forward
   waits for that unit only. Stage 3 keeps only the shard and all-gathers a unit right before its
-  forward (prefetching the next unit) and again before its backward, freeing it afterwards.
+  forward (prefetching the next unit), frees it after the forward (``reshard_after_forward``),
+  re-gathers it when its output gradient arrives (prefetching the previous unit) and frees it again
+  once its backward is done. Activation-checkpoint recomputation runs inside backward and is detected
+  (autograd graph task active): it neither prefetches forward nor releases the unit it recomputes.
+* **Sharded mode at dp = 1.** ``force_sharded=True`` (env ``LLMT_FORCE_SHARDED=1``) runs every
+  dp > 1 code path — comm stream, events, reduce-scatter / all-gather, stage-3 free / regather /
+  prefetch, transient gradients — over a one-rank process group, so a single GPU executes exactly
+  the schedule an 8-GPU node runs (tests/test_engine_gpu.py).
 
 * **Optimizer offload** (``offload_optimizer=True``; DeepSpeed ``offload_optimizer`` / FSDP2
   ``offload_policy``, deepspeed_strategy.py:22-27, fsdp2_strategy.py:58): master / m / v shards live
-  in pinned host memory (12 B/param / dp off the GPU). At the step every unit's bf16 gradient shard is
+  in pinned host memory (12 B/param / dp off the GPU). At the step every unit's gradient shard is
   copied down on a copy stream up front; the host walks the units in order, waits for that unit's
   copy, runs the native C++ AdamW (csrc/cpu_adam.cpp, ATen thread pool) and queues the bf16 shard's
   upload, so the PCIe traffic of unit i+1 overlaps the host math of unit i and the next forward only
   waits for its own unit.
 
-Checkpoint layout (see ckpt/): per-unit shards of master / m / v plus the step counter.
+Checkpoint layout (see ckpt/): per-rank shards of master / m / v / params plus a JSON index.
 """
 from __future__ import annotations
 
@@ -57,6 +69,11 @@ def _round_up(n: int, m: int) -> int:
     return (n + m - 1) // m * m
 
 
+def _in_backward() -> bool:
+    """True while the autograd engine runs a backward pass (e.g. activation-checkpoint recompute)."""
+    return torch._C._current_graph_task_id() != -1
+
+
 @dataclass
 class _Unit:
     idx: int
@@ -64,28 +81,30 @@ class _Unit:
     params: list[nn.Parameter]
     offsets: list[int]
     numel: int                      # padded flat size (multiple of dp * ALIGN)
+    dp: int = 1                     # data-parallel degree of this unit (1 for TP-replicated units)
     pflat: torch.Tensor | None = None     # full bf16 params (stage <3: persistent)
-    gflat: torch.Tensor | None = None     # full gradient buffer
+    gflat: torch.Tensor | None = None     # full gradient buffer (transient at stage >= 2)
     pshard: torch.Tensor | None = None    # stage 3: persistent bf16 shard
-    gshard: torch.Tensor | None = None    # reduced gradient shard (stage >= 1)
+    gshard: torch.Tensor | None = None    # reduced gradient shard (stage >= 1, sharded)
     master: torch.Tensor | None = None    # fp32 master (shard or full)
     exp_avg: torch.Tensor | None = None
     exp_avg_sq: torch.Tensor | None = None
-    ready: bool = False
     reduced: bool = False
+    gshard_valid: bool = False      # gshard holds this step's first reduced micro-batch
     gathered: bool = True
     ag_event: object = None
-    rs_event: object = None
     hook_handles: list = field(default_factory=list)
     opt_event: object = None        # async AdamW of this unit done (stage 3 shard update)
     replicated: bool = False
     keep_gathered: bool = False     # stage 3: params used outside the hooked module's forward
-    g_host: torch.Tensor | None = None    # optimizer offload: pinned bf16 gradient shard
+    transient_grad: bool = False    # gradient buffer allocated per backward, freed after its reduce
+    grad_gaps: list = field(default_factory=list)  # alignment padding ranges of the flat buffer
+    g_host: torch.Tensor | None = None    # optimizer offload: pinned gradient shard
     p_host: torch.Tensor | None = None    # optimizer offload: pinned bf16 parameter shard
 
     @property
     def shard_numel(self):
-        return self.numel // max(1, getattr(self, "_dp", 1))
+        return self.numel // self.dp
 
 
 class DataParallelEngine:
@@ -93,15 +112,23 @@ class DataParallelEngine:
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01,
                  grad_dtype: torch.dtype | None = None, reduce_dtype: torch.dtype | None = None,
                  reshard_after_forward: bool = True, overlap_comm: bool = True, overlap_step: bool = True,
-                 offload_optimizer: bool = False):
+                 offload_optimizer: bool = False, force_sharded: bool | None = None,
+                 shard_gradients: bool | None = None):
         self.model = model
         self.offload = bool(offload_optimizer)
         self.pc = pc
         self.stage = int(zero_stage)
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.dp = pc.dp_size
-        self.group = pc.dp_group if pc.dp else None
-        self.overlap = overlap_comm and self.dp > 1
+        if force_sharded is None:
+            force_sharded = os.environ.get("LLMT_FORCE_SHARDED", "0") not in ("0", "", "false")
+        self.sharded = self.dp > 1 or bool(force_sharded)
+        self.group = pc.dp_group
+        if self.sharded and self.group is None:
+            if not dist.is_initialized():
+                raise RuntimeError("force_sharded needs an initialised process group (a one-rank group is fine)")
+            self.group = dist.group.WORLD
+        self.overlap = overlap_comm and self.sharded
         self.reshard_after_forward = reshard_after_forward
         self.step_count = 0
         self.accum = 1
@@ -121,6 +148,10 @@ class DataParallelEngine:
         # models built from our fused ops write weight grads straight into the flat buffers; others
         # (transformers modules) leave ordinary .grad tensors that are absorbed after backward
         self.autograd_grads = not getattr(model, "writes_main_grad", True)
+        if shard_gradients is None:
+            shard_gradients = os.environ.get("LLMT_SHARD_GRADS", "1") != "0"
+        self.shard_gradients = (bool(shard_gradients) and self.stage >= 2 and self.sharded
+                                and not self.autograd_grads)
         self.param_dtype = next(model.parameters()).dtype
         self.grad_dtype = grad_dtype or self.param_dtype
         self.reduce_dtype = reduce_dtype or self.grad_dtype
@@ -161,47 +192,68 @@ class DataParallelEngine:
             groups.append((m, params, False))
         if rep:
             groups.append((None, rep, True))
+        n_named = len(groups) - (1 if rep else 0)
         for i, (m, params, replicated) in enumerate(groups):
-            self.units.append(self._make_unit(i, m, params, replicated))
-            self.units[-1].keep_gathered = i in multi or i == len(groups) - 1
+            u = self._make_unit(i, m, params, replicated, keep=(i in multi or i == n_named - 1))
+            self.units.append(u)
         nparams = sum(p.numel() for u in self.units for p in u.params)
-        logger.info("engine: %d units, %.3f B trainable params (local), zero stage %d, dp %d, tp %d",
-                    len(self.units), nparams / 1e9, self.stage, self.dp, self.pc.tp_size)
+        logger.info("engine: %d units, %.3f B trainable params (local), zero stage %d, dp %d, tp %d%s%s",
+                    len(self.units), nparams / 1e9, self.stage, self.dp, self.pc.tp_size,
+                    ", sharded(forced)" if self.sharded and self.dp == 1 else "",
+                    ", sharded grads" if self.shard_gradients else "")
 
-    def _make_unit(self, i, m, params, replicated: bool) -> _Unit:
+    def _make_unit(self, i, m, params, replicated: bool, keep: bool) -> _Unit:
         # a replicated unit (TP only) keeps full fp32 masters everywhere and all-reduces over the world
         dp = 1 if replicated else self.dp
         offs, n = [], 0
+        gaps = []
         for p in params:
             offs.append(n)
-            n = _round_up(n + p.numel(), ALIGN)
+            end = n + p.numel()
+            n = _round_up(end, ALIGN)
+            if n > end:
+                gaps.append((end, n))
         numel = _round_up(max(n, 1), ALIGN * dp)
-        u = _Unit(i, m, params, offs, numel)
-        u._dp = dp
+        if numel > n:
+            gaps.append((n, numel))
+        if not params:
+            gaps = [(0, numel)]
+        u = _Unit(i, m, params, offs, numel, dp=dp)
         u.replicated = replicated
+        u.keep_gathered = keep
+        u.grad_gaps = gaps
         dev, dt = self.device, self.param_dtype
         pflat = torch.zeros(numel, device=dev, dtype=dt)
         for p, o in zip(params, offs):
             pflat[o:o + p.numel()].copy_(p.detach().reshape(-1))
             p.data = pflat[o:o + p.numel()].view(p.shape)
         u.pflat = pflat
+        sharded = self._usharded(u)
+        # decoder layers (hooked, not the first / last unit) get transient full gradient buffers;
+        # the embedding and the lm_head unit receive gradients outside their module's backward window
+        # (tied weights, the fused loss head) and keep theirs
+        u.transient_grad = (self.shard_gradients and sharded and not keep and i > 0 and m is not None
+                            and _hookable(m))
         u.gflat = torch.zeros(numel, device=dev, dtype=self.grad_dtype)
         for p, o in zip(params, offs):
             p.main_grad = u.gflat[o:o + p.numel()].view(p.shape)
             p.grad_added = False
+        if u.transient_grad:
+            u.gflat.untyped_storage().resize_(0)
         sn = numel // dp
         r = self.pc.dp_rank if dp > 1 else 0
-        stage = 0 if replicated else self.stage
+        stage = self._ustage(u)
         if stage >= 1:
             u.master = pflat[r * sn:(r + 1) * sn].float().clone()
-            if dp > 1:
+            if sharded:
                 u.gshard = torch.zeros(sn, device=dev, dtype=self.reduce_dtype)
         else:
             u.master = pflat.float().clone()
         if self.offload:
             pin = self.cuda
             u.master = u.master.cpu().pin_memory() if pin else u.master.cpu()
-            u.g_host = torch.empty(u.master.numel(), dtype=self.grad_dtype, pin_memory=pin)
+            gdt = self.reduce_dtype if (stage >= 1 and sharded) else self.grad_dtype
+            u.g_host = torch.empty(u.master.numel(), dtype=gdt, pin_memory=pin)
             # bf16 models: the host kernel also writes the bf16 copy that is uploaded; fp32 models
             # upload the master itself
             if self.param_dtype == torch.bfloat16:
@@ -210,7 +262,7 @@ class DataParallelEngine:
         u.exp_avg_sq = torch.zeros_like(u.master)
         if self.offload and self.cuda:
             u.exp_avg, u.exp_avg_sq = u.exp_avg.pin_memory(), u.exp_avg_sq.pin_memory()
-        if stage >= 3 and dp > 1:
+        if stage >= 3 and sharded:
             u.pshard = pflat[r * sn:(r + 1) * sn].clone()
             self._free_full(u)
         return u
@@ -219,7 +271,22 @@ class DataParallelEngine:
         return 0 if u.replicated else self.stage
 
     def _udp(self, u: _Unit) -> int:
-        return 1 if u.replicated else self.dp
+        return u.dp
+
+    def _usharded(self, u: _Unit) -> bool:
+        """Does this unit take part in the data-parallel sharding collectives?"""
+        return self.sharded and not u.replicated
+
+    def _zero3(self, u: _Unit) -> bool:
+        return self._ustage(u) >= 3 and self._usharded(u)
+
+    def shard_range(self, u: _Unit) -> tuple[int, int]:
+        """[start, end) of this rank's shard in the unit's flat buffer (whole buffer if unsharded)."""
+        if self._ustage(u) >= 1 and self._usharded(u):
+            sn = u.numel // u.dp
+            r = self.pc.dp_rank if u.dp > 1 else 0
+            return r * sn, (r + 1) * sn
+        return 0, u.numel
 
     def _free_full(self, u: _Unit):
         u.pflat.untyped_storage().resize_(0)
@@ -230,26 +297,46 @@ class DataParallelEngine:
         if st.size() == 0:
             st.resize_(u.numel * u.pflat.element_size())
 
+    # ------------------------------------------------------------------ transient gradient buffers
+    def _grad_allocated(self, u: _Unit) -> bool:
+        return u.gflat.untyped_storage().size() > 0
+
+    def _alloc_grad(self, u: _Unit):
+        if self._grad_allocated(u):
+            return
+        u.gflat.untyped_storage().resize_(u.numel * u.gflat.element_size())
+        for a, b in u.grad_gaps:  # alignment padding is reduced too: keep it zero
+            u.gflat[a:b].zero_()
+        for p in u.params:  # fresh buffer: the first gradient written is a copy, not an add
+            p.grad_added = False
+
+    def _free_grad(self, u: _Unit, stream=None):
+        if stream is not None:
+            u.gflat.record_stream(stream)
+        u.gflat.untyped_storage().resize_(0)
+
     # ------------------------------------------------------------------ hooks
     def _install_hooks(self):
         for u in self.units:
             if u.module is None:
                 continue
             u.hook_handles.append(u.module.register_forward_pre_hook(self._make_pre_fwd(u)))
-            if self.stage >= 3 and self.dp > 1:
+            if self._zero3(u) or u.transient_grad:
                 u.hook_handles.append(u.module.register_forward_hook(self._make_post_fwd(u)))
 
     def _make_pre_fwd(self, u: _Unit):
         def hook(mod, args):
-            if self.stage >= 3 and self.dp > 1:
+            recompute = _in_backward()
+            if self._zero3(u):
                 self._gather_unit(u)
                 nxt = self.units[u.idx + 1] if u.idx + 1 < len(self.units) else None
-                if nxt is not None and torch.is_grad_enabled():
+                if nxt is not None and not recompute and self._zero3(nxt):
                     self._gather_unit(nxt, async_=True)
             elif u.ag_event is not None:
                 torch.cuda.current_stream().wait_event(u.ag_event)
                 u.ag_event = None
-            if torch.is_grad_enabled() and (self.dp > 1 or self.pc.tp) and not self.autograd_grads:
+            if (torch.is_grad_enabled() and not recompute and (self.sharded or self.pc.tp)
+                    and not self.autograd_grads):
                 for a in args:
                     if isinstance(a, torch.Tensor) and a.requires_grad:
                         a.register_hook(self._make_grad_ready(u))
@@ -259,30 +346,39 @@ class DataParallelEngine:
 
     def _make_post_fwd(self, u: _Unit):
         def hook(mod, args, out):
-            if self.reshard_after_forward and not u.keep_gathered:
-                self._release_unit(u)
-            # re-gather before this unit's backward: hook the unit's output gradient
+            if _in_backward():
+                return None  # recompute inside backward: the unit's backward needs it right now
             if torch.is_grad_enabled():
+                # before this unit's backward: hook the unit's output gradient
                 outs = out if isinstance(out, (tuple, list)) else (out,)
                 for t in outs:
                     if isinstance(t, torch.Tensor) and t.requires_grad:
                         t.register_hook(self._make_pre_bwd(u))
                         break
+            if self._zero3(u) and not u.keep_gathered and (self.reshard_after_forward
+                                                          or not torch.is_grad_enabled()):
+                self._release_unit(u)
             return None
         return hook
 
     def _make_pre_bwd(self, u: _Unit):
         def hook(g):
-            self._gather_unit(u)
-            if u.idx > 0:
-                self._gather_unit(self.units[u.idx - 1], async_=True)
+            if self._zero3(u):
+                self._gather_unit(u)
+                prv = self.units[u.idx - 1] if u.idx > 0 else None
+                if prv is not None and self._zero3(prv):
+                    self._gather_unit(prv, async_=True)
+            if u.transient_grad:
+                self._alloc_grad(u)
             return g
         return hook
 
     def _make_grad_ready(self, u: _Unit):
         def hook(g):
-            if not u.reduced and self.micro == self.accum - 1:
+            if not u.reduced and (u.transient_grad or self.micro == self.accum - 1):
                 self._reduce_unit(u)
+            if self._zero3(u) and not u.keep_gathered:
+                self._release_unit(u)  # backward of this unit is done: drop the gathered params
             return g
         return hook
 
@@ -294,7 +390,6 @@ class DataParallelEngine:
                 u.ag_event = None
             return
         self._alloc_full(u)
-        sn = u.numel // self.dp
         if self.cuda and u.opt_event is not None:
             torch.cuda.current_stream().wait_event(u.opt_event)  # updated shard (async AdamW)
             u.opt_event = None
@@ -313,11 +408,15 @@ class DataParallelEngine:
         else:
             dist.all_gather_into_tensor(u.pflat, u.pshard, group=self.group)
         u.gathered = True
-        del sn
 
     def _release_unit(self, u: _Unit):
+        if not u.gathered:
+            return
         if self.cuda:
             u.pflat.record_stream(torch.cuda.current_stream())
+            if self.comm_stream is not None:
+                u.pflat.record_stream(self.comm_stream)
+        u.ag_event = None
         self._free_full(u)
 
     # ------------------------------------------------------------------ gradient reduction
@@ -327,13 +426,29 @@ class DataParallelEngine:
             # partial grads of sequence shards (TP) and of data shards (DP): sum over the whole world
             dist.all_reduce(u.gflat)
             return
-        if self.dp == 1:
+        if not self.sharded:
             return
-        src = u.gflat if u.gflat.dtype == self.reduce_dtype else u.gflat.to(self.reduce_dtype)
+        transient = u.transient_grad
+        if transient and not self._grad_allocated(u):
+            self._alloc_grad(u)
+            u.gflat.zero_()  # the unit received no gradient in this micro-batch
+        for p in u.params:
+            if not p.grad_added:  # a parameter without gradient contributes zeros
+                p.main_grad.zero_()
+                p.grad_added = True
+        accumulate = transient and u.gshard_valid
+        u.gshard_valid = True
+        stage = self.stage
 
         def op():
-            if self.stage >= 1:
-                dist.reduce_scatter_tensor(u.gshard, src, group=self.group)
+            src = u.gflat if u.gflat.dtype == self.reduce_dtype else u.gflat.to(self.reduce_dtype)
+            if stage >= 1:
+                if accumulate:
+                    tmp = torch.empty_like(u.gshard)
+                    dist.reduce_scatter_tensor(tmp, src, group=self.group)
+                    u.gshard.add_(tmp)
+                else:
+                    dist.reduce_scatter_tensor(u.gshard, src, group=self.group)
             else:
                 dist.all_reduce(src, group=self.group)
                 if src is not u.gflat:
@@ -345,11 +460,18 @@ class DataParallelEngine:
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
                 op()
-                done = torch.cuda.Event()
-                done.record(self.comm_stream)
-            u.rs_event = done
+            if transient:
+                self._free_grad(u, self.comm_stream)
         else:
             op()
+            if transient:
+                self._free_grad(u)
+
+    def _flush_transient(self):
+        """Reduce transient gradient buffers whose input-gradient hook did not fire this micro-batch."""
+        for u in self.units:
+            if u.transient_grad and not u.reduced and self._grad_allocated(u):
+                self._reduce_unit(u)
 
     # ------------------------------------------------------------------ public API used by the trainer
     def begin_step(self, accumulate_grad_batches: int = 1):
@@ -364,11 +486,17 @@ class DataParallelEngine:
                     u.ag_event = None
 
     def begin_micro(self, i: int):
+        if i > 0:
+            self._flush_transient()
         self.micro = i
+        for u in self.units:
+            if u.transient_grad:
+                u.reduced = False
 
     def zero_grad(self):
         for u in self.units:
             u.reduced = False
+            u.gshard_valid = False
             for p in u.params:
                 p.grad_added = False
                 p.grad = None
@@ -376,6 +504,10 @@ class DataParallelEngine:
     def finish_backward(self):
         """Called after the last micro-batch's backward: reduce units whose hook did not fire."""
         for u in self.units:
+            if u.transient_grad:
+                if not u.reduced and (self._grad_allocated(u) or not u.gshard_valid):
+                    self._reduce_unit(u)
+                continue
             if not u.reduced:
                 for p in u.params:
                     if p.grad is not None:  # autograd-produced gradient (non-fused modules)
@@ -393,13 +525,24 @@ class DataParallelEngine:
                 self._reduce_unit(u)
         if self.comm_stream is not None:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
-        for u in self.units:
-            u.rs_event = None
 
     def _grad_shard(self, u: _Unit) -> torch.Tensor:
-        if self._ustage(u) >= 1 and self._udp(u) > 1:
+        if self._ustage(u) >= 1 and self._usharded(u):
             return u.gshard
         return u.gflat
+
+    def grad_memory_bytes(self) -> dict[str, int]:
+        """Resident gradient memory of this rank: persistent buffers vs transient (currently allocated)."""
+        persistent = transient = 0
+        for u in self.units:
+            if u.gshard is not None:
+                persistent += u.gshard.numel() * u.gshard.element_size()
+            nb = u.gflat.untyped_storage().size()
+            if u.transient_grad:
+                transient += nb
+            else:
+                persistent += nb
+        return {"persistent": persistent, "transient": transient}
 
     def clip_and_scale(self, max_norm: float | None):
         """Global grad norm computed on device; returns the device scalar scale used by the optimizer."""
@@ -449,19 +592,19 @@ class DataParallelEngine:
             self.opt_stream.wait_event(start)
             self._step_units(lr)
 
+    def _param_out(self, u: _Unit) -> torch.Tensor:
+        """The bf16 parameter slice the optimizer writes for this rank (shard, or all)."""
+        if self._zero3(u):
+            return u.pshard
+        a, b = self.shard_range(u)
+        return u.pflat[a:b]
+
     def _step_units(self, lr: float):
         b1, b2 = self.betas
-        dp, r = self.dp, self.pc.dp_rank
         cur = torch.cuda.current_stream() if self.cuda else None
         for u in self.units:
             g = self._grad_shard(u)
-            st, udp = self._ustage(u), self._udp(u)
-            sn = u.numel // udp
-            rr = r if udp > 1 else 0
-            if st >= 1:
-                pout = u.pshard if (st >= 3 and udp > 1) else u.pflat[rr * sn:(rr + 1) * sn]
-            else:
-                pout = u.pflat
+            pout = self._param_out(u)
             if self.native:
                 lib().adamw_(u.master, u.exp_avg, u.exp_avg_sq, g, pout, lr, b1, b2, self.eps,
                              self.weight_decay, self.step_count, self._gscale)
@@ -474,26 +617,16 @@ class DataParallelEngine:
                 done = torch.cuda.Event()
                 done.record(cur)
             self._publish_update(u, cur, done)
-        if self.stage >= 3 and dp > 1:
-            for u in self.units:
-                if u.gathered and not u.replicated:
-                    self._release_unit(u)
+        for u in self.units:
+            if self._zero3(u) and u.gathered:
+                self._release_unit(u)
 
     def _step_units_offload(self, lr: float):
         """AdamW on the host for optimizer-offloaded shards (see the module docstring)."""
         b1, b2 = self.betas
-        dp, r = self.dp, self.pc.dp_rank
         scale = float(self._gscale.reshape(-1)[0].item())  # the one host sync of the step
-        outs, grads = [], []
-        for u in self.units:
-            st, udp = self._ustage(u), self._udp(u)
-            sn = u.numel // udp
-            rr = r if udp > 1 else 0
-            if st >= 1:
-                outs.append(u.pshard if (st >= 3 and udp > 1) else u.pflat[rr * sn:(rr + 1) * sn])
-            else:
-                outs.append(u.pflat)
-            grads.append(self._grad_shard(u))
+        outs = [self._param_out(u) for u in self.units]
+        grads = [self._grad_shard(u) for u in self.units]
         cur = torch.cuda.current_stream() if self.cuda else None
         down = []
         if self.cuda:
@@ -524,22 +657,19 @@ class DataParallelEngine:
             else:
                 pout.copy_(u.p_host if u.p_host is not None else u.master)
                 self._publish_update(u, None, None)
-        if self.stage >= 3 and dp > 1:
-            for u in self.units:
-                if u.gathered and not u.replicated:
-                    self._release_unit(u)
+        for u in self.units:
+            if self._zero3(u) and u.gathered:
+                self._release_unit(u)
 
     def _publish_update(self, u: _Unit, cur, done):
         """Make unit ``u``'s updated shard visible: all-gather (stage 1/2) and the per-unit event the
         next forward waits on. ``cur`` is the stream the update was issued on, ``done`` its event."""
-        dp, r = self.dp, self.pc.dp_rank
-        st, udp = self._ustage(u), self._udp(u)
-        sn = u.numel // udp
         # stage 1/2: refresh this unit's full bf16 parameters with an in-place all-gather of the
         # updated shards on the comm stream right away, so it overlaps the remaining units' AdamW
         # and the next forward (which waits per unit in its pre-forward hook)
-        if self.stage in (1, 2) and dp > 1 and not u.replicated:
-            shard = u.pflat[r * sn:(r + 1) * sn]
+        if self.stage in (1, 2) and self._usharded(u):
+            a, b = self.shard_range(u)
+            shard = u.pflat[a:b]
             if self.comm_stream is not None:
                 ev = torch.cuda.Event()
                 ev.record(cur)
@@ -555,7 +685,7 @@ class DataParallelEngine:
                 if done is not None:
                     done = torch.cuda.Event()
                     done.record(torch.cuda.current_stream())
-        if st >= 3 and udp > 1:
+        if self._zero3(u):
             u.opt_event = done
         else:
             u.ag_event = done
@@ -568,6 +698,8 @@ class DataParallelEngine:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
         if self.copy_stream is not None:
             torch.cuda.current_stream().wait_stream(self.copy_stream)
+            # host-side too: pinned host buffers of an in-flight upload must not be overwritten
+            self.copy_stream.synchronize()
         for u in self.units:
             u.ag_event = None
             u.opt_event = None
@@ -597,15 +729,14 @@ class DataParallelEngine:
         """Write bf16 params from the fp32 masters (after loading weights / optimizer state)."""
         self.wait_params()
         for u in self.units:
-            dp, st = self._udp(u), self._ustage(u)
-            r = self.pc.dp_rank if dp > 1 else 0
-            sn = u.numel // dp
-            if st >= 3 and dp > 1:
+            if self._zero3(u):
                 u.pshard.copy_(u.master)
-            elif st >= 1:
-                u.pflat[r * sn:(r + 1) * sn].copy_(u.master)
-                if dp > 1:
-                    dist.all_gather_into_tensor(u.pflat, u.pflat[r * sn:(r + 1) * sn].clone(), group=self.group)
+                if u.gathered:
+                    dist.all_gather_into_tensor(u.pflat, u.pshard, group=self.group)
+            elif self._ustage(u) >= 1 and self._usharded(u):
+                a, b = self.shard_range(u)
+                u.pflat[a:b].copy_(u.master)
+                dist.all_gather_into_tensor(u.pflat, u.pflat[a:b].clone(), group=self.group)
             else:
                 u.pflat.copy_(u.master)
 
@@ -614,15 +745,11 @@ class DataParallelEngine:
         """Re-derive fp32 masters from the (freshly loaded) bf16/fp32 params."""
         self.wait_params()
         for u in self.units:
-            dp, st = self._udp(u), self._ustage(u)
-            r = self.pc.dp_rank if dp > 1 else 0
-            sn = u.numel // dp
-            if st >= 3 and dp > 1:
+            if self._zero3(u):
                 u.master.copy_(u.pshard)
-            elif st >= 1:
-                u.master.copy_(u.pflat[r * sn:(r + 1) * sn])
             else:
-                u.master.copy_(u.pflat)
+                a, b = self.shard_range(u)
+                u.master.copy_(u.pflat[a:b])
 
     def full_params_context(self):
         """Context manager materialising full params (stage 3) e.g. for export/eval."""
@@ -631,17 +758,16 @@ class DataParallelEngine:
         class _Ctx:
             def __enter__(self_):
                 eng.wait_params()
-                if eng.stage >= 3 and eng.dp > 1:
-                    for u in eng.units:
-                        if not u.replicated:
-                            eng._gather_unit(u)
+                self_.gathered = []
+                for u in eng.units:
+                    if eng._zero3(u) and not u.gathered:
+                        eng._gather_unit(u)
+                        self_.gathered.append(u)
                 return eng.model
 
             def __exit__(self_, *a):
-                if eng.stage >= 3 and eng.dp > 1:
-                    for u in eng.units:
-                        if not u.replicated:
-                            eng._release_unit(u)
+                for u in self_.gathered:
+                    eng._release_unit(u)
                 return False
 
         return _Ctx()

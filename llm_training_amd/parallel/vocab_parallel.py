@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 from torch.autograd import Function
 
-from ..ops.fused import _wgrad_mm, mm_nn, mm_nt
+from ..ops.fused import _apply_weight_grad, _wgrad_mm, mm_nn, mm_nt
 from ..ops.native import lib, use_native
 
 
@@ -59,48 +59,59 @@ def _local_grad(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, native):
 
 
 class _VPFusedCE(Function):
+    """Vocab-parallel fused linear + CE, memory bounded by one local logits chunk: pass 1 computes the
+    local (lse, target logit) per chunk and drops the logits; after the TP combine, pass 2 recomputes
+    each chunk's logits, turns them into d loss / d logits in place and produces that chunk's dh rows
+    and dW contribution immediately (one extra GEMM instead of O(N * V/tp) saved logits)."""
+
     @staticmethod
     def forward(ctx, h, w, labels, v0, ignore_index, group, chunk):
         native = use_native(h)
         N = h.shape[0]
         inv_n = (1.0 / (labels != ignore_index).sum().clamp(min=1).float()).reshape(1)
-        lgs, lses, tgts = [], [], []
+        lses, tgts = [], []
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
-            lgs.append(lg)
             lses.append(lse)
             tgts.append(tgt)
+            del lg
         lse = _combine_lse(torch.cat(lses), group)
         tgt = torch.cat(tgts)
         dist.all_reduce(tgt, group=group)
         valid = labels != ignore_index
         loss = ((lse - tgt) * valid).sum() * inv_n[0]
-        for i, lg in enumerate(lgs):
-            s0 = i * chunk
-            s1 = s0 + lg.shape[0]
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dh = torch.empty_like(h) if need_h else None
+        dw = torch.empty(w.shape, device=w.device, dtype=w.dtype) if need_w else None
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = mm_nt(h[s0:s1], w)
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), None, inv_n, native)
-        ctx.save_for_backward(h, w, *lgs)
-        ctx.chunk = chunk
+            if need_h:
+                mm_nn(lg, w, out=dh[s0:s1])
+            if need_w:
+                if s0 == 0:
+                    torch.mm(lg.t(), h[s0:s1], out=dw)
+                else:
+                    dw.addmm_(lg.t(), h[s0:s1])
+            del lg
+        ctx.save_for_backward(*(t for t in (dh, dw) if t is not None))
+        ctx.has = (need_h, need_w)
+        ctx.w = w
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        h, w, *lgs = ctx.saved_tensors
-        chunk = ctx.chunk
-        dh = torch.empty_like(h)
-        hs = h * g.to(h.dtype)
-        dw = None
-        for i, lg in enumerate(lgs):
-            s0 = i * chunk
-            s1 = s0 + lg.shape[0]
-            mm_nn(lg, w, out=dh[s0:s1])
-            r = _wgrad_mm(w, lg.t(), hs[s0:s1])
-            if r is not None:
-                dw = r if dw is None else dw + r
-        dh.mul_(g.to(dh.dtype))
-        return dh, dw, None, None, None, None, None
+        saved = list(ctx.saved_tensors)
+        need_h, need_w = ctx.has
+        dh = saved.pop(0) if need_h else None
+        dw = saved.pop(0) if need_w else None
+        if dh is not None:
+            dh = dh * g.to(dh.dtype)
+        dwr = _apply_weight_grad(ctx.w, dw, g) if dw is not None else None
+        return dh, dwr, None, None, None, None, None
 
 
 class _VPLogps(Function):
@@ -119,13 +130,15 @@ class _VPLogps(Function):
         tgt = torch.cat(tgts)
         dist.all_reduce(tgt, group=group)
         valid = labels != ignore_index
-        ctx.save_for_backward(h, w, labels, lse)
+        ctx.save_for_backward(h, labels, lse)
+        ctx.w = w
         ctx.cfg = (v0, ignore_index, chunk)
         return (tgt - lse) * valid
 
     @staticmethod
     def backward(ctx, g):
-        h, w, labels, lse = ctx.saved_tensors
+        h, labels, lse = ctx.saved_tensors
+        w = ctx.w
         v0, ignore_index, chunk = ctx.cfg
         native = use_native(h)
         N = h.shape[0]

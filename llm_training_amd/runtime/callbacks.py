@@ -40,8 +40,9 @@ class LearningRateMonitor(Callback):
 class ModelCheckpoint(Callback):
     def __init__(self, dirpath: str | None = None, filename: str | None = None, every_n_train_steps: int | None = None,
                  save_on_train_epoch_end: bool | None = None, save_top_k: int = 1, save_last: bool | None = None,
-                 monitor: str | None = None, mode: str = "min", **kw):
+                 monitor: str | None = None, mode: str = "min", async_save: bool = False, **kw):
         self.dirpath = dirpath
+        self.async_save = async_save  # write the shard files on a background thread
         self.filename = filename or "epoch={epoch}-step={step}"
         self.every_n_train_steps = every_n_train_steps
         self.save_on_train_epoch_end = save_on_train_epoch_end
@@ -62,7 +63,7 @@ class ModelCheckpoint(Callback):
         path = os.path.join(self._dir(trainer), name)
         if path in self.saved:
             return
-        trainer.save_checkpoint(path)
+        trainer.save_checkpoint(path, async_write=self.async_save)
         self.saved.append(path)
         if self.save_top_k > 0 and self.monitor is None:
             while len(self.saved) > self.save_top_k:

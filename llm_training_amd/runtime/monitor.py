@@ -204,15 +204,8 @@ _STEP_RE = re.compile(r"step=(\d+)")
 
 
 def is_complete_checkpoint(path: str | os.PathLike) -> bool:
-    p = Path(path)
-    meta = p / "meta.json"
-    if not meta.is_file():
-        return False
-    try:
-        tp = int(json.loads(meta.read_text()).get("tp_size", 1))
-    except (ValueError, OSError):
-        return False
-    return all((p / f"tp{t}.safetensors").is_file() for t in range(tp))
+    from ..ckpt.checkpoint import is_complete
+    return is_complete(path)
 
 
 def checkpoint_step(path: str | os.PathLike) -> int:

@@ -254,6 +254,8 @@ class Trainer:
                 self.state.epoch += 1
                 self.state.batch_idx = 0
         self._flush_logs(force=True)
+        from ..ckpt.checkpoint import wait_for_pending_saves
+        wait_for_pending_saves()
         for cb in self.callbacks:
             _call(cb, "on_fit_end", self, lm)
         for lg in self.loggers:
@@ -406,9 +408,9 @@ class Trainer:
         return out
 
     # ------------------------------------------------------------------ checkpoint helpers for callbacks
-    def save_checkpoint(self, path: str):
+    def save_checkpoint(self, path: str, async_write: bool = False):
         from ..ckpt.checkpoint import save_checkpoint
-        save_checkpoint(self, path)
+        save_checkpoint(self, path, async_write=async_write)
 
 
 def _call(obj, name, *args):

@@ -16,22 +16,32 @@ def _batches(vocab, n, B=2, S=16, seed=0):
     return [torch.randint(0, vocab, (B, S), generator=g) for _ in range(n)]
 
 
-def _train(model, pc, stage, batches, lr=1e-2, offload=False):
+def _train(model, pc, stage, batches, lr=1e-2, offload=False, accum=1, probe=None):
+    """Each element of ``batches`` is one optimizer step, split into ``accum`` micro-batches."""
     from llm_training_amd.lms.clm import CLM
     from llm_training_amd.parallel.engine import DataParallelEngine
     eng = DataParallelEngine(model, pc, stage, lr=lr, weight_decay=0.0, offload_optimizer=offload)
     lm = CLM({"model": None})
     lm.model = model
+    lm.train()
     losses = []
     for ids in batches:
-        eng.begin_step(1)
+        eng.begin_step(accum)
         eng.zero_grad()
-        loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
-        loss.backward()
+        mb = ids.shape[0] // accum
+        tot = 0.0
+        for i in range(accum):
+            eng.begin_micro(i)
+            part = ids[i * mb:(i + 1) * mb]
+            loss, _, _ = lm.training_step({"input_ids": part, "labels": part})
+            loss.backward()
+            if probe is not None:
+                probe(eng)
+            tot += loss.item() / accum
         eng.finish_backward()
         eng.clip_and_scale(1.0)
         eng.step(lr)
-        losses.append(loss.item())
+        losses.append(tot)
     return eng, losses
 
 
@@ -52,7 +62,7 @@ def _single_reference(cfg_kw, global_batches, seed=1):
     return full0, _full_params(m, eng), losses
 
 
-def _dp_worker(rank, world, stage, cfg_kw, full0, global_batches, offload=False):
+def _dp_worker(rank, world, stage, cfg_kw, full0, global_batches, offload=False, accum=1, check_release=False):
     from llm_training_amd.models.llama import Llama
     from llm_training_amd.parallel.context import ParallelContext
     pc = ParallelContext.create("auto", 1, "cpu")
@@ -60,8 +70,18 @@ def _dp_worker(rank, world, stage, cfg_kw, full0, global_batches, offload=False)
     m.load_full_state_dict(full0)
     B = global_batches[0].shape[0] // world
     local = [b[rank * B:(rank + 1) * B] for b in global_batches]
-    eng, losses = _train(m, pc, stage, local, offload=offload)
-    return {"params": _full_params(m, eng), "losses": losses}
+    seen = {"gathered_after_bwd": [], "grad_bytes": []}
+
+    def probe(eng):
+        # after a backward: stage-3 decoder layers must be released again (the keep-gathered lm_head
+        # unit and the embedding — first in the next forward, no input gradient to hook — stay), and no
+        # transient gradient buffer may outlive its reduce-scatter
+        seen["gathered_after_bwd"].append([u.idx for u in eng.units
+                                           if u.gathered and not u.keep_gathered and u.idx > 0])
+        seen["grad_bytes"].append(eng.grad_memory_bytes())
+
+    eng, losses = _train(m, pc, stage, local, offload=offload, accum=accum, probe=probe if check_release else None)
+    return {"params": _full_params(m, eng), "losses": losses, **seen}
 
 
 @pytest.mark.parametrize("stage,offload", [(0, False), (1, False), (2, False), (3, False), (2, True), (3, True)])
@@ -89,6 +109,56 @@ def _tp_worker(rank, world, tp, cfg_kw, full0, global_batches):
     local = [b[pc.dp_rank * B:(pc.dp_rank + 1) * B] for b in global_batches]
     eng, losses = _train(m, pc, 2, local)
     return {"params": _full_params(m, eng), "losses": losses}
+
+
+@pytest.mark.parametrize("stage,accum", [(2, 2), (3, 1), (3, 2)])
+def test_zero_with_activation_checkpointing_and_accumulation(stage, accum):
+    """Full activation checkpointing recomputes each layer inside backward: at stage 3 the recompute must
+    neither prefetch forward nor release the layer it recomputes, every layer is released once its
+    backward is done, and stage >= 2 gradient buffers exist only transiently (reduce-scattered per
+    micro-batch into the 1/dp shard)."""
+    cfg_kw = dict(enable_gradient_checkpointing=True, num_hidden_layers=3)
+    gb = _batches(128, STEPS, B=4 * accum)
+    full0, ref, ref_losses = _single_reference(cfg_kw, gb)
+    out = run_gloo(_dp_worker, 2, (stage, cfg_kw, full0, gb, False, accum, True))
+    tol = 2e-5 if accum == 1 else 3e-4  # accumulation reorders the fp32 sums (Adam amplifies tiny grads)
+    for r in (0, 1):
+        for k, v in ref.items():
+            assert torch.allclose(out[r]["params"][k], v, atol=tol, rtol=1e-4), (stage, accum, r, k)
+        if stage == 3:
+            assert all(not g for g in out[r]["gathered_after_bwd"]), out[r]["gathered_after_bwd"]
+        assert all(b["transient"] == 0 for b in out[r]["grad_bytes"]), out[r]["grad_bytes"]
+    avg = [(a + b) / 2 for a, b in zip(out[0]["losses"], out[1]["losses"])]
+    for a, b in zip(avg, ref_losses):
+        assert abs(a - b) < 1e-5
+
+
+def _gradmem_worker(rank, world, stage):
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+    pc = ParallelContext.create("auto", 1, "cpu")
+    m = Llama(tiny_llama_cfg(num_hidden_layers=4, hidden_size=128, intermediate_size=256), pc, dtype=torch.float32)
+    m.init_weights(0)
+    eng = DataParallelEngine(m, pc, stage)
+    layer_elems = sum(u.numel for u in eng.units if u.transient_grad)
+    other = sum(u.numel for u in eng.units if not u.transient_grad)
+    return {"mem": eng.grad_memory_bytes(), "layer_elems": layer_elems, "other": other,
+            "n_transient": sum(u.transient_grad for u in eng.units)}
+
+
+def test_stage2_gradient_memory_is_sharded():
+    """ZeRO-2: resident gradient bytes of the decoder layers are 1/dp of their size (the full-size
+    buffers exist only during each layer's backward); stage 1 keeps full gradient buffers."""
+    out2 = run_gloo(_gradmem_worker, 4, (2,))
+    out1 = run_gloo(_gradmem_worker, 4, (1,))
+    o2, o1 = out2[0], out1[0]
+    assert o2["n_transient"] == 4 and o1["n_transient"] == 0
+    el = 4  # fp32 grads
+    expect2 = (o2["layer_elems"] // 4 + o2["other"] + o2["other"] // 4) * el  # layer shards + full/shard others
+    assert o2["mem"]["persistent"] == expect2, (o2, expect2)
+    assert o2["mem"]["transient"] == 0
+    assert o1["mem"]["persistent"] > 3 * o2["mem"]["persistent"] - 4 * o2["other"] * el
 
 
 @pytest.mark.parametrize("world,tp", [(2, 2), (4, 2)])
@@ -137,7 +207,7 @@ def test_vocab_parallel_losses():
     assert torch.allclose(torch.cat([out[0]["dw"], out[1]["dw"]]), wr.grad, atol=1e-5)
 
 
-def _ckpt_worker(rank, world, tp, stage, path, mode):
+def _ckpt_worker(rank, world, tp, stage, path, mode, offload=False):
     from llm_training_amd.data.dummy import DummyDataModule
     from llm_training_amd.lms.clm import CLM
     from llm_training_amd.runtime.strategies import FSDP2Strategy
@@ -148,8 +218,8 @@ def _ckpt_worker(rank, world, tp, stage, path, mode):
                                          "num_key_value_heads": 2}},
               "optim": {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 1e-2}}})
     dm = DummyDataModule({"batch_size": 2, "vocab_size": 96, "max_length": 16, "num_samples": 64, "base_seed": 5})
-    t = Trainer(strategy=FSDP2Strategy(tensor_parallel_size=tp, zero_stage=stage), precision="32-true",
-                max_steps=2, seed=3, default_root_dir=path)
+    t = Trainer(strategy=FSDP2Strategy(tensor_parallel_size=tp, zero_stage=stage, offload_policy=offload),
+                precision="32-true", max_steps=2, seed=3, default_root_dir=path)
     if mode == "save":
         t.fit(lm, dm)
         t.save_checkpoint(os.path.join(path, "ck"))
@@ -157,7 +227,10 @@ def _ckpt_worker(rank, world, tp, stage, path, mode):
         t.setup(lm, dm, os.path.join(path, "ck"))
     with t.engine.full_params_context():
         sd = lm.model.gather_full_state_dict()
-    return {"sd": sd, "step": t.global_step}
+    files = sorted(os.listdir(os.path.join(path, "ck")))
+    return {"sd": sd, "step": t.global_step, "files": files,
+            "state": {k: (u.master.clone(), u.exp_avg.clone()) for k, u in enumerate(t.engine.units)},
+            "used": {k: u.offsets[-1] + u.params[-1].numel() for k, u in enumerate(t.engine.units)}}
 
 
 def test_checkpoint_reshards_across_layouts(tmp_path):
@@ -166,3 +239,28 @@ def test_checkpoint_reshards_across_layouts(tmp_path):
     for k, v in saved[0]["sd"].items():
         assert torch.allclose(loaded[0]["sd"][k], v), k
     assert loaded[1]["step"] == 2
+    # one shard file per rank, no full gather anywhere
+    assert {f for f in saved[0]["files"] if f.endswith(".safetensors")} == {
+        f"shard-tp{t}-dp{d}.safetensors" for t in range(2) for d in range(2)}
+
+
+def test_checkpoint_dp4_zero3_to_dp2_zero2_and_offload(tmp_path):
+    """dp4 x ZeRO-3 -> dp2 x ZeRO-2 (each rank reads only its overlapping ranges); then a dp2 ZeRO-2
+    run with optimizer offload (host-resident shards) saves and a dp2 ZeRO-3 run resumes it."""
+    saved = run_gloo(_ckpt_worker, 4, (1, 3, str(tmp_path / "a"), "save"))
+    loaded = run_gloo(_ckpt_worker, 2, (1, 2, str(tmp_path / "a"), "load"))
+    for k, v in saved[0]["sd"].items():
+        assert torch.allclose(loaded[0]["sd"][k], v), k
+    # optimizer state: the dp2 shards concatenate to the dp4 shards (up to the layout's tail padding)
+    for u in saved[0]["state"]:
+        n = saved[0]["used"][u]
+        for i in (0, 1):
+            new = torch.cat([loaded[r]["state"][u][i] for r in (0, 1)])[:n]
+            old = torch.cat([saved[r]["state"][u][i] for r in range(4)])[:n]
+            assert torch.equal(new, old), (u, i)
+    so = run_gloo(_ckpt_worker, 2, (1, 2, str(tmp_path / "b"), "save", True))
+    lo = run_gloo(_ckpt_worker, 2, (1, 3, str(tmp_path / "b"), "load"))
+    for k, v in so[0]["sd"].items():
+        assert torch.allclose(lo[0]["sd"][k], v), k
+    for u in so[0]["state"]:
+        assert torch.equal(lo[1]["state"][u][1], so[1]["state"][u][1])

@@ -148,67 +148,38 @@ def test_deterministic_mode_is_bitwise_reproducible(monkeypatch):
     assert not bad, bad
 
 
-def test_optimizer_offload_matches_device_adamw():
+def test_optimizer_offload_matches_device_adamw(monkeypatch):
     """Optimizer offload (pinned host master/m/v, native C++ AdamW, per-unit D2H/H2D on a copy stream)
-    trains like the fused device AdamW: same losses, parameters within run-to-run noise."""
+    trains like the fused device AdamW. Deterministic kernels make everything but the two AdamW
+    implementations identical, so the remaining difference is fp32 rounding of the update (a flipped
+    bf16 rounding here and there), far below one learning-rate step (~5e-2 relative)."""
+    monkeypatch.setenv("LLMT_DETERMINISTIC", "1")
     dev = torch.device("cuda", 0)
     cfg = _cfg(num_hidden_layers=2)
     _, la, pa = _train_engine(cfg, dev, overlap_step=False)
-    _, lb, pb = _train_engine(cfg, dev, overlap_step=False)
     eng, lo, po = _train_engine(cfg, dev, offload_optimizer=True)
     assert eng.units[0].master.device.type == "cpu" and eng.units[0].master.is_pinned()
     for a, b in zip(la, lo):
-        assert abs(a - b) < 1e-3 * abs(a), (la, lo)
-    num_n = num_o = den = 0.0
+        assert abs(a - b) < 2e-4 * abs(a), (la, lo)
+    num = den = 0.0
     for k in pa:
-        num_n += (pb[k] - pa[k]).norm().item() ** 2
-        num_o += (po[k] - pa[k]).norm().item() ** 2
+        num += (po[k] - pa[k]).norm().item() ** 2
         den += pa[k].norm().item() ** 2
-    noise, rel = (num_n / den) ** 0.5, (num_o / den) ** 0.5
-    assert rel <= 3 * noise + 5e-3, (rel, noise)  # see test_async_optimizer_stream_matches_synchronous
+    assert (num / den) ** 0.5 < 1e-3, (num / den) ** 0.5
 
 
-def test_async_optimizer_stream_matches_synchronous():
-    """AdamW on its own stream (overlapping the next forward) must train exactly like the synchronous
-    update up to the run-to-run noise of atomics (embedding backward): a read-before-update race would
-    show up as a full learning-rate step of difference."""
+def test_async_optimizer_stream_matches_synchronous(monkeypatch):
+    """AdamW on its own stream (overlapping the next forward, per-unit events) must train exactly like
+    the synchronous update: with deterministic kernels the two runs are bitwise identical, so even a
+    partial read-before-update race (some elements / units stale) fails the test."""
+    monkeypatch.setenv("LLMT_DETERMINISTIC", "1")
     dev = torch.device("cuda", 0)
     cfg = _cfg(num_hidden_layers=2)
-    outs = []
-    for overlap in (False, False, True):
-        torch.manual_seed(0)
-        m = Llama(cfg, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
-        m.init_weights(5)
-        eng = DataParallelEngine(m, ParallelContext.single(dev), 0, lr=1e-3, overlap_step=overlap)
-        lm = CLM({"model": None})
-        lm.model = m
-        g = torch.Generator(device=dev).manual_seed(11)
-        losses = []
-        for _ in range(4):
-            ids = torch.randint(0, cfg.vocab_size, (1, 512), device=dev, generator=g)
-            eng.begin_step(1)
-            eng.zero_grad()
-            loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
-            loss.backward()
-            eng.finish_backward()
-            eng.clip_and_scale(1.0)
-            eng.step(1e-3)
-            losses.append(loss.item())
-        eng.wait_params()
-        outs.append((losses, {k: v.float().cpu() for k, v in m.state_dict().items()}))
-    for a, b in zip(outs[0][0], outs[2][0]):
-        assert abs(a - b) < 5e-4 * abs(a), (outs[0][0], outs[2][0])
-    num_a = num_n = den = 0.0
-    for k in outs[0][1]:
-        ref, again, asy = outs[0][1][k], outs[1][1][k], outs[2][1][k]
-        num_n += (again - ref).norm().item() ** 2  # sync vs sync: atomics (embedding backward) + Adam
-        num_a += (asy - ref).norm().item() ** 2
-        den += ref.norm().item() ** 2
-    noise, rel = (num_n / den) ** 0.5, (num_a / den) ** 0.5
-    # run-to-run noise (embedding-backward atomics, amplified by Adam's normalisation of near-zero grads)
-    # reaches ~3e-3 on some runs and 0 on others (scripts/async_race_probe.py); one missed update would
-    # be a full Adam step on every element (~5e-2 relative), so 5e-3 still separates the two
-    assert rel <= 3 * noise + 5e-3, (rel, noise)
+    _, ls, ps = _train_engine(cfg, dev, steps=5, overlap_step=False)
+    _, la, pa = _train_engine(cfg, dev, steps=5, overlap_step=True)
+    assert ls == la, (ls, la)
+    bad = [k for k in ps if not torch.equal(ps[k], pa[k])]
+    assert not bad, bad
 
 
 def test_dpo_orpo_hip_match_cpu_reference():

@@ -62,12 +62,13 @@ def test_stall_watchdog_dumps_stack(tmp_path):
     assert not StallWatchdog(timeout=0).enabled
 
 
-def _fake_ckpt(root, name, step, tp=1, complete=True):
+def _fake_ckpt(root, name, step, tp=1, complete=True, dp=2):
     d = root / name
     d.mkdir(parents=True)
-    (d / "meta.json").write_text(json.dumps({"tp_size": tp, "trainer": {"global_step": step}}))
-    for t in range(tp if complete else tp - 1):
-        (d / f"tp{t}.safetensors").write_bytes(b"x")
+    (d / "meta.json").write_text(json.dumps({"tp_size": tp, "dp_size": dp, "trainer": {"global_step": step}}))
+    ranks = [(t, r) for t in range(tp) for r in range(dp)]
+    for t, r in ranks[:len(ranks) if complete else -1]:  # an incomplete save lacks one rank's marker
+        (d / f"shard-tp{t}-dp{r}.done").write_bytes(b"")
     return d
 
 

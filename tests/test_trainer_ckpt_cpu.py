@@ -49,11 +49,12 @@ def test_resume_is_exact(tmp_path, strategy):
     log1 = tmp_path / "a"
     t1 = Trainer(strategy=strategy, precision="32-true", logger=JSONLLogger(str(log1), "r"), max_steps=6,
                  log_every_n_steps=1, accumulate_grad_batches=2, gradient_clip_val=1.0, seed=11,
-                 callbacks=[ModelCheckpoint(dirpath=str(tmp_path / "ck"), every_n_train_steps=3, save_top_k=-1)])
+                 callbacks=[ModelCheckpoint(dirpath=str(tmp_path / "ck"), every_n_train_steps=3, save_top_k=-1,
+                                            async_save=True)])
     t1.fit(_lm(), _dm())
     full = _losses(log1 / "r")
     ck = tmp_path / "ck" / "epoch=0-step=3.ckpt"
-    assert (ck / "meta.json").exists() and (ck / "tp0.safetensors").exists()
+    assert (ck / "meta.json").exists() and (ck / "shard-tp0-dp0.safetensors").exists()
     log2 = tmp_path / "b"
     t2 = Trainer(strategy=strategy, precision="32-true", logger=JSONLLogger(str(log2), "r"), max_steps=6,
                  log_every_n_steps=1, accumulate_grad_batches=2, gradient_clip_val=1.0, seed=11)
@@ -92,3 +93,26 @@ def test_training_time_estimator_stops(tmp_path):
                 default_root_dir=str(tmp_path))
     t.fit(_lm(), _dm())
     assert t.global_step == 4 and est.result is not None and est.result["steps_per_sec"] > 0
+
+
+def test_dpo_resume_rebuilds_reference_from_pretrained(tmp_path):
+    """Resuming a DPO run must not copy the (trained) policy into the frozen reference model: the
+    reference is rebuilt from the pre-trained weights, exactly as in the original run."""
+    from safetensors.torch import save_file
+
+    from llm_training_amd.lms.preference import DPO
+    from llm_training_amd.parallel.context import ParallelContext
+    mcfg = {"vocab_size": 96, "hidden_size": 32, "intermediate_size": 64, "num_hidden_layers": 2,
+            "num_attention_heads": 4, "num_key_value_heads": 2}
+    src = DPO({"model": {"model_class": "llm_training.models.Llama", "model_config": mcfg}})
+    src.configure_model(ParallelContext.single(), torch.device("cpu"), torch.float32, seed=11)
+    path = str(tmp_path / "pre.safetensors")
+    save_file({k: v.contiguous() for k, v in src.model.state_dict().items()}, path)
+    refs = []
+    for resuming in (False, True):
+        lm = DPO({"model": {"model_class": "llm_training.models.Llama", "model_config": mcfg},
+                  "pre_trained_weights": path})
+        lm.configure_model(ParallelContext.single(), torch.device("cpu"), torch.float32, seed=3, resuming=resuming)
+        refs.append({k: v.clone() for k, v in lm.ref_model.state_dict().items()})
+    for k, v in src.model.state_dict().items():
+        assert torch.equal(refs[0][k], v) and torch.equal(refs[1][k], v), k
