@@ -33,7 +33,7 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
                                int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss, int64_t q_sh,
                                int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh,
                                int64_t o_sb, int64_t o_ss, int64_t o_sh, float scale, int causal, int window,
-                               hipStream_t stream);
+                               int seg_runs, hipStream_t stream);
 hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N, int K,
                      int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream);
 int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D);
@@ -43,7 +43,7 @@ hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
                                int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss,
                                int64_t v_sh, int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss,
                                int64_t dq_sh, int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb,
-                               int64_t dv_ss, int64_t dv_sh, float scale, int causal, int window,
+                               int64_t dv_ss, int64_t dv_sh, float scale, int causal, int window, int seg_runs,
                                hipStream_t stream);
 }
 
@@ -292,7 +292,19 @@ void gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool a_mn, bo
 
 // ---------------------------------------------------------------- flash attention
 // q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (any batch/seq/head strides, unit stride on D).
-// seg: optional int32 [B, S] segment ids (0 = padding): attention is restricted to equal ids.
+// seg: optional int32 segment ids (0 = padding): attention is restricted to the token's contiguous run of
+// equal ids. [B, S] = ids only (every tile compares ids); [3, B, S] = ids, run start, run end per token
+// (ops/fused.py segment_info): key tiles outside a query block's runs are skipped and tiles inside one
+// run take the unmasked path.
+static int seg_layout(const c10::optional<at::Tensor>& seg, int64_t B, int64_t S, const int** sp) {
+  *sp = nullptr;
+  if (!seg.has_value() || !seg->defined()) return 0;
+  TORCH_CHECK(seg->scalar_type() == at::kInt && seg->is_contiguous() && seg->is_cuda(), "flash_attn: seg must be "
+              "contiguous int32 on the GPU");
+  TORCH_CHECK(seg->numel() == B * S || seg->numel() == 3 * B * S, "flash_attn: seg must be [B, S] or [3, B, S]");
+  *sp = seg->data_ptr<int>();
+  return seg->numel() == 3 * B * S ? 1 : 0;
+}
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                                   const c10::optional<at::Tensor>& seg, double scale, bool causal,
                                                   int64_t window) {
@@ -311,14 +323,11 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
                                         : at::empty({S, B, Hq, D}, q.options()).transpose(0, 1);
   auto lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   const int* sp = nullptr;
-  if (seg.has_value() && seg->defined()) {
-    TORCH_CHECK(seg->scalar_type() == at::kInt && seg->is_contiguous() && seg->numel() == B * S, "flash_attn: seg");
-    sp = seg->data_ptr<int>();
-  }
+  const int runs = seg_layout(seg, B, S, &sp);
   check(llmt_flash_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), sp, (int)B,
                             (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                             k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1),
-                            o.stride(2), (float)scale, causal ? 1 : 0, (int)window, cur_stream()),
+                            o.stride(2), (float)scale, causal ? 1 : 0, (int)window, runs, cur_stream()),
         "flash_attn_fwd");
   return {o, lse};
 }
@@ -336,7 +345,7 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
               "flash_attn_bwd: unit stride on head dim");
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == B * Hq * S, "flash_attn_bwd: lse");
   const int* sp = nullptr;
-  if (seg.has_value() && seg->defined()) sp = seg->data_ptr<int>();
+  const int runs = seg_layout(seg, B, S, &sp);
   auto delta = at::empty({llmt_flash_attn_bwd_ws((int)B, (int)S, (int)Hq, (int)D)}, q.options().dtype(at::kFloat));
   TORCH_CHECK(dout.strides() == o.strides(), "flash_attn_bwd: dout must share O's layout");
   at::Tensor work;  // fp32 per-q-head dK/dV partials, only needed for GQA
@@ -347,7 +356,8 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
                             q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0),
                             v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
                             dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0),
-                            dv.stride(1), dv.stride(2), (float)scale, causal ? 1 : 0, (int)window, cur_stream()),
+                            dv.stride(1), dv.stride(2), (float)scale, causal ? 1 : 0, (int)window, runs,
+                            cur_stream()),
         "flash_attn_bwd");
 }
 

@@ -24,6 +24,13 @@
 //  * K/V (or Q/dO) tiles are register-staged: the next tile's global loads are issued before the
 //    current tile's MFMAs and written to LDS after the barrier (async-stage split).
 //  * query blocks are scheduled heaviest-first (reverse order) so the causal triangle load-balances.
+//  * packed sequences (varlen): segments are contiguous runs of equal ids. With the run
+//    boundaries of every token (rs = first, re = last index of its run; `seg` then points at a
+//    [3][B][S] int32 block: ids, rs, re) a query block only visits key tiles from the run start of its
+//    first query (and, non-causal, up to the run end of its last query) — the reference's
+//    flash_attn_varlen_func cost, attention_op.py:606-619 — and a tile lying inside the block's single
+//    run takes the unmasked fast path; only tiles that straddle a run boundary pay for the
+//    per-element segment compare. The same bounds drive the key-parallel dK/dV passes.
 #include "common.h"
 
 #include <cstdlib>
@@ -160,6 +167,8 @@ struct AttnArgs {
   float* lse;
   const float* delta;
   const int* seg;
+  const int* rs;  // run start / end of each token (packed segments), or null
+  const int* re;
   bf16* dk;
   bf16* dv;
   float* dk_part;
@@ -173,6 +182,28 @@ struct AttnArgs {
 };
 
 constexpr float kThr = 6.0f;  // defer-max threshold (log2 units): P <= 2^6 before a forced rescale
+
+// The contiguous segment run of a block's first token [lo] and whether the whole block [lo, hi] lies in
+// it (uni). Without run information (no segments, or ids only) rs = 0, re = S - 1, uni = !seg: every
+// tile then keeps the per-element compare whenever segment ids are present.
+struct RunInfo {
+  int rs, re;
+  bool uni;
+};
+__device__ __forceinline__ RunInfo block_run(const AttnArgs& a, int b, int lo, int hi) {
+  RunInfo ri{0, a.S - 1, a.seg == nullptr};
+  if (a.rs) {
+    const int64_t base = (int64_t)b * a.S;
+    ri.rs = a.rs[base + lo];
+    ri.re = a.re[base + lo];
+    ri.uni = ri.re >= hi;
+  }
+  return ri;
+}
+// does the segment compare matter for the tile [t0, t1] against a block described by ri?
+__device__ __forceinline__ bool seg_mask(const AttnArgs& a, const RunInfo& ri, int t0, int t1) {
+  return a.seg && !(ri.uni && t0 >= ri.rs && t1 <= ri.re);
+}
 
 // ============================================================================ forward
 // grid: (ceil(S/128), Hq, B), block 256 = 4 waves x 32 queries; KV tiles of 64 keys, double-buffered LDS
@@ -210,9 +241,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
     for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
 
-  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = kv_beg / BN * BN;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
 
   bfv8 kst[NV], vst[NV];
   int sst = 0;
@@ -261,8 +294,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
     const bool m_causal = a.causal && (n0 + BN - 1 > qw);
     const bool m_window = a.window >= 0 && (n0 < qw + 31 - a.window);
     const bool m_end = n0 + BN > S;
+    const bool m_seg = seg_mask(a, qr, n0, n0 + BN - 1);
     float smax = -INFINITY;
-    if (m_causal || m_window || m_end || seg) {
+    if (m_causal || m_window || m_end || m_seg || qrow >= S) {
       const int lim = qrow - n0 - 4 * hh;         // causal: key offset <= lim
       const int lo = qrow - a.window - n0 - 4 * hh;  // window: key offset >= lo
       const int hi = S - 1 - n0 - 4 * hh;            // bounds
@@ -271,14 +305,14 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           int4 sk = make_int4(sq, sq, sq, sq);
-          if (seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * t + 8 * c + 4 * hh);
+          if (m_seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * t + 8 * c + 4 * hh);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int i = 4 * c + j, ko = 32 * t + 8 * c + j;
             bool ok = (ko <= hi) && (qrow < S);
             if (a.causal) ok = ok && (ko <= lim);
             if (a.window >= 0) ok = ok && (ko >= lo);
-            if (seg) ok = ok && ((&sk.x)[j] == sq);
+            if (m_seg) ok = ok && ((&sk.x)[j] == sq);
             const float s = ok ? st[t][i] * sl2 : -INFINITY;
             st[t][i] = s;
             smax = fmaxf(smax, s);
@@ -414,9 +448,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqt[dt][i] = 0.f;
 
-  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = kv_beg / BN * BN;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
 
   bfv8 kst[NV], vst[NV];
   int sst = 0;
@@ -450,7 +486,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
     const char* Ks = smem + cur * BUF;
     const char* Vs = Ks + KB;
     const int* Ss = reinterpret_cast<const int*>(Vs + BN * G::KP);
-    const bool need_mask = seg || (n0 + BN > S) || (a.causal && n0 + BN - 1 > qw) ||
+    const bool m_seg = seg_mask(a, qr, n0, n0 + BN - 1);
+    const bool need_mask = m_seg || (n0 + BN > S) || (a.causal && n0 + BN - 1 > qw) ||
                            (a.window >= 0 && n0 < qw + 31 - a.window) || qw + 31 >= S;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -472,14 +509,14 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           int4 sk = make_int4(sq, sq, sq, sq);
-          if (seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * t + 8 * c + 4 * hh);
+          if (m_seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * t + 8 * c + 4 * hh);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int i = 4 * c + j, ko = 8 * c + j;
             bool ok = (ko <= hi) && (qrow < S);
             if (a.causal) ok = ok && (ko <= lim);
             if (a.window >= 0) ok = ok && (ko >= lo);
-            if (seg) ok = ok && ((&sk.x)[j] == sq);
+            if (m_seg) ok = ok && ((&sk.x)[j] == sq);
             const float p = ok ? fexp2(st[i] * sl2 - lse2) : 0.f;
             st[i] = p * (dpt[i] - dlt);
           }
@@ -556,9 +593,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
       dvt[dt][i] = 0.f;
     }
 
+  const RunInfo kr_run = block_run(a, b, min(ks, S - 1), min(ks + 127, S - 1));
   int q_beg = a.causal ? ks : 0;
+  if (!a.causal) q_beg = max(q_beg, kr_run.rs);
   q_beg = q_beg / BM * BM;
-  const int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+  int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+  if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
 
   bfv8 qst[NV], dst_[NV];
   float lst = 0.f, dls = 0.f;
@@ -620,7 +660,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
       sacc = mfma32(QI::row_read(Qs, r, 2 * kk + hh), kf[kk], sacc);
       dpacc = mfma32(QI::row_read(Ds, r, 2 * kk + hh), vf[kk], dpacc);
     }
-    const bool need_mask = seg || (q0 + BM > S) || (kw + 31 >= S) || (a.causal && kw + 31 > q0) ||
+    const bool m_seg = seg_mask(a, kr_run, q0, q0 + BM - 1);
+    const bool need_mask = m_seg || (q0 + BM > S) || (kw + 31 >= S) || (a.causal && kw + 31 > q0) ||
                            (a.window >= 0 && q0 + BM - 1 > kw + a.window);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -636,7 +677,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
           bool ok = kr < S && qi < S;
           if (a.causal) ok = ok && (kr <= qi);
           if (a.window >= 0) ok = ok && (kr >= qi - a.window);
-          if (seg) ok = ok && (Sg[qloc] == sk);
+          if (m_seg) ok = ok && (Sg[qloc] == sk);
           p = ok ? p : 0.f;
         }
         sacc[i] = p;                                 // P
@@ -859,8 +900,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
       dvt[dt][i] = 0.f;
     }
 
-  const int q_beg = a.causal ? ks : 0;  // multiple of 32
-  const int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+  const RunInfo kr_run = block_run(a, b, min(ks, S - 1), min(ks + 127, S - 1));
+  const int q_beg = a.causal ? ks : max(0, kr_run.rs) / 32 * 32;  // multiple of 32
+  int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+  if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
   const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
   const int T = nq * grp;
 
@@ -930,20 +973,21 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
         di[4 * c] = d4.x; di[4 * c + 1] = d4.y; di[4 * c + 2] = d4.z; di[4 * c + 3] = d4.w;
       }
       const int q0 = tile_q0(t);
-      const bool need = a.seg || (a.causal && kw + 31 > q0) || (a.window >= 0 && q0 + 31 - a.window > kw);
+      const bool m_seg = seg_mask(a, kr_run, q0, q0 + 31);
+      const bool need = m_seg || (a.causal && kw + 31 > q0) || (a.window >= 0 && q0 + 31 - a.window > kw);
       if (need) {
         const int* Sg = reinterpret_cast<const int*>(Ls + 64);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           int4 s4 = make_int4(sk, sk, sk, sk);
-          if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+          if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int qi = q0 + 8 * c + 4 * hh + j;
             bool ok = true;
             if (a.causal) ok = ok && (kr <= qi);
             if (a.window >= 0) ok = ok && (qi - kr <= a.window);
-            if (a.seg) ok = ok && ((&s4.x)[j] == sk);
+            if (m_seg) ok = ok && ((&s4.x)[j] == sk);
             si[4 * c + j] = ok ? si[4 * c + j] : -INFINITY;
           }
         }
@@ -1136,9 +1180,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const 
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqt[dt][i] = 0.f;
 
-  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = kv_beg / BN * BN;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
   const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
 
   if (T > 0) {
@@ -1199,23 +1245,25 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const 
     }
     auto need_mask = [&](int hs) {
       const int k0 = hkey0(hs);
-      return a.seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) || (a.window >= 0 && k0 < qw + 31 - a.window);
+      return seg_mask(a, qr, k0, k0 + 31) || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
+             (a.window >= 0 && k0 < qw + 31 - a.window);
     };
     auto masked_init = [&](int hs) {
       const int k0 = hkey0(hs);
+      const bool m_seg = seg_mask(a, qr, k0, k0 + 31);
       f32v16 si;
       const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         int4 s4 = make_int4(sq, sq, sq, sq);
-        if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+        if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int kx = k0 + 8 * c + 4 * hh + j;
           bool ok = kx < S;
           if (a.causal) ok = ok && (kx <= qrow);
           if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
-          if (a.seg) ok = ok && ((&s4.x)[j] == sq);
+          if (m_seg) ok = ok && ((&s4.x)[j] == sq);
           si[4 * c + j] = ok ? lsn : -INFINITY;
         }
       }
@@ -1343,9 +1391,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
     for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
 
-  const int kv_end = a.causal ? min(S, qs + 128) : S;
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = kv_beg / BN * BN;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
   const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
 
   if (T > 0) {
@@ -1394,21 +1444,22 @@ __global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
       const int k0 = hkey0(hs);
 #pragma unroll
       for (int i = 0; i < 16; ++i) si[i] = 0.f;
-      const bool need = a.seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
-                        (a.window >= 0 && k0 < qw + 31 - a.window);
+      const bool m_seg = seg_mask(a, qr, k0, k0 + 31);
+      const bool need = m_seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
+                        (a.window >= 0 && k0 < qw + 31 - a.window) || qw + 31 >= S;
       if (need) {
         const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           int4 s4 = make_int4(sq, sq, sq, sq);
-          if (a.seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+          if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int kx = k0 + 8 * c + 4 * hh + j;
             bool ok = kx < S && qrow < S;
             if (a.causal) ok = ok && (kx <= qrow);
             if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
-            if (a.seg) ok = ok && ((&s4.x)[j] == sq);
+            if (m_seg) ok = ok && ((&s4.x)[j] == sq);
             si[4 * c + j] = ok ? 0.f : -INFINITY;
           }
         }
@@ -1534,7 +1585,8 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
                                           const int* seg, int B, int S, int Hq, int Hkv, int D, int64_t q_sb,
                                           int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh,
                                           int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
-                                          int64_t o_sh, float scale, int causal, int window, hipStream_t stream) {
+                                          int64_t o_sh, float scale, int causal, int window, int seg_runs,
+                                          hipStream_t stream) {
   if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
   if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
       !aligned16(o, o_sb, o_ss, o_sh))
@@ -1544,6 +1596,10 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   if (!strides32({q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh})) return hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.out = (bf16*)o; a.lse = lse; a.seg = seg;
+  if (seg && seg_runs) {
+    a.rs = seg + (int64_t)B * S;
+    a.re = seg + 2 * (int64_t)B * S;
+  }
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv;
   a.q_sb = q_sb; a.q_ss = q_ss; a.q_sh = q_sh; a.k_sb = k_sb; a.k_ss = k_ss; a.k_sh = k_sh;
   a.v_sb = v_sb; a.v_ss = v_ss; a.v_sh = v_sh; a.o_sb = o_sb; a.o_ss = o_ss; a.o_sh = o_sh;
@@ -1580,7 +1636,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
                                           int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb,
                                           int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss, int64_t dq_sh,
                                           int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb, int64_t dv_ss,
-                                          int64_t dv_sh, float scale, int causal, int window, hipStream_t stream) {
+                                          int64_t dv_sh, float scale, int causal, int window, int seg_runs,
+                                          hipStream_t stream) {
   if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
   if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
       !aligned16(o, o_sb, o_ss, o_sh) || !aligned16(dout, o_sb, o_ss, o_sh) || !aligned16(dq, dq_sb, dq_ss, dq_sh) ||
@@ -1594,6 +1651,10 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.o = (const bf16*)o;
   a.dout = (const bf16*)dout; a.out = (bf16*)dq; a.lse = (float*)lse; a.delta = delta; a.seg = seg;
+  if (seg && seg_runs) {
+    a.rs = seg + (int64_t)B * S;
+    a.re = seg + 2 * (int64_t)B * S;
+  }
   a.dk = (bf16*)dk; a.dv = (bf16*)dv;
   const int64_t part = (int64_t)B * S * Hq * D;
   a.dk_part = work; a.dv_part = work ? work + part : nullptr;

@@ -104,7 +104,8 @@ class LlamaAttention(nn.Module):
         qkv = self.qkv_proj(h).view(S, B, self.nq + 2 * self.nkv, self.hd)
         def core(t):
             return F_.rope_attention(t, rt["positions"], rt["cos"], rt["sin"], self.nq, self.nkv, causal=True,
-                                     segment_ids=rt["segment_ids"], window=rt.get("window", -1), impl=rt["impl"])
+                                     segment_ids=rt["segment_ids"], window=rt.get("window", -1), impl=rt["impl"],
+                                     seg_info=rt.get("seg_info"))
 
         if rt.get("selective") and rt["impl"] != "flash" and self.training and torch.is_grad_enabled():
             # selective recompute (reference llama_model.py:506-534): keep only the attention inputs and
@@ -217,8 +218,11 @@ class Llama(BaseModel):
         cos, sin = self.rope.get(device, S)
         impl = self.config.resolved_attn_implementation(device.type)
         selective = self.gradient_checkpointing and self.config.recompute_granularity == "selective"
+        seg_info = None
+        if segment_ids is not None and device.type == "cuda" and impl in ("flash", "flash_attention_2", "hip"):
+            seg_info = F_.segment_info(segment_ids)  # run bounds, shared by every layer's attention
         return {"positions": position_ids, "cos": cos, "sin": sin, "segment_ids": segment_ids, "impl": impl,
-                "selective": selective}
+                "selective": selective, "seg_info": seg_info}
 
     def hidden_states(self, input_ids=None, position_ids=None, segment_ids=None, inputs_embeds=None,
                       gather_sequence: bool = True, embed_hook=None):

@@ -349,11 +349,39 @@ class _FlashAttnFn(Function):
         return dq, dk, dv, None, None, None, None
 
 
-def flash_attention(q, k, v, causal: bool = True, segment_ids=None, window: int = -1, scale: float | None = None):
-    """q: [B, S, Hq, D]; k/v: [B, S, Hkv, D]; segment_ids: optional int [B, S] (equal ids attend)."""
+def segment_info(segment_ids: torch.Tensor) -> torch.Tensor:
+    """[3, B, S] int32 for the flash kernels: segment id, first and last index of the contiguous run of
+    equal ids containing each token. Computed once per forward (a handful of scans) and shared by every
+    layer; lets a query block skip all key tiles outside its runs (ops on device, no host sync)."""
+    seg = segment_ids.to(torch.int32)
+    B, S = seg.shape
+    idx = torch.arange(S, device=seg.device, dtype=torch.int32).expand(B, S)
+    start = torch.ones_like(seg, dtype=torch.bool)
+    start[:, 1:] = seg[:, 1:] != seg[:, :-1]
+    end = torch.ones_like(seg, dtype=torch.bool)
+    end[:, :-1] = start[:, 1:]
+    rs = torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), dim=1).values
+    re = torch.where(end, idx, torch.full_like(idx, S)).flip(1).cummin(dim=1).values.flip(1)
+    return torch.stack([seg, rs.to(torch.int32), re.to(torch.int32)]).contiguous()
+
+
+def _native_seg(segment_ids, seg_info):
+    if segment_ids is None:
+        return None
+    if seg_info is not None:
+        return seg_info
+    if segment_ids.dim() == 3:  # already [3, B, S]
+        return segment_ids.to(torch.int32).contiguous()
+    return segment_info(segment_ids)
+
+
+def flash_attention(q, k, v, causal: bool = True, segment_ids=None, window: int = -1, scale: float | None = None,
+                    seg_info=None):
+    """q: [B, S, Hq, D]; k/v: [B, S, Hkv, D]; segment_ids: optional int [B, S] — tokens attend within
+    their contiguous run of equal ids (packed documents; 0 = padding)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if use_native(q):
-        seg = segment_ids.to(torch.int32).contiguous() if segment_ids is not None else None
+        seg = _native_seg(segment_ids, seg_info)
         return _FlashAttnFn.apply(q, k, v, seg, causal, -1 if window is None else int(window), scale)
     return ref.attention(q, k, v, causal, segment_ids, -1 if window is None else window, scale)
 
@@ -366,11 +394,12 @@ def rope_tables_to_full(cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor)
 
 
 def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool = True, segment_ids=None,
-                   window: int = -1, scale: float | None = None, impl: str = "flash"):
+                   window: int = -1, scale: float | None = None, impl: str = "flash", seg_info=None):
     """Fused RoPE + attention on the SEQ-MAJOR fused QKV buffer [S, B, n_q + 2 n_kv, D] -> [S, B, n_q, D].
 
     ``cos``/``sin``: fp32 half-width tables [max_pos, D/2]; ``positions``: [B, S] int;
-    ``segment_ids``: optional [B, S] (tokens attend only within equal ids).
+    ``segment_ids``: optional [B, S] (tokens attend only within their contiguous run of equal ids);
+    ``seg_info``: its precomputed :func:`segment_info` (shared across layers).
     """
     D = qkv.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -378,7 +407,7 @@ def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool =
     if use_native(qkv) and impl in ("flash", "flash_attention_2", "hip"):
         qkv = qkv.contiguous()
         pos = positions.t().contiguous().reshape(-1)
-        seg = segment_ids.to(torch.int32).contiguous() if segment_ids is not None else None
+        seg = _native_seg(segment_ids, seg_info)
         return _RopeFlashAttnFn.apply(qkv, pos, cos, sin, seg, n_q, n_kv, causal, win, scale)
     return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale,
                                impl).transpose(0, 1)
