@@ -12,6 +12,14 @@ and the fused AdamW update. Data is synthetic: three packed sequences of S=8192 
 per step (micro-batch 3 by default, weak scaling). W untimed warm-up steps, then exactly K timed steps between
 a barrier + device synchronize on both sides; the reported time is the MAX over ranks. Rank 0
 prints one JSON line.
+
+Other BASELINE.json configs (``--workload``; same JSON schema, their own metric string):
+  pt-packed  Llama-3-8B CLM with ``--packed-docs K`` isolated documents per row (varlen attention)
+  it         Phi-3-mini instruction tuning, NEFTune (alpha 5), GROUP_BY_LENGTH-style packed rows of
+             4096 tokens with segment ids (no cross-contamination), loss on ~half the tokens
+  dpo / orpo Llama-3-8B preference tuning: chosen + rejected sequences of 4096 tokens each per
+             micro-batch (DPO adds the frozen reference model's forward)
+TP / SP: ``--tp 2`` (the driver's scaling runs use the default data-parallel layout).
 """
 from __future__ import annotations
 
@@ -29,15 +37,41 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 LLAMA3_8B = dict(vocab_size=128256, hidden_size=4096, intermediate_size=14336, num_hidden_layers=32,
                  num_attention_heads=32, num_key_value_heads=8, max_position_embeddings=8192, rope_theta=500000.0,
                  rms_norm_eps=1e-5, bos_token_id=128000, eos_token_id=128001, tie_word_embeddings=False)
+# Phi-3-mini-128k-instruct geometry (LongRoPE tables with neutral factors: the HF factor lists are not
+# available offline; they do not change the compute)
+PHI3_MINI = dict(vocab_size=32064, hidden_size=3072, intermediate_size=8192, num_hidden_layers=32,
+                 num_attention_heads=32, num_key_value_heads=32, max_position_embeddings=131072,
+                 original_max_position_embeddings=4096, rope_theta=10000.0, rms_norm_eps=1e-5,
+                 rope_scaling={"type": "longrope", "short_factor": [1.0] * 48, "long_factor": [1.0] * 48},
+                 bos_token_id=1, eos_token_id=32000, pad_token_id=32000)
+
+# workload -> (metric, model name, default seq len, default micro-batch)
+WORKLOADS = {
+    "pt": ("tokens/sec (whole node) Llama-3-8B CLM pre-train", "Llama-3-8B", 8192, 3),
+    "pt-packed": ("tokens/sec (whole node) Llama-3-8B CLM pre-train, isolated packed documents", "Llama-3-8B",
+                  8192, 3),
+    "it": ("tokens/sec (whole node) Phi-3-mini instruction tuning, NEFTune + varlen packing", "Phi-3-mini-128k",
+           4096, 8),
+    "dpo": ("tokens/sec (whole node) Llama-3-8B DPO preference tuning", "Llama-3-8B", 4096, 2),
+    "orpo": ("tokens/sec (whole node) Llama-3-8B ORPO preference tuning", "Llama-3-8B", 4096, 2),
+}
 
 
-def flops_per_token(cfg: dict, S: int) -> float:
+def flops_per_token(cfg: dict, S: int, attn_frac: float = 1.0) -> float:
+    """6 x matmul params + causal attention FLOPs per token (attn_frac < 1 for packed documents)."""
     h, I, L, V = cfg["hidden_size"], cfg["intermediate_size"], cfg["num_hidden_layers"], cfg["vocab_size"]
     hq, hkv = cfg["num_attention_heads"], cfg["num_key_value_heads"]
     d = h // hq
     n_matmul = L * (h * (hq + 2 * hkv) * d + hq * d * h + 3 * h * I) + V * h
-    attn = L * 6 * 2 * S * h / 2  # causal: 6 (fwd+bwd) x 2 matmuls x S x h x 1/2
+    attn = L * 6 * 2 * S * h / 2 * attn_frac  # causal: 6 (fwd+bwd) x 2 matmuls x S x h x 1/2
     return 6 * n_matmul + attn
+
+
+def doc_lengths(S: int, n: int, g: torch.Generator) -> list[int]:
+    """n random document lengths summing to S (best-fit-packed rows hold a few documents each)."""
+    cuts = sorted(torch.randint(1, S, (n - 1,), generator=g).tolist()) if n > 1 else []
+    edges = [0, *cuts, S]
+    return [b - a for a, b in zip(edges[:-1], edges[1:]) if b > a]
 
 
 def main():
@@ -45,8 +79,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--seq", type=int, default=8192)
-    ap.add_argument("--micro-batch", type=int, default=3)
+    ap.add_argument("--workload", default="pt", choices=sorted(WORKLOADS))
+    ap.add_argument("--seq", type=int, default=None, help="sequence length (per side for dpo/orpo)")
+    ap.add_argument("--micro-batch", type=int, default=None)
+    ap.add_argument("--packed-docs", type=int, default=8, help="pt-packed / it: documents per row")
     ap.add_argument("--layers", type=int, default=None, help="debug only: fewer layers (result marked invalid)")
     ap.add_argument("--zero-stage", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1)
@@ -56,18 +92,18 @@ def main():
     ap.add_argument("--loss-chunk", type=int, default=8192, help="rows per lm_head GEMM of the fused CE")
     ap.add_argument("--force-sharded", action="store_true",
                     help="run the dp>1 engine schedule (RCCL reduce-scatter/all-gather, comm stream) even on 1 GPU")
-    ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
                     help="hipBLASLt solution selection (default: shipped TunableOp results)")
     args = ap.parse_args()
 
-    from llm_training_amd.lms.clm import CLM
-    from llm_training_amd.models.llama import Llama, LlamaConfig
     from llm_training_amd.ops.native import lib
     from llm_training_amd.parallel.context import ParallelContext, init_distributed
     from llm_training_amd.parallel.engine import DataParallelEngine
     from llm_training_amd.runtime.gemm_tuning import setup_gemm_tuning
 
+    metric, model_name, S_def, mb_def = WORKLOADS[args.workload]
+    S = args.seq or S_def
+    B = args.micro_batch or mb_def
     rank, local, world, device = init_distributed()
     if args.force_sharded and world == 1:
         import socket
@@ -82,28 +118,81 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     lib()  # fail loudly if the HIP extension is missing
     pc = ParallelContext.create("auto", args.tp, device)
-    cfg = dict(LLAMA3_8B)
+
+    phi3 = args.workload == "it"
+    cfg = dict(PHI3_MINI if phi3 else LLAMA3_8B)
     if args.layers:
         cfg["num_hidden_layers"] = args.layers
-    mcfg = LlamaConfig(**cfg, attn_implementation=args.attn, enable_gradient_checkpointing=args.ckpt,
-                       loss_chunk_size=args.loss_chunk)
+    common = dict(attn_implementation=args.attn, enable_gradient_checkpointing=args.ckpt,
+                  loss_chunk_size=args.loss_chunk)
+    if phi3:
+        from llm_training_amd.models.phi3 import Phi3 as Model
+        from llm_training_amd.models.phi3 import Phi3Config as MCfg
+    else:
+        from llm_training_amd.models.llama import Llama as Model
+        from llm_training_amd.models.llama import LlamaConfig as MCfg
+    mcfg = MCfg(**cfg, **common)
     torch.manual_seed(1234)
-    model = Llama(mcfg, pc, dtype=torch.bfloat16, device=device)
+    model = Model(mcfg, pc, dtype=torch.bfloat16, device=device)
     model.init_weights(seed=1234)
     stage = args.zero_stage if args.zero_stage is not None else (0 if pc.dp_size == 1 else 2)
     engine = DataParallelEngine(model, pc, stage, lr=3e-5, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
                                 offload_optimizer=args.offload_optimizer, force_sharded=args.force_sharded)
-    lm = CLM({"model": None})
-    lm.model = model
+    if args.workload in ("dpo", "orpo"):
+        from llm_training_amd.lms.preference import DPO, ORPO
+        lm = (DPO if args.workload == "dpo" else ORPO)({"model": None, "beta": 0.1})
+        lm.model = model
+        if args.workload == "dpo":
+            ref = Model(mcfg, pc, dtype=torch.bfloat16, device=device)
+            ref.load_state_dict(model.state_dict())
+            ref.requires_grad_(False)
+            ref.eval()
+            lm.ref_model = ref
+    else:
+        from llm_training_amd.lms.clm import CLM
+        lm = CLM({"model": None, "neftune_alpha": 5.0 if phi3 else None})
+        lm.model = model
     lm.train()
 
-    B, S = args.micro_batch, args.seq
+    V = cfg["vocab_size"]
     g = torch.Generator(device=device).manual_seed(1000 + pc.dp_rank)
+    gcpu = torch.Generator().manual_seed(2000 + pc.dp_rank)
+    attn_work = []  # fraction of full-causal attention work per step (packed documents)
+
+    def packed_segments(n_docs):
+        seg = torch.empty(B, S, dtype=torch.int32)
+        frac = 0.0
+        for b in range(B):
+            lens = doc_lengths(S, n_docs, gcpu)
+            seg[b] = torch.repeat_interleave(torch.arange(1, len(lens) + 1, dtype=torch.int32), torch.tensor(lens))
+            frac += sum(ln * ln for ln in lens) / (S * S)
+        attn_work.append(frac / B)
+        return seg.to(device)
 
     def make_batch():
-        ids = torch.randint(0, cfg["vocab_size"], (B, S), device=device, generator=g)
-        return {"input_ids": ids, "labels": ids, "position_ids": torch.arange(S, device=device).expand(B, S),
-                "attention_mask": None}
+        if args.workload in ("dpo", "orpo"):
+            out = {}
+            for side in ("chosen", "rejected"):
+                ids = torch.randint(0, V, (B, S), device=device, generator=g)
+                lab = ids.clone()
+                lab[:, : S // 4] = -100  # the prompt part carries no loss
+                out.update({f"{side}_input_ids": ids, f"{side}_labels": lab,
+                            f"{side}_attention_mask": torch.ones(B, S, dtype=torch.long, device=device)})
+            attn_work.append(1.0)
+            return out
+        ids = torch.randint(0, V, (B, S), device=device, generator=g)
+        batch = {"input_ids": ids, "labels": ids, "position_ids": torch.arange(S, device=device).expand(B, S),
+                 "attention_mask": None}
+        if args.workload in ("pt-packed", "it"):
+            batch["attention_mask"] = packed_segments(args.packed_docs)
+            batch["attention_mask_trivial"] = False
+            if args.workload == "it":  # loss only on the "assistant" part of the documents
+                lab = ids.clone()
+                lab[torch.rand(B, S, device=device, generator=g) < 0.5] = -100
+                batch["labels"] = lab
+        else:
+            attn_work.append(1.0)
+        return batch
 
     def step(batch):
         engine.begin_step(1)
@@ -121,14 +210,14 @@ def main():
     for i in range(args.warmup):
         loss = step(batches[i])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(batches[args.warmup + i])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     el = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
@@ -136,22 +225,37 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = el.item()
     final_loss = float(loss.detach().float().item())
-    tokens = pc.dp_size * B * S * args.steps
+    seqs = 2 * B if args.workload in ("dpo", "orpo") else B
+    tokens = pc.dp_size * seqs * S * args.steps
     tps = tokens / el
-    fpt = flops_per_token(cfg, S)
+    timed = attn_work[args.warmup:]
+    frac = sum(timed) / max(1, len(timed))
+    fpt = flops_per_token(cfg, S, frac)
+    if args.workload == "dpo":
+        fpt += flops_per_token(cfg, S, frac) / 3  # frozen reference model: forward only
     peak_mem = torch.cuda.max_memory_allocated(device) / 2 ** 30
     if rank == 0:
         par = f"dp{pc.dp_size}" + (f"-tp{pc.tp_size}" if pc.tp_size > 1 else "")
+        cfg_out = {"model": model_name if not args.layers else f"{model_name}-{args.layers}L(INVALID-debug)",
+                   "global_batch": pc.dp_size * B, "seq_len": S, "parallelism": par, "zero_stage": stage,
+                   "attn": args.attn, "activation_checkpointing": args.ckpt,
+                   "optimizer": ("host AdamW (offload) fp32 master" if args.offload_optimizer
+                                 else "fused AdamW fp32 master"),
+                   "grad_clip": 1.0, "gemm_tuning": gemm_mode}
+        if args.workload != "pt":
+            cfg_out["workload"] = args.workload
+        if args.workload in ("pt-packed", "it"):
+            cfg_out.update(packed_docs_per_row=args.packed_docs, attn_work_vs_causal=round(frac, 4))
+        if phi3:
+            cfg_out["neftune_alpha"] = 5.0
+        if args.force_sharded:
+            cfg_out["force_sharded"] = True
         out = {
-            "metric": "tokens/sec (whole node) Llama-3-8B CLM pre-train",
+            "metric": metric,
             "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1000, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random tokens, random-init weights)",
-            "config": {"model": "Llama-3-8B" if not args.layers else f"Llama-3-8B-{args.layers}L(INVALID-debug)",
-                       "global_batch": pc.dp_size * B, "seq_len": S, "parallelism": par, "zero_stage": stage,
-                       "attn": args.attn, "activation_checkpointing": args.ckpt, "optimizer": ("host AdamW (offload) fp32 master" if args.offload_optimizer else "fused AdamW fp32 master"),
-                       "grad_clip": 1.0, "gemm_tuning": gemm_mode,
-                       **({"force_sharded": True} if args.force_sharded else {})},
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)", "config": cfg_out,
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "mfu": round(tps / world * fpt / 2.5e15, 4),
             "tflops_per_gpu": round(tps / world * fpt / 1e12, 1),

@@ -15,10 +15,13 @@ optim/master_weight_wrapper.py) — with one engine designed around MI355X:
   a tensor hook on that input launches the unit's reduce-scatter (ZeRO) or all-reduce (DDP) on a
   dedicated communication stream while backward continues with the previous unit.
 * **Gradient sharding (stage >= 2).** A decoder layer's full-size gradient buffer exists only while
-  that layer's backward runs: a hook on the layer OUTPUT's gradient allocates it, the input-gradient
-  hook reduce-scatters it into the persistent 1/dp shard (accumulating across micro-batches, like
-  DeepSpeed stage 2's per-micro-batch reduction, deepspeed_strategy.py:40-44) and frees it. Resident
-  gradient memory is 2 B/param / dp plus at most a couple of in-flight layers.
+  that layer's backward runs: a hook on the layer OUTPUT's gradient takes a buffer from a small ring
+  (GRAD_POOL slots of the largest layer's size, reused in order; a slot's previous reduce-scatter is
+  awaited with a stream event, never the host), the input-gradient hook reduce-scatters it into the
+  persistent 1/dp shard (accumulating across micro-batches, like DeepSpeed stage 2's per-micro-batch
+  reduction, deepspeed_strategy.py:40-44) and hands the slot back. Resident gradient memory is
+  2 B/param / dp plus the ring (3 layers); a fixed ring instead of the caching allocator keeps the
+  footprint constant when HBM is nearly full (allocator retries there cost device-wide syncs).
 * **Optimizer.** fp32 master weights, Adam m and v exist only for this rank's shard of each unit
   (stage >= 1) — 12 B/param / dp — and are updated by ONE fused HIP AdamW launch per unit that also
   writes the bf16 parameter shard. Gradient averaging (1/dp), accumulation (1/accum) and clipping are
@@ -63,6 +66,7 @@ from .context import ParallelContext
 logger = logging.getLogger("llm_training")
 
 ALIGN = 64  # elements
+GRAD_POOL = 3  # transient gradient buffers (stage >= 2): layer being written + reductions in flight
 
 
 def _round_up(n: int, m: int) -> int:
@@ -97,7 +101,8 @@ class _Unit:
     opt_event: object = None        # async AdamW of this unit done (stage 3 shard update)
     replicated: bool = False
     keep_gathered: bool = False     # stage 3: params used outside the hooked module's forward
-    transient_grad: bool = False    # gradient buffer allocated per backward, freed after its reduce
+    transient_grad: bool = False    # gradient buffer taken from the ring per backward, returned after its reduce
+    gslot: object = None            # the ring slot currently held
     grad_gaps: list = field(default_factory=list)  # alignment padding ranges of the flat buffer
     g_host: torch.Tensor | None = None    # optimizer offload: pinned gradient shard
     p_host: torch.Tensor | None = None    # optimizer offload: pinned bf16 parameter shard
@@ -234,12 +239,14 @@ class DataParallelEngine:
         # (tied weights, the fused loss head) and keep theirs
         u.transient_grad = (self.shard_gradients and sharded and not keep and i > 0 and m is not None
                             and _hookable(m))
-        u.gflat = torch.zeros(numel, device=dev, dtype=self.grad_dtype)
-        for p, o in zip(params, offs):
-            p.main_grad = u.gflat[o:o + p.numel()].view(p.shape)
-            p.grad_added = False
         if u.transient_grad:
-            u.gflat.untyped_storage().resize_(0)
+            u.gflat = torch.empty(0, device=dev, dtype=self.grad_dtype)  # bound to a ring slot per backward
+        else:
+            u.gflat = torch.zeros(numel, device=dev, dtype=self.grad_dtype)
+            for p, o in zip(params, offs):
+                p.main_grad = u.gflat[o:o + p.numel()].view(p.shape)
+        for p in params:
+            p.grad_added = False
         sn = numel // dp
         r = self.pc.dp_rank if dp > 1 else 0
         stage = self._ustage(u)
@@ -299,21 +306,40 @@ class DataParallelEngine:
 
     # ------------------------------------------------------------------ transient gradient buffers
     def _grad_allocated(self, u: _Unit) -> bool:
-        return u.gflat.untyped_storage().size() > 0
+        return u.gslot is not None
 
     def _alloc_grad(self, u: _Unit):
-        if self._grad_allocated(u):
+        if u.gslot is not None:
             return
-        u.gflat.untyped_storage().resize_(u.numel * u.gflat.element_size())
+        if not hasattr(self, "_gpool"):
+            n = max(v.numel for v in self.units if v.transient_grad)
+            self._gpool = [{"buf": torch.empty(n, device=self.device, dtype=self.grad_dtype), "event": None,
+                            "owner": None} for _ in range(GRAD_POOL)]
+            self._gpool_next = 0
+        slot = self._gpool[self._gpool_next]
+        self._gpool_next = (self._gpool_next + 1) % len(self._gpool)
+        assert slot["owner"] is None, "gradient ring exhausted: a slot's owner never reduced it"
+        if slot["event"] is not None:  # its previous reduce-scatter must have read it
+            torch.cuda.current_stream().wait_event(slot["event"])
+            slot["event"] = None
+        slot["owner"] = u.idx
+        u.gslot = slot
+        u.gflat = slot["buf"][:u.numel]
+        for p, o in zip(u.params, u.offsets):
+            p.main_grad = u.gflat[o:o + p.numel()].view(p.shape)
+            p.grad_added = False  # fresh buffer: the first gradient written is a copy, not an add
         for a, b in u.grad_gaps:  # alignment padding is reduced too: keep it zero
             u.gflat[a:b].zero_()
-        for p in u.params:  # fresh buffer: the first gradient written is a copy, not an add
-            p.grad_added = False
 
     def _free_grad(self, u: _Unit, stream=None):
+        slot = u.gslot
         if stream is not None:
-            u.gflat.record_stream(stream)
-        u.gflat.untyped_storage().resize_(0)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            slot["event"] = ev
+        slot["owner"] = None
+        u.gslot = None
+        u.gflat = u.gflat.new_empty(0)
 
     # ------------------------------------------------------------------ hooks
     def _install_hooks(self):
@@ -532,17 +558,18 @@ class DataParallelEngine:
         return u.gflat
 
     def grad_memory_bytes(self) -> dict[str, int]:
-        """Resident gradient memory of this rank: persistent buffers vs transient (currently allocated)."""
+        """Gradient memory of this rank: persistent buffers, transient buffers held right now (ring slots
+    bound to a unit) and the ring itself."""
         persistent = transient = 0
         for u in self.units:
             if u.gshard is not None:
                 persistent += u.gshard.numel() * u.gshard.element_size()
-            nb = u.gflat.untyped_storage().size()
             if u.transient_grad:
-                transient += nb
+                transient += u.gflat.numel() * u.gflat.element_size()
             else:
-                persistent += nb
-        return {"persistent": persistent, "transient": transient}
+                persistent += u.gflat.numel() * u.gflat.element_size()
+        pool = sum(s["buf"].numel() * s["buf"].element_size() for s in getattr(self, "_gpool", []))
+        return {"persistent": persistent, "transient": transient, "pool": pool}
 
     def clip_and_scale(self, max_norm: float | None):
         """Global grad norm computed on device; returns the device scalar scale used by the optimizer."""
