@@ -46,12 +46,23 @@ def _split_args(argv: list[str]):
     return configs, overrides, rest
 
 
+def check_top_level(cfg: dict):
+    """Reject unknown top-level keys (jsonargparse does, cli.py:17-83): a typo must not be ignored."""
+    import difflib
+    bad = [k for k in cfg if k not in TOP_LEVEL]
+    if bad:
+        hints = {k: difflib.get_close_matches(k, sorted(TOP_LEVEL), n=1) for k in bad}
+        msg = ", ".join(f"{k!r}" + (f" (did you mean {h[0]!r}?)" if h else "") for k, h in hints.items())
+        raise ValueError(f"unknown top-level config key(s): {msg}; allowed: {sorted(TOP_LEVEL)}")
+
+
 def build_from_config(cfg: dict):
     """(trainer, lm, datamodule) from a resolved config dict."""
     from ..config.loader import instantiate
     from ..runtime.callbacks import ExtraConfig, OutputRedirection, SaveConfigCallback, TQDMProgressBar
     from ..runtime.trainer import Trainer
 
+    check_top_level(cfg)
     ExtraConfig(cfg.get("float32_matmul_precision"), cfg.get("logging_level", "INFO"))
     if os.environ.get("SLURM_NTASKS") == "1":
         for k in ("SLURM_JOB_ID", "SLURM_NTASKS"):
@@ -60,8 +71,11 @@ def build_from_config(cfg: dict):
     tcfg = instantiate(tcfg)
     callbacks = list(tcfg.pop("callbacks", None) or [])
     callbacks.insert(0, SaveConfigCallback(cfg))
-    orc = cfg.get("output_redirection")
-    if orc is not None and (orc.get("enabled", True) if isinstance(orc, dict) else orc):
+    # on by default, as in the reference (cli.py:67 adds OutputRedirection with enabled=True)
+    orc = cfg.get("output_redirection", {})
+    if orc is None or orc is True:
+        orc = {}
+    if orc is not False and (orc.get("enabled", True) if isinstance(orc, dict) else True):
         callbacks.insert(1, OutputRedirection(**(orc if isinstance(orc, dict) else {})))
     tq = cfg.get("tqdm_progress")
     if isinstance(tq, dict):

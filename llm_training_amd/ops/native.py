@@ -51,8 +51,11 @@ def lib():
 
 
 def use_native(t: torch.Tensor) -> bool:
-    """GPU tensors always go to the HIP kernels (no silent fallback)."""
+    """bf16 GPU tensors always go to the HIP kernels (no silent fallback: a missing library raises).
+
+    The kernels are bf16 MFMA kernels; fp32 GPU tensors (``precision: 32-true``) and CPU tensors run
+    the torch reference ops of :mod:`llm_training_amd.ops.reference`."""
     if t.device.type == "cuda":
         lib()
-        return True
+        return t.dtype == torch.bfloat16
     return False

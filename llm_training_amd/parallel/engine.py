@@ -141,7 +141,8 @@ class DataParallelEngine:
         dev = next(model.parameters()).device
         self.device = dev
         self.cuda = dev.type == "cuda"
-        self.native = self.cuda and use_native(torch.empty(0, device=dev))
+        # the optimizer / norm kernels take fp32 or bf16 gradients: native on any GPU
+        self.native = self.cuda and use_native(torch.empty(0, device=dev, dtype=torch.bfloat16))
         self.comm_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.overlap) else None
         # AdamW runs on its own stream: unit i's update overlaps the next step's forward of units < i
         # (memory-bound optimizer beside compute-bound GEMMs); each unit's forward waits for its own

@@ -70,6 +70,7 @@ class FSDP2Strategy(Strategy):
         # master and Adam moments move to pinned host memory, updated by the native host AdamW; the bf16
         # parameters and gradients stay in HBM (288 GB holds them for any model that fits the node)
         self.offload_optimizer = _wants_offload(offload_policy)
+        _check_kwargs("FSDP2Strategy", kw, FSDP2_PASSIVE)
         self.extra = {"mp_policy": mp_policy, "use_master_weights": use_master_weights, **kw}
 
 
@@ -88,6 +89,33 @@ class DeepSpeedStrategy(Strategy):
                            "offload_optimizer is")
         self.extra = {"exclude_frozen_parameters": exclude_frozen_parameters,
                       "allgather_bucket_size": allgather_bucket_size, "reduce_bucket_size": reduce_bucket_size, **kw}
+
+
+# upstream DeepSpeedStrategy / Lightning arguments (deepspeed_strategy.py:17-72) that the engine takes no
+# action on (buffer / bucket / aio tuning of DeepSpeed's own engine, fp16 loss scaling): accepted so
+# reference configs load, recorded in ``extra``; any other name is a typo and raises
+DEEPSPEED_PASSIVE = {
+    "accelerator", "zero_optimization", "remote_device", "offload_params_device", "params_buffer_count",
+    "params_buffer_size", "max_in_cpu", "optimizer_buffer_count", "block_size", "queue_depth", "single_submit",
+    "overlap_events", "thread_count", "pin_memory", "sub_group_size", "contiguous_gradients",
+    "allgather_partitions", "reduce_scatter", "allgather_bucket_size", "reduce_bucket_size",
+    "zero_allow_untested_optimizer", "logging_batch_size_per_gpu", "config", "logging_level", "parallel_devices",
+    "cluster_environment", "loss_scale", "initial_scale_power", "loss_scale_window", "hysteresis",
+    "min_loss_scale", "partition_activations", "cpu_checkpointing", "contiguous_memory_optimization",
+    "synchronize_checkpoint_boundary", "load_full_weights", "precision_plugin", "exclude_frozen_parameters",
+    "raise_error_at_min_scale", "zero3_leaf_modules", "stage3_max_live_parameters", "stage3_max_reuse_distance",
+    "stage3_prefetch_bucket_size", "stage3_param_persistence_threshold"}
+FSDP2_PASSIVE = {"accelerator", "parallel_devices", "cluster_environment", "checkpoint_io", "precision_plugin",
+                 "precision", "mp_policy", "use_master_weights"}
+
+
+def _check_kwargs(cls_name: str, kw: dict, allowed: set):
+    bad = sorted(k for k in kw if k not in allowed)
+    if bad:
+        import difflib
+        hint = {k: difflib.get_close_matches(k, sorted(allowed), n=1) for k in bad}
+        raise TypeError(f"{cls_name} got unknown argument(s): " + ", ".join(
+            f"{k!r}" + (f" (did you mean {h[0]!r}?)" if h else "") for k, h in hint.items()))
 
 
 def _wants_offload(policy) -> bool:

@@ -32,9 +32,25 @@ from .strategies import Strategy, resolve_strategy
 
 logger = logging.getLogger("llm_training")
 
-PRECISIONS = {"bf16-true": torch.bfloat16, "bf16": torch.bfloat16, "16-true": torch.float16,
-              "32-true": torch.float32, "32": torch.float32, "bf16-mixed": torch.bfloat16, 32: torch.float32,
-              16: torch.float16, "16-mixed": torch.float16}
+# precision -> (parameter / compute dtype, gradient accumulation + reduction dtype)
+#  * bf16-true : bf16 params, bf16 gradients, fp32 master weights + Adam state (reference bf16-true with
+#                use_master_weights, fsdp2_strategy.py:249-250)
+#  * bf16-mixed: bf16 compute copies, fp32 gradients (accumulated and reduced in fp32) on fp32 masters —
+#                the numerics of autocast over fp32 parameters (fsdp2_precision.py:55-90,106-117)
+#  * 32-true   : fp32 everywhere; on the GPU the torch ops run (the HIP kernels are bf16 MFMA kernels)
+#  * 16-*      : rejected with an explanation (fp16 needs loss scaling and the kernels are bf16; bf16 runs
+#                at the same MFMA rate on MI355X with fp32's exponent range)
+PRECISIONS = {"bf16-true": (torch.bfloat16, None), "bf16": (torch.bfloat16, None),
+              "bf16-mixed": (torch.bfloat16, torch.float32), "32-true": (torch.float32, None),
+              "32": (torch.float32, None), 32: (torch.float32, None), "64-true": None, "16-true": None,
+              "16-mixed": None, 16: None, "16": None, "transformer-engine": None}
+# Lightning Trainer arguments that exist upstream but have no effect here: accepted (with a warning)
+# so reference configs load; anything else is a typo and raises, as jsonargparse would
+IGNORED_TRAINER_ARGS = {"devices", "accelerator", "num_sanity_val_steps", "benchmark", "fast_dev_run",
+                        "overfit_batches", "profiler", "detect_anomaly", "barebones", "plugins",
+                        "sync_batchnorm", "reload_dataloaders_every_n_epochs", "enable_model_summary",
+                        "inference_mode", "use_distributed_sampler", "min_epochs", "min_steps", "max_time",
+                        "limit_test_batches", "limit_predict_batches", "move_metrics_to_cpu"}
 
 
 class TrainerState:
@@ -88,8 +104,23 @@ class Trainer:
         self.state = TrainerState()
         self.should_stop = False
         self.unused = unused
+        bad = sorted(k for k in unused if k not in IGNORED_TRAINER_ARGS)
+        if bad:
+            import difflib
+            import inspect
+            known = sorted(set(inspect.signature(Trainer.__init__).parameters) - {"self", "unused"}
+                           | IGNORED_TRAINER_ARGS)
+            hint = {k: difflib.get_close_matches(k, known, n=1) for k in bad}
+            raise TypeError("Trainer got unknown argument(s): " + ", ".join(
+                f"{k!r}" + (f" (did you mean {h[0]!r}?)" if h else "") for k, h in hint.items()))
         if unused:
-            logger.debug("Trainer: ignoring unsupported arguments %s", sorted(unused))
+            logger.info("Trainer: arguments without effect in this framework: %s", sorted(unused))
+        if precision not in PRECISIONS:
+            raise ValueError(f"unknown precision {precision!r}; use one of bf16-true, bf16-mixed, 32-true")
+        if PRECISIONS[precision] is None:
+            raise ValueError(f"precision {precision!r} is not supported: the MI355X kernels are bf16 MFMA kernels "
+                             "(same rate as fp16, fp32 exponent range, no loss scaling needed) — use bf16-true or "
+                             "bf16-mixed, or 32-true for fp32")
         self.pc: ParallelContext | None = None
         self.engine: DataParallelEngine | None = None
         self.lm = None
@@ -128,16 +159,11 @@ class Trainer:
 
     @property
     def param_dtype(self):
-        dt = PRECISIONS.get(self.precision, torch.bfloat16)
-        if dt == torch.float16 and torch.cuda.is_available():
-            # the reference's fp16 modes need a GradScaler; on MI355X bf16 runs the MFMAs at the same
-            # rate with fp32's exponent range, and the HIP kernels are bf16-only: run fp16 configs in bf16
-            if not getattr(self, "_fp16_warned", False):
-                logger.warning("precision %s: training in bf16 (same MFMA rate, no loss scaling needed)",
-                               self.precision)
-                self._fp16_warned = True
-            return torch.bfloat16
-        return dt
+        return PRECISIONS[self.precision][0]
+
+    @property
+    def grad_dtype(self):
+        return PRECISIONS[self.precision][1]
 
     # ------------------------------------------------------------------ setup
     def setup(self, lm, datamodule, ckpt_path: str | None = None):
@@ -170,7 +196,8 @@ class Trainer:
         rd = getattr(st, "grad_reduce_dtype", None)
         self.engine = DataParallelEngine(lm.model, self.pc, st.zero_stage, lr=hp["lr"], betas=hp["betas"],
                                          eps=hp["eps"], weight_decay=hp["weight_decay"],
-                                         reduce_dtype=getattr(torch, rd) if rd else None,
+                                         grad_dtype=self.grad_dtype,
+                                         reduce_dtype=getattr(torch, rd) if rd else self.grad_dtype,
                                          reshard_after_forward=st.reshard_after_forward,
                                          overlap_comm=st.overlap_comm,
                                          offload_optimizer=getattr(st, "offload_optimizer", False))
