@@ -37,6 +37,10 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
 hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N, int K,
                      int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream);
 int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D);
+hipError_t llmt_quant_int8(const void* x, int x_fp32, int8_t* q, float* scale, int64_t n, hipStream_t stream);
+hipError_t llmt_dequant_int8(const int8_t* q, const float* scale, void* y, int64_t n, hipStream_t stream);
+hipError_t llmt_dequant_sum(const int8_t* q, const float* scale, void* out, int out_fp32, int64_t n, int k,
+                            int accumulate, hipStream_t stream);
 hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                                const float* lse, float* delta, const int* seg, void* dq, void* dk, void* dv,
                                float* work, int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss,
@@ -255,6 +259,43 @@ void sumsq_(const at::Tensor& x, at::Tensor out) {
         "sumsq");
 }
 
+// ---------------------------------------------------------------- int8 blockwise quantisation (ZeRO++)
+// one fp32 scale per 64 elements; n must be a multiple of 64
+void quant_int8_(const at::Tensor& x, at::Tensor q, at::Tensor scale) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "quant_int8: x must be a contiguous bf16/fp32 GPU tensor");
+  const int64_t n = x.numel();
+  TORCH_CHECK(n % 64 == 0, "quant_int8: numel % 64");
+  TORCH_CHECK(q.scalar_type() == at::kChar && q.numel() == n && q.is_contiguous(), "quant_int8: q");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == n / 64 && scale.is_contiguous(), "quant_int8: scale");
+  check(llmt_quant_int8(x.data_ptr(), x.scalar_type() == at::kFloat, (int8_t*)q.data_ptr(), scale.data_ptr<float>(), n,
+                        cur_stream()),
+        "quant_int8");
+}
+
+void dequant_int8_(const at::Tensor& q, const at::Tensor& scale, at::Tensor y) {
+  const int64_t n = y.numel();
+  TORCH_CHECK(y.is_cuda() && y.is_contiguous() && y.scalar_type() == at::kBFloat16 && n % 64 == 0, "dequant_int8: y");
+  TORCH_CHECK(q.scalar_type() == at::kChar && q.numel() == n && q.is_contiguous(), "dequant_int8: q");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == n / 64 && scale.is_contiguous(), "dequant_int8: scale");
+  check(llmt_dequant_int8((const int8_t*)q.data_ptr(), scale.data_ptr<float>(), y.data_ptr(), n, cur_stream()),
+        "dequant_int8");
+}
+
+// out (+)= sum over the k chunks of q [k, n] (scales [k, n/64])
+void dequant_sum_(const at::Tensor& q, const at::Tensor& scale, at::Tensor out, int64_t k, bool accumulate) {
+  const int64_t n = out.numel();
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && n % 64 == 0 &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "dequant_sum: out");
+  TORCH_CHECK(q.scalar_type() == at::kChar && q.numel() == k * n && q.is_contiguous(), "dequant_sum: q");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() == k * n / 64 && scale.is_contiguous(),
+              "dequant_sum: scale");
+  check(llmt_dequant_sum((const int8_t*)q.data_ptr(), scale.data_ptr<float>(), out.data_ptr(),
+                         out.scalar_type() == at::kFloat, n, (int)k, accumulate ? 1 : 0, cur_stream()),
+        "dequant_sum");
+}
+
 // ---------------------------------------------------------------- GEMM
 // c (+)= X . Y^T with X = a ([M, K], or [K, M] when a_mn) and Y = b ([N, K], or [K, N] when b_mn);
 // bf16 operands, c bf16 or fp32 [M, N] with unit column stride.
@@ -378,6 +419,9 @@ TORCH_LIBRARY(llmt, m) {
       "adamw_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? pout, float lr, float b1, float b2, "
       "float eps, float wd, int step, Tensor? gscale) -> ()");
   m.def("sumsq_(Tensor x, Tensor(a!) out) -> ()");
+  m.def("quant_int8_(Tensor x, Tensor(a!) q, Tensor(b!) scale) -> ()");
+  m.def("dequant_int8_(Tensor q, Tensor scale, Tensor(a!) y) -> ()");
+  m.def("dequant_sum_(Tensor q, Tensor scale, Tensor(a!) out, int k, bool accumulate) -> ()");
   m.def("gemm_(Tensor a, Tensor b, Tensor(a!) c, bool a_mn, bool b_mn, bool accumulate) -> ()");
   m.def(
       "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window) -> (Tensor, "
@@ -396,6 +440,9 @@ TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("cross_entropy_", &cross_entropy_);
   m.impl("adamw_", &adamw_);
   m.impl("sumsq_", &sumsq_);
+  m.impl("quant_int8_", &quant_int8_);
+  m.impl("dequant_int8_", &dequant_int8_);
+  m.impl("dequant_sum_", &dequant_sum_);
   m.impl("gemm_", &gemm_);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
