@@ -46,6 +46,22 @@ optim/master_weight_wrapper.py) — with one engine designed around MI355X:
   upload, so the PCIe traffic of unit i+1 overlaps the host math of unit i and the next forward only
   waits for its own unit.
 
+* **Parameter offload** (``offload_params=True``, stage 3; DeepSpeed ``offload_parameters``): the bf16
+  parameter shard lives in pinned host memory and is uploaded into the unit's own slice of the
+  gathered buffer right before its in-place all-gather (both on the comm stream). With optimizer
+  offload the host AdamW writes that shard directly; otherwise the device AdamW's output is copied
+  down after the step.
+* **NVMe optimizer offload** (``offload_device="nvme"``, DeepSpeed ``offload_optimizer_device: nvme``
+  + ``nvme_path``): master / m / v are file-backed (mmap) host tensors under ``nvme_path``; the host
+  AdamW streams through them and the page cache moves them to and from the drive.
+* **ZeRO++** (deepspeed_strategy.py:70-72,94-102):
+  - ``quantized_weights`` (qwZ): stage-3 parameter all-gathers move int8 + one fp32 scale per 64
+    elements (csrc/quant.hip) instead of bf16 — half the bytes; every rank keeps its own slice exact.
+  - ``quantized_gradients`` (qgZ): gradient reduce-scatter becomes an all-to-all of int8-quantised
+    chunks plus a fused dequantise-and-sum into the fp32/bf16 shard.
+  - ``hpz_partition_size`` (hpZ): after a stage-3 unit's forward a secondary copy partitioned over the
+    hpz sub-group (the GPUs of one node) is kept, so the backward re-gather stays on xGMI.
+
 Checkpoint layout (see ckpt/): per-rank shards of master / m / v / params plus a JSON index.
 """
 from __future__ import annotations
@@ -106,6 +122,7 @@ class _Unit:
     grad_gaps: list = field(default_factory=list)  # alignment padding ranges of the flat buffer
     g_host: torch.Tensor | None = None    # optimizer offload: pinned gradient shard
     p_host: torch.Tensor | None = None    # optimizer offload: pinned bf16 parameter shard
+    sec: torch.Tensor | None = None       # hpZ: secondary (intra-node) partition of the gathered params
 
     @property
     def shard_numel(self):
@@ -118,9 +135,18 @@ class DataParallelEngine:
                  grad_dtype: torch.dtype | None = None, reduce_dtype: torch.dtype | None = None,
                  reshard_after_forward: bool = True, overlap_comm: bool = True, overlap_step: bool = True,
                  offload_optimizer: bool = False, force_sharded: bool | None = None,
-                 shard_gradients: bool | None = None):
+                 shard_gradients: bool | None = None, offload_params: bool = False, offload_device: str = "cpu",
+                 nvme_path: str | None = None, quantized_weights: bool = False, quantized_gradients: bool = False,
+                 hpz_partition_size: int = 1):
         self.model = model
-        self.offload = bool(offload_optimizer)
+        self.offload = bool(offload_optimizer) or offload_device == "nvme"
+        self.offload_device = offload_device
+        self.nvme_path = nvme_path
+        if offload_device == "nvme" and not nvme_path:
+            raise ValueError("optimizer offload to nvme needs nvme_path")
+        self.offload_params = bool(offload_params)
+        self.quantized_weights = bool(quantized_weights)
+        self.quantized_gradients = bool(quantized_gradients)
         self.pc = pc
         self.stage = int(zero_stage)
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
@@ -135,6 +161,22 @@ class DataParallelEngine:
             self.group = dist.group.WORLD
         self.overlap = overlap_comm and self.sharded
         self.reshard_after_forward = reshard_after_forward
+        if self.offload_params and not (self.stage >= 3 and self.sharded):
+            raise ValueError("parameter offload needs ZeRO stage 3 (DeepSpeed offload_parameters)")
+        # hpZ: contiguous blocks of hpz ranks of the data-parallel group (one node's GPUs)
+        self.hpz = int(hpz_partition_size or 1)
+        self.hpz_group = None
+        if self.hpz > 1 and self.stage >= 3 and self.sharded and self.hpz < self.dp:
+            if self.dp % self.hpz:
+                raise ValueError(f"zero_hpz_partition_size {self.hpz} must divide the data-parallel size {self.dp}")
+            ranks = dist.get_process_group_ranks(self.group) if self.group is not dist.group.WORLD else \
+                list(range(dist.get_world_size()))
+            for b in range(self.dp // self.hpz):
+                blk = ranks[b * self.hpz:(b + 1) * self.hpz]
+                g = dist.new_group(blk)
+                if dist.get_rank() in blk:
+                    self.hpz_group = g
+            self.hpz_rank = self.pc.dp_rank % self.hpz
         self.step_count = 0
         self.accum = 1
         self.micro = 0
@@ -150,7 +192,8 @@ class DataParallelEngine:
         overlap_step = overlap_step and os.environ.get("LLMT_OVERLAP_STEP", "1") != "0"
         self.opt_stream = (torch.cuda.Stream(device=dev) if (self.cuda and overlap_step and not self.offload)
                            else None)
-        self.copy_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.offload) else None
+        self.copy_stream = (torch.cuda.Stream(device=dev) if (self.cuda and (self.offload or self.offload_params))
+                            else None)
         # models built from our fused ops write weight grads straight into the flat buffers; others
         # (transformers modules) leave ordinary .grad tensors that are absorbed after backward
         self.autograd_grads = not getattr(model, "writes_main_grad", True)
@@ -259,21 +302,49 @@ class DataParallelEngine:
             u.master = pflat.float().clone()
         if self.offload:
             pin = self.cuda
-            u.master = u.master.cpu().pin_memory() if pin else u.master.cpu()
+            if self.offload_device == "nvme":
+                u.master = self._nvme_tensor(i, "master", u.master)
+            else:
+                u.master = u.master.cpu().pin_memory() if pin else u.master.cpu()
             gdt = self.reduce_dtype if (stage >= 1 and sharded) else self.grad_dtype
             u.g_host = torch.empty(u.master.numel(), dtype=gdt, pin_memory=pin)
             # bf16 models: the host kernel also writes the bf16 copy that is uploaded; fp32 models
             # upload the master itself
             if self.param_dtype == torch.bfloat16:
                 u.p_host = torch.empty(u.master.numel(), dtype=torch.bfloat16, pin_memory=pin)
-        u.exp_avg = torch.zeros_like(u.master)
-        u.exp_avg_sq = torch.zeros_like(u.master)
-        if self.offload and self.cuda:
-            u.exp_avg, u.exp_avg_sq = u.exp_avg.pin_memory(), u.exp_avg_sq.pin_memory()
+        if self.offload and self.offload_device == "nvme":
+            u.exp_avg = self._nvme_tensor(i, "exp_avg", torch.zeros(u.master.numel()))
+            u.exp_avg_sq = self._nvme_tensor(i, "exp_avg_sq", torch.zeros(u.master.numel()))
+        else:
+            u.exp_avg = torch.zeros_like(u.master)
+            u.exp_avg_sq = torch.zeros_like(u.master)
+            if self.offload and self.cuda:
+                u.exp_avg, u.exp_avg_sq = u.exp_avg.pin_memory(), u.exp_avg_sq.pin_memory()
         if stage >= 3 and sharded:
-            u.pshard = pflat[r * sn:(r + 1) * sn].clone()
+            if self.offload_params:
+                if u.p_host is not None:  # the host AdamW writes the offloaded shard in place
+                    u.p_host.copy_(pflat[r * sn:(r + 1) * sn])
+                    u.pshard = u.p_host
+                else:
+                    u.pshard = pflat[r * sn:(r + 1) * sn].to("cpu", copy=True)
+                    if self.cuda:
+                        u.pshard = u.pshard.pin_memory()
+            else:
+                u.pshard = pflat[r * sn:(r + 1) * sn].clone()
             self._free_full(u)
         return u
+
+    def _nvme_tensor(self, unit: int, kind: str, init: torch.Tensor) -> torch.Tensor:
+        """fp32 host tensor backed by a file under nvme_path (mmap; the page cache does the I/O)."""
+        os.makedirs(self.nvme_path, exist_ok=True)
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        fn = os.path.join(self.nvme_path, f"rank{rank}_unit{unit}_{kind}.bin")
+        n = init.numel()
+        with open(fn, "wb") as f:
+            f.truncate(n * 4)
+        t = torch.from_file(fn, shared=True, size=n, dtype=torch.float32)
+        t.copy_(init.reshape(-1))
+        return t
 
     def _ustage(self, u: _Unit) -> int:
         return 0 if u.replicated else self.stage
@@ -384,7 +455,7 @@ class DataParallelEngine:
                         break
             if self._zero3(u) and not u.keep_gathered and (self.reshard_after_forward
                                                           or not torch.is_grad_enabled()):
-                self._release_unit(u)
+                self._release_unit(u, keep_secondary=torch.is_grad_enabled())
             return None
         return hook
 
@@ -425,7 +496,7 @@ class DataParallelEngine:
             ev.record(torch.cuda.current_stream())
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
-                dist.all_gather_into_tensor(u.pflat, u.pshard, group=self.group)
+                self._all_gather_params(u)
                 done = torch.cuda.Event()
                 done.record(self.comm_stream)
             u.ag_event = done
@@ -433,12 +504,41 @@ class DataParallelEngine:
                 torch.cuda.current_stream().wait_event(done)
                 u.ag_event = None
         else:
-            dist.all_gather_into_tensor(u.pflat, u.pshard, group=self.group)
+            self._all_gather_params(u)
         u.gathered = True
 
-    def _release_unit(self, u: _Unit):
+    def _all_gather_params(self, u: _Unit):
+        """Fill u.pflat from the shards (runs on the comm stream when overlapping)."""
+        if u.sec is not None:  # hpZ: re-gather from the intra-node secondary partition
+            dist.all_gather_into_tensor(u.pflat, u.sec, group=self.hpz_group)
+            if self.cuda:
+                u.sec.record_stream(torch.cuda.current_stream())
+            u.sec = None
+            return
+        if not (self.offload_params or self.quantized_weights):
+            dist.all_gather_into_tensor(u.pflat, u.pshard, group=self.group)
+            return
+        a, b = self.shard_range(u)
+        own = u.pflat[a:b]
+        own.copy_(u.pshard, non_blocking=True)  # host -> device when the shard is offloaded
+        if self.quantized_weights:
+            q, sc = quantize_int8(own)
+            qa = torch.empty(u.numel, dtype=torch.int8, device=own.device)
+            sa = torch.empty(u.numel // QBLOCK, dtype=torch.float32, device=own.device)
+            dist.all_gather_into_tensor(qa, q, group=self.group)
+            dist.all_gather_into_tensor(sa, sc, group=self.group)
+            exact = own.clone()
+            dequantize_int8(qa, sa, u.pflat)
+            own.copy_(exact)  # this rank's own slice stays exact
+        else:
+            dist.all_gather_into_tensor(u.pflat, own, group=self.group)
+
+    def _release_unit(self, u: _Unit, keep_secondary: bool = False):
         if not u.gathered:
             return
+        if keep_secondary and self.hpz_group is not None:
+            n = u.numel // self.hpz
+            u.sec = u.pflat[self.hpz_rank * n:(self.hpz_rank + 1) * n].clone()
         if self.cuda:
             u.pflat.record_stream(torch.cuda.current_stream())
             if self.comm_stream is not None:
@@ -468,6 +568,14 @@ class DataParallelEngine:
         stage = self.stage
 
         def op():
+            if stage >= 1 and self.quantized_gradients:
+                # qgZ: all-to-all of int8 chunks, then dequantise + sum into this rank's shard
+                q, sc = quantize_int8(u.gflat)
+                qr, sr = torch.empty_like(q), torch.empty_like(sc)
+                dist.all_to_all_single(qr, q, group=self.group)
+                dist.all_to_all_single(sr, sc, group=self.group)
+                dequant_sum(qr, sr, u.gshard, self.dp, accumulate)
+                return
             src = u.gflat if u.gflat.dtype == self.reduce_dtype else u.gflat.to(self.reduce_dtype)
             if stage >= 1:
                 if accumulate:
@@ -623,6 +731,10 @@ class DataParallelEngine:
     def _param_out(self, u: _Unit) -> torch.Tensor:
         """The bf16 parameter slice the optimizer writes for this rank (shard, or all)."""
         if self._zero3(u):
+            if self.offload_params and not self.offload and self.cuda:
+                # device AdamW: write a device scratch, copied down to the host shard after the update
+                u._pscratch = torch.empty(u.pshard.shape, dtype=u.pshard.dtype, device=self.device)
+                return u._pscratch
             return u.pshard
         a, b = self.shard_range(u)
         return u.pflat[a:b]
@@ -640,6 +752,10 @@ class DataParallelEngine:
                 _adamw_ref(u.master, u.exp_avg, u.exp_avg_sq, g.float() * self._gscale, lr, b1, b2, self.eps,
                            self.weight_decay, self.step_count)
                 pout.copy_(u.master)
+            if getattr(u, "_pscratch", None) is not None:
+                u.pshard.copy_(u._pscratch, non_blocking=True)
+                u._pscratch.record_stream(cur)
+                u._pscratch = None
             done = None
             if self.cuda and self.opt_stream is not None:
                 done = torch.cuda.Event()
@@ -676,14 +792,17 @@ class DataParallelEngine:
             lib().adamw_cpu_(u.master, u.exp_avg, u.exp_avg_sq, g, u.p_host, lr, b1, b2, self.eps,
                              self.weight_decay, self.step_count, scale)
             done = None
+            src = u.p_host if u.p_host is not None else u.master
             if self.cuda:
                 with torch.cuda.stream(self.copy_stream):
-                    pout.copy_(u.p_host if u.p_host is not None else u.master, non_blocking=True)
+                    if pout is not src:  # offloaded params: the host AdamW already wrote the shard
+                        pout.copy_(src, non_blocking=True)
                     done = torch.cuda.Event()
                     done.record(self.copy_stream)
                 self._publish_update(u, self.copy_stream, done)
             else:
-                pout.copy_(u.p_host if u.p_host is not None else u.master)
+                if pout is not src:
+                    pout.copy_(src)
                 self._publish_update(u, None, None)
         for u in self.units:
             if self._zero3(u) and u.gathered:
@@ -715,6 +834,7 @@ class DataParallelEngine:
                     done.record(torch.cuda.current_stream())
         if self._zero3(u):
             u.opt_event = done
+            u.sec = None  # an hpZ secondary copy holds last step's parameters
         else:
             u.ag_event = done
 
@@ -799,6 +919,42 @@ class DataParallelEngine:
                 return False
 
         return _Ctx()
+
+
+QBLOCK = 64  # elements per int8 scale (csrc/quant.hip)
+
+
+def quantize_int8(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Blockwise symmetric int8: (q [n], scale [n / 64]) with scale = absmax / 127 per block."""
+    if x.is_cuda:
+        q = torch.empty(x.numel(), dtype=torch.int8, device=x.device)
+        sc = torch.empty(x.numel() // QBLOCK, dtype=torch.float32, device=x.device)
+        lib().quant_int8_(x.contiguous(), q, sc)
+        return q, sc
+    xb = x.float().reshape(-1, QBLOCK)
+    am = xb.abs().amax(1)
+    inv = torch.where(am > 0, 127.0 / am, torch.zeros_like(am))
+    q = torch.round(xb * inv[:, None]).clamp(-127, 127).to(torch.int8).reshape(-1)
+    return q, am / 127.0
+
+
+def dequantize_int8(q: torch.Tensor, sc: torch.Tensor, out: torch.Tensor):
+    if out.is_cuda:
+        lib().dequant_int8_(q, sc, out)
+    else:
+        out.copy_((q.float().reshape(-1, QBLOCK) * sc[:, None]).reshape(-1))
+
+
+def dequant_sum(q: torch.Tensor, sc: torch.Tensor, out: torch.Tensor, k: int, accumulate: bool):
+    """out (+)= sum over k chunks of the dequantised q (q: [k * n], sc: [k * n / 64])."""
+    if out.is_cuda:
+        lib().dequant_sum_(q, sc, out, k, accumulate)
+        return
+    x = (q.float().reshape(-1, QBLOCK) * sc[:, None]).reshape(k, -1).sum(0)
+    if accumulate:
+        out.add_(x.to(out.dtype))
+    else:
+        out.copy_(x)
 
 
 def _hookable(m: nn.Module) -> bool:

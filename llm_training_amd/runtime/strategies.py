@@ -29,7 +29,21 @@ class Strategy:
     overlap_comm: bool = True
     save_distributed_checkpoint: bool = True
     offload_optimizer: bool = False
+    offload_parameters: bool = False
+    offload_optimizer_device: str = "cpu"
+    nvme_path: str | None = None
+    zero_hpz_partition_size: int = 1
+    zero_quantized_weights: bool = False
+    zero_quantized_gradients: bool = False
     extra: dict = field(default_factory=dict)
+
+    def engine_kwargs(self) -> dict:
+        """Keyword arguments of :class:`DataParallelEngine` this strategy selects."""
+        return {"offload_optimizer": self.offload_optimizer, "offload_params": self.offload_parameters,
+                "offload_device": self.offload_optimizer_device, "nvme_path": self.nvme_path,
+                "hpz_partition_size": self.zero_hpz_partition_size,
+                "quantized_weights": self.zero_quantized_weights,
+                "quantized_gradients": self.zero_quantized_gradients}
 
     @property
     def timeout_minutes(self) -> float:
@@ -67,9 +81,10 @@ class FSDP2Strategy(Strategy):
                          timeout=timeout, reshard_after_forward=bool(reshard_after_forward),
                          save_distributed_checkpoint=save_distributed_checkpoint)
         # FSDP2 OffloadPolicy (CPUOffloadPolicy / {"class_path": ...CPUOffloadPolicy} / True): the fp32
-        # master and Adam moments move to pinned host memory, updated by the native host AdamW; the bf16
-        # parameters and gradients stay in HBM (288 GB holds them for any model that fits the node)
+        # master and Adam moments move to pinned host memory, updated by the native host AdamW, and
+        # (ZeRO-3) the bf16 parameter shards too (CPUOffloadPolicy offloads parameters, fsdp2_strategy.py:58)
         self.offload_optimizer = _wants_offload(offload_policy)
+        self.offload_parameters = self.offload_optimizer and stage >= 3
         _check_kwargs("FSDP2Strategy", kw, FSDP2_PASSIVE)
         self.extra = {"mp_policy": mp_policy, "use_master_weights": use_master_weights, **kw}
 
@@ -78,17 +93,24 @@ class DeepSpeedStrategy(Strategy):
     """ZeRO stage 1/2/3 with DeepSpeed's argument names (stage=2 default, as in the reference)."""
 
     def __init__(self, stage: int = 2, offload_optimizer: bool = False, offload_parameters: bool = False,
-                 exclude_frozen_parameters: bool = True, allgather_bucket_size: float = 2e8,
-                 reduce_bucket_size: float = 2e8, overlap_comm: bool = True, process_group_backend=None,
-                 timeout=datetime.timedelta(minutes=30), **kw):
+                 offload_optimizer_device: str = "cpu", nvme_path: str = "/local_nvme", overlap_comm: bool = True,
+                 process_group_backend=None, timeout=datetime.timedelta(minutes=30), zero_hpz_partition_size: int = 1,
+                 zero_quantized_weights: bool = False, zero_quantized_gradients: bool = False, **kw):
         super().__init__(zero_stage=int(stage), process_group_backend=process_group_backend, timeout=timeout,
                          overlap_comm=overlap_comm)
-        self.offload_optimizer = bool(offload_optimizer)
-        if offload_parameters:
-            logger.warning("DeepSpeedStrategy: offload_parameters is not supported (parameters stay in HBM); "
-                           "offload_optimizer is")
-        self.extra = {"exclude_frozen_parameters": exclude_frozen_parameters,
-                      "allgather_bucket_size": allgather_bucket_size, "reduce_bucket_size": reduce_bucket_size, **kw}
+        if offload_optimizer_device not in ("cpu", "nvme"):
+            raise ValueError(f"offload_optimizer_device must be cpu or nvme, got {offload_optimizer_device!r}")
+        self.offload_optimizer = bool(offload_optimizer) or offload_optimizer_device == "nvme"
+        self.offload_optimizer_device = offload_optimizer_device
+        self.nvme_path = nvme_path
+        if offload_parameters and int(stage) < 3:
+            raise ValueError("DeepSpeedStrategy: offload_parameters needs stage 3 (as in DeepSpeed)")
+        self.offload_parameters = bool(offload_parameters)
+        self.zero_hpz_partition_size = int(zero_hpz_partition_size)
+        self.zero_quantized_weights = bool(zero_quantized_weights)
+        self.zero_quantized_gradients = bool(zero_quantized_gradients)
+        _check_kwargs("DeepSpeedStrategy", kw, DEEPSPEED_PASSIVE)
+        self.extra = dict(kw)
 
 
 # upstream DeepSpeedStrategy / Lightning arguments (deepspeed_strategy.py:17-72) that the engine takes no

@@ -199,8 +199,7 @@ class Trainer:
                                          grad_dtype=self.grad_dtype,
                                          reduce_dtype=getattr(torch, rd) if rd else self.grad_dtype,
                                          reshard_after_forward=st.reshard_after_forward,
-                                         overlap_comm=st.overlap_comm,
-                                         offload_optimizer=getattr(st, "offload_optimizer", False))
+                                         overlap_comm=st.overlap_comm, **st.engine_kwargs())
         self.scheduler = lm.build_lr_scheduler(self.base_lr, self.estimated_stepping_batches())
         if ckpt_path:
             from ..ckpt.checkpoint import load_checkpoint

@@ -39,13 +39,13 @@ def _cfg(**kw):
     return LlamaConfig(**base)
 
 
-def _run(dev, stage, forced, ckpt=False, accum=1, offload=False, steps=3, S=512):
+def _run(dev, stage, forced, ckpt=False, accum=1, offload=False, steps=3, S=512, **eng_kw):
     torch.manual_seed(0)
     cfg = _cfg(enable_gradient_checkpointing=ckpt)
     m = Llama(cfg, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
     m.init_weights(5)
     eng = DataParallelEngine(m, ParallelContext.single(dev), stage, lr=1e-3, force_sharded=forced,
-                             offload_optimizer=offload)
+                             offload_optimizer=offload, **eng_kw)
     lm = CLM({"model": None})
     lm.model = m
     lm.train()
@@ -173,3 +173,26 @@ def test_checkpoint_save_resume_sharded_offload(rccl_group, tmp_path, monkeypatc
     assert b.engine.step_count == 2
     got = step(b, batches[2])
     assert got == want, (got, want)
+
+
+@pytest.mark.parametrize("offload,kw,exact", [
+    (False, {"offload_params": True}, True),
+    (True, {"offload_params": True}, False),
+    (False, {"quantized_weights": True}, True),  # one rank: its own exact slice is the whole unit
+    (False, {"quantized_gradients": True}, False),
+])
+def test_forced_sharded_zero3_offload_and_zeropp(rccl_group, monkeypatch, offload, kw, exact):
+    """Stage 3 with parameter offload (pinned host shards, H2D into the gather buffer on the comm
+    stream), and the int8 ZeRO++ paths (csrc/quant.hip + RCCL all-gather / all-to-all)."""
+    monkeypatch.setenv("LLMT_DETERMINISTIC", "1")
+    dev = rccl_group
+    ref_l, ref_p, _, _ = _run(dev, 0, forced=False)
+    l, p, eng, _ = _run(dev, 3 if "quantized_gradients" not in kw else 2, forced=True, offload=offload, **kw)
+    if kw.get("offload_params"):
+        assert eng.units[1].pshard.device.type == "cpu" and eng.units[1].pshard.is_pinned()
+    if exact:
+        assert l == ref_l, (l, ref_l)
+        assert all(torch.equal(p[k], ref_p[k]) for k in ref_p)
+    else:
+        for a, b in zip(l, ref_l):
+            assert abs(a - b) < 1e-2 * abs(b), (l, ref_l)

@@ -279,3 +279,27 @@ def test_linear_hip_gemm_grads_into_grad_buffer(monkeypatch):
     assert _rel(w.main_grad, sum(dy.float().t() @ x.float() for x, dy in zip(xs, dys))) < 1e-3
     for x, dy in zip(xs, dys):
         assert _rel(x.grad, dy.float() @ w.float()) < 1e-2
+
+
+# ----------------------------------------------------------------------------- int8 blockwise quant (ZeRO++)
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_int8_quant_dequant_matches_torch(dtype):
+    from llm_training_amd.parallel.engine import QBLOCK, dequant_sum, dequantize_int8, quantize_int8
+    torch.manual_seed(0)
+    n = 64 * 1000
+    x = (torch.randn(n, device=DEV) * torch.rand(n // 64, device=DEV).repeat_interleave(64)).to(dtype)
+    q, sc = quantize_int8(x)
+    xb = x.float().reshape(-1, QBLOCK)
+    am = xb.abs().amax(1)
+    assert torch.allclose(sc, am / 127, rtol=1e-6)
+    qr = torch.round(xb * (127 / am)[:, None]).clamp(-127, 127).to(torch.int8).reshape(-1)
+    assert (q.int() - qr.int()).abs().max().item() <= 1  # round-half cases
+    y = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    dequantize_int8(q, sc, y)
+    assert (y.float() - x.float()).abs().max().item() <= (am.max() / 127).item() * 0.51 + 1e-2
+    k = 3
+    qs, ss = zip(*(quantize_int8(x * (j + 1)) for j in range(k)))
+    out = torch.ones(n, device=DEV, dtype=torch.float32)
+    dequant_sum(torch.cat(qs), torch.cat(ss), out, k, True)
+    want = 1 + sum((qq.float().reshape(-1, QBLOCK) * s[:, None]).reshape(-1) for qq, s in zip(qs, ss))
+    assert torch.allclose(out, want, rtol=1e-5, atol=1e-5)
