@@ -91,7 +91,9 @@ def build(verbose: bool = False, debug: bool = False) -> Path:
     if jobs or _stale(LIB, objs):
         tmp = LIB.with_suffix(".so.tmp")
         _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(tmp),
-              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{tlib}"])
+              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip",
+              # torch's own hipBLASLt build (same soname as /opt/rocm's): one copy in the process
+              "-lhipblaslt", f"-Wl,-rpath,{tlib}"])
         os.replace(tmp, LIB)
         if verbose:
             print(f"linked {LIB}")

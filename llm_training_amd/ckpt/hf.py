@@ -11,6 +11,8 @@ from __future__ import annotations
 import json
 import logging
 import os
+import re
+from collections import defaultdict
 from pathlib import Path
 
 import torch
@@ -47,6 +49,57 @@ def load_safetensors_state_dict(path: str | os.PathLike) -> dict[str, torch.Tens
     return torch.load(str(p), map_location="cpu", weights_only=True)
 
 
+_LAYER = re.compile(r"(?:^|\.)layers\.(\d+)\.")
+
+
+def _safetensors_files(p: Path) -> list[Path]:
+    if p.is_file():
+        return [p] if p.suffix == ".safetensors" else []
+    idx = p / "model.safetensors.index.json"
+    if idx.exists():
+        return [p / f for f in sorted(set(json.loads(idx.read_text())["weight_map"].values()))]
+    return sorted(p.glob("*.safetensors"))
+
+
+def iter_weight_groups(path: str | os.PathLike):
+    """Yield the checkpoint's tensors one decoder layer at a time (then everything outside the layers).
+
+    safetensors files are memory-mapped and each group's tensors are materialised only while that group
+    is loaded, so a rank's host memory holds one layer (~0.44 GB for Llama-3-8B) instead of the whole
+    state dict (16 GB), and the ranks of a node share one page-cache copy of the files — the disk is read
+    once per node however many ranks load (reference: rank-0 load + broadcast, lms/base_lm.py:147-191).
+    ``pytorch_model*.bin`` checkpoints (no mmap format) are read whole with ``weights_only=True``.
+    """
+    from safetensors import safe_open
+
+    p = Path(path)
+    files = _safetensors_files(p)
+    if not files:
+        yield load_safetensors_state_dict(p)
+        return
+    handles = {f: safe_open(str(f), framework="pt", device="cpu") for f in files}
+    groups: dict[int, list[tuple[Path, str]]] = defaultdict(list)
+    for f, h in handles.items():
+        for k in h.keys():
+            m = _LAYER.search(k)
+            groups[int(m.group(1)) if m else -1].append((f, k))
+    for gid in sorted(groups, key=lambda g: (g < 0, g)):
+        yield {k: handles[f].get_tensor(k) for f, k in groups[gid]}
+
+
+def stream_load_weights(model, path: str | os.PathLike, convert=None) -> list[str]:
+    """Load a (possibly sharded) checkpoint into ``model`` group by group (TP slicing per group);
+    returns the model keys that no group provided."""
+    own = set(model.state_dict().keys())
+    seen: set[str] = set()
+    for sd in iter_weight_groups(path):
+        full = convert(sd) if convert is not None else sd
+        model.load_full_state_dict(full, strict=False)
+        seen.update(k for k in full if k in own)
+        del sd, full
+    return sorted(own - seen)
+
+
 def load_hf_weights(model, hf_path: str) -> bool:
     """Load a local HF checkpoint dir into ``model`` (TP-sharded as needed). False if not available."""
     p = Path(hf_path)
@@ -54,12 +107,13 @@ def load_hf_weights(model, hf_path: str) -> bool:
         logger.warning("hf_path %s is not a local directory; weights not loaded (random init)", hf_path)
         return False
     try:
-        sd = load_safetensors_state_dict(p)
+        missing = stream_load_weights(model, p, lambda sd: type(model).convert_state_dict_from_hf(sd, model.config))
     except FileNotFoundError:
         logger.warning("no weights under %s; random init", hf_path)
         return False
-    full = type(model).convert_state_dict_from_hf(sd, model.config)
-    model.load_full_state_dict(full, strict=False)
+    if missing:
+        logger.warning("HF checkpoint %s did not provide %d tensors (kept initialised): %s", hf_path,
+                       len(missing), missing[:8])
     logger.info("loaded HF weights from %s", hf_path)
     return True
 

@@ -9,6 +9,8 @@ from __future__ import annotations
 import hashlib
 import json
 import logging
+import tempfile
+from pathlib import Path
 from typing import Any
 
 from .base import BaseDataModule, BaseDataModuleConfig
@@ -23,21 +25,34 @@ class HFBasedDataModuleConfig(BaseDataModuleConfig):
     enable_cache: bool = True
 
 
+_TOK_HASH: dict[int, tuple[object, str]] = {}
+
+
 def tokenizer_fingerprint(tok) -> str:
-    """Stable identity of a tokenizer for ``datasets`` cache fingerprints (vocab + special tokens + template)."""
+    """Stable identity of a tokenizer for ``datasets`` cache fingerprints: the bytes of every file
+    ``save_pretrained`` writes (vocab, merges, special tokens, chat template, padding side), as the
+    reference's hash_tokenizer (hf_based_datamodule.py:89-97). Memoised per tokenizer object."""
     if tok is None:
         return "none"
+    hit = _TOK_HASH.get(id(tok))
+    if hit is not None and hit[0] is tok:
+        return hit[1]
     h = hashlib.sha256()
-    h.update(str(getattr(tok, "name_or_path", "")).encode())
     try:
-        h.update(json.dumps(sorted(tok.get_vocab().items())[:2000]).encode())
-    except Exception:  # noqa: BLE001
-        pass
-    h.update(str(len(tok)).encode())
-    h.update(json.dumps(getattr(tok, "special_tokens_map", {}), sort_keys=True, default=str).encode())
-    h.update(str(getattr(tok, "chat_template", "")).encode())
-    h.update(str(getattr(tok, "padding_side", "")).encode())
-    return h.hexdigest()[:16]
+        with tempfile.TemporaryDirectory() as d:
+            tok.save_pretrained(d)
+            for p in sorted(Path(d).glob("*")):
+                h.update(p.name.encode())
+                h.update(p.read_bytes())
+    except Exception:  # noqa: BLE001 — tokenizers that cannot serialise: hash their full observable state
+        h.update(str(getattr(tok, "name_or_path", "")).encode())
+        h.update(json.dumps(sorted(tok.get_vocab().items())).encode())
+        h.update(json.dumps(getattr(tok, "special_tokens_map", {}), sort_keys=True, default=str).encode())
+        h.update(str(getattr(tok, "chat_template", "")).encode())
+        h.update(str(getattr(tok, "padding_side", "")).encode())
+    digest = h.hexdigest()[:16]
+    _TOK_HASH[id(tok)] = (tok, digest)
+    return digest
 
 
 class HFBasedDataModule(BaseDataModule):
@@ -53,6 +68,12 @@ class HFBasedDataModule(BaseDataModule):
         if isinstance(ds, hfd.Dataset):
             ds = hfd.DatasetDict({"train": ds})
         return ds
+
+    def prepare_data(self):
+        """Warm the ``datasets`` cache: load + pre-process once (the Trainer calls this on one rank per
+        node or per job, then every rank's ``setup`` hits the cache; reference :61-65)."""
+        if self.config.pre_processed_data_path is None and self.config.enable_cache:
+            self.pre_process_data(self.load_data())
 
     def fingerprint(self, name: str, **parts) -> str:
         h = hashlib.sha256(name.encode())

@@ -97,11 +97,11 @@ class BaseLM:
         loaded = False
         if not resuming and self.config.load_weights:
             if path:
-                from ..ckpt.hf import load_safetensors_state_dict
-                sd = load_safetensors_state_dict(path)
-                sd = {k[len("model."):] if k.startswith("model.") and not k.startswith("model.layers") and
-                      k[len("model."):] in model.state_dict() else k: v for k, v in sd.items()}
-                model.load_full_state_dict(sd, strict=False)
+                from ..ckpt.hf import stream_load_weights
+                own = set(model.state_dict().keys())
+                stream_load_weights(model, path, lambda sd: {
+                    k[len("model."):] if k.startswith("model.") and not k.startswith("model.layers") and
+                    k[len("model."):] in own else k: v for k, v in sd.items()})
                 loaded = True
             elif hf_path and getattr(model.config, "load_hf_weights", True):
                 from ..ckpt.hf import load_hf_weights

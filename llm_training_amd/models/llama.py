@@ -280,6 +280,8 @@ class Llama(BaseModel):
             out[k2] = v
         for i in range(L):
             p = f"layers.{i}."
+            if p + "self_attn.q_proj.weight" not in out:
+                continue  # a partial (streamed, one layer at a time) state dict
             q, kk, vv = (out.pop(p + f"self_attn.{n}_proj.weight") for n in ("q", "k", "v"))
             out[p + "self_attn.qkv_proj.weight"] = torch.cat([q, kk, vv], 0)
             if p + "self_attn.q_proj.bias" in out:

@@ -28,15 +28,28 @@ from . import reference as ref
 from .native import lib, use_native
 
 # ----------------------------------------------------------------------------- GEMM dispatch
-# The three GEMMs of a linear layer run on the hand-written gfx950 kernel (csrc/gemm.hip) or on
-# hipBLASLt through torch.matmul. ``LLMT_GEMM`` picks per layout: "hip" (all), "blas" (none) or a comma
-# list of fwd,dgrad,wgrad. Shapes the kernel does not take (K % 32, N % 4, unaligned or strided
-# operands) always go to the library. Default "blas": on the Llama-3-8B step the library GEMMs are
-# faster end to end (profiles/r1_gemm_hip_v1_vs_hipblaslt.jsonl: 1.1-1.2 vs 1.2-1.6 PF/s per projection;
-# bench 16.6k tok/s blas vs 16.4k wgrad-only vs 15.7k all-hip).
-_GEMM_ENV = os.environ.get("LLMT_GEMM", "blas").strip().lower()
-HIP_GEMM_LAYOUTS = ({"fwd", "dgrad", "wgrad"} if _GEMM_ENV == "hip" else
-                    set() if _GEMM_ENV in ("blas", "", "none") else {x.strip() for x in _GEMM_ENV.split(",")})
+# The three GEMMs of a linear layer (fwd x @ W^T, dgrad dy @ W, wgrad dy^T @ x) go to one of:
+#  * "lt"   — hipBLASLt through csrc/blaslt.cpp with the solution measured per problem on the device
+#             (the library's default heuristic is 1.1 PF/s on the forward layout vs 1.3-1.5 backward);
+#  * "blas" — hipBLASLt / rocBLAS through torch.matmul (library default heuristic);
+#  * "hip"  — the hand-written gfx950 kernel (csrc/gemm.hip).
+# ``LLMT_GEMM`` picks one for all layouts, or per layout as "fwd=lt,dgrad=blas,wgrad=hip". Shapes a path
+# cannot take (unaligned / strided operands, K % 32 for "hip") fall back to torch.matmul.
+_GEMM_DEFAULT = "lt"
+
+
+def _gemm_modes() -> dict:
+    env = os.environ.get("LLMT_GEMM", _GEMM_DEFAULT).strip().lower()
+    if "=" not in env:
+        return {k: env for k in ("fwd", "dgrad", "wgrad")}
+    modes = {k: _GEMM_DEFAULT for k in ("fwd", "dgrad", "wgrad")}
+    for part in env.split(","):
+        k, v = part.split("=")
+        modes[k.strip()] = v.strip()
+    return modes
+
+
+GEMM_MODES = _gemm_modes()
 
 
 def _gemm_operand_ok(t: torch.Tensor) -> bool:
@@ -44,62 +57,96 @@ def _gemm_operand_ok(t: torch.Tensor) -> bool:
             and (t.size(0) <= 1 or t.stride(0) % 8 == 0) and t.data_ptr() % 16 == 0)
 
 
-def _hip_gemm_ok(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> bool:
-    if layout not in HIP_GEMM_LAYOUTS or k % 32 or k == 0 or ncols % 4:
-        return False
-    return all(_gemm_operand_ok(t) for t in ts) and use_native(ts[0])
+def _ld(t: torch.Tensor) -> int:
+    return t.stride(0) if t.size(0) > 1 else max(8, (t.size(1) + 7) // 8 * 8)
+
+
+def _path(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> str:
+    mode = GEMM_MODES.get(layout, "blas")
+    if mode == "blas" or not all(_gemm_operand_ok(t) for t in ts) or not use_native(ts[0]):
+        return "blas"
+    if mode == "hip" and (k % 32 or k == 0 or ncols % 4):
+        return "blas"
+    return mode
 
 
 def mm_nt(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """x2 [M, K] @ w[N, K]^T -> [M, N] (forward of a linear layer)."""
-    if _hip_gemm_ok("fwd", x2.shape[1], w.shape[0], x2, w):
-        y = torch.empty(x2.shape[0], w.shape[0], device=x2.device, dtype=x2.dtype)
+    path = _path("fwd", x2.shape[1], w.shape[0], x2, w)
+    if path == "blas":
+        return torch.matmul(x2, w.t())
+    M, K = x2.shape
+    N = w.shape[0]
+    y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
+    if path == "lt":  # column-major: y^T (N x M) = w^T (from K x N) . x^T (K x M)
+        lib().gemm_lt(w, x2, y, True, False, N, M, K, _ld(w), _ld(x2), N, False)
+    else:
         lib().gemm_(x2, w, y, False, False, False)
-        return y
-    return torch.matmul(x2, w.t())
+    return y
 
 
 def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """dy2 [M, N] @ w [N, K] -> [M, K] (input gradient of a linear layer)."""
-    if _hip_gemm_ok("dgrad", dy2.shape[1], w.shape[1], dy2, w) and (out is None or _gemm_operand_ok(out)):
+    path = _path("dgrad", dy2.shape[1], w.shape[1], dy2, w)
+    if out is not None and path != "blas" and not _gemm_operand_ok(out):
+        path = "blas"
+    if path == "blas":
         if out is None:
-            out = torch.empty(dy2.shape[0], w.shape[1], device=dy2.device, dtype=dy2.dtype)
-        lib().gemm_(dy2, w, out, False, True, False)
-        return out
+            return torch.matmul(dy2, w)
+        return torch.matmul(dy2, w, out=out)
+    M, N = dy2.shape
+    K = w.shape[1]
     if out is None:
-        return torch.matmul(dy2, w)
-    return torch.matmul(dy2, w, out=out)
+        out = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
+    if path == "lt":  # column-major: dx^T (K x M) = w^T (K x N) . dy^T (N x M)
+        lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False)
+    else:
+        lib().gemm_(dy2, w, out, False, True, False)
+    return out
+
+
+def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate: bool) -> bool:
+    """out [N, K] (+)= dy[M, N]^T @ x[M, K] on the selected GEMM path; False if only torch can do it."""
+    if not (out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32)):
+        return False
+    path = _path("wgrad", dy.shape[0], x.shape[1], dy, x)
+    M, N = dy.shape
+    K = x.shape[1]
+    if path == "lt":  # column-major: dW^T (K x N) = x^T (K x M) . dy (M x N)
+        lib().gemm_lt(x, dy, out.view(N, K), False, True, K, N, M, _ld(x), _ld(dy), K, accumulate)
+        return True
+    if path == "hip":
+        lib().gemm_(dy, x, out.view(N, K), True, True, accumulate)
+        return True
+    return False
 
 
 def _wgrad_mm(w: torch.Tensor, a_t: torch.Tensor, b: torch.Tensor):
     """dW = a_t @ b. Writes into ``w.main_grad`` if present (returns None), else returns dW.
 
-    ``a_t`` is the transpose view of dy [T, N]; on the HIP path both operands are read token-major
-    (MN-major) straight from dy and x and the output is stored / accumulated in the buffer's dtype.
+    ``a_t`` is the transpose view of dy [T, N]; on the native paths both operands are read token-major
+    straight from dy and x and the output is stored / accumulated in the buffer's dtype.
     """
     mg = getattr(w, "main_grad", None)
     a = a_t.t()
-    if (_hip_gemm_ok("wgrad", a.shape[0], b.shape[1], a, b)
-            and (mg is None or (mg.is_contiguous() and mg.dtype in (torch.bfloat16, torch.float32)))):
-        if mg is None:
-            out = torch.empty(a.shape[1], b.shape[1], device=a.device, dtype=w.dtype)
-            lib().gemm_(a, b, out, True, True, False)
+    if mg is None:
+        out = torch.empty(a.shape[1], b.shape[1], device=a.device, dtype=w.dtype)
+        if wgrad_into(out, a, b, False):
             return out
-        added = bool(getattr(w, "grad_added", False))
-        lib().gemm_(a, b, mg.view(a.shape[1], b.shape[1]), True, True, added)
+        return (a_t @ b).to(w.dtype)
+    added = bool(getattr(w, "grad_added", False))
+    if wgrad_into(mg, a, b, added):
         w.grad_added = True
         return None
-    if mg is None:
-        return (a_t @ b).to(w.dtype)
     mg2 = mg.view(a_t.shape[0], b.shape[1])
     if mg.dtype == a_t.dtype:
-        if getattr(w, "grad_added", False):
+        if added:
             mg2.addmm_(a_t, b)
         else:
             torch.mm(a_t, b, out=mg2)
     else:  # fp32 gradient buffer with bf16 operands
         part = torch.mm(a_t, b, out_dtype=mg.dtype) if a_t.is_cuda else (a_t.float() @ b.float())
-        if getattr(w, "grad_added", False):
+        if added:
             mg2.add_(part)
         else:
             mg2.copy_(part)
@@ -484,7 +531,7 @@ class _FusedLinearCEFn(Function):
             loss_rows[s0:s1] = lr
             if need_h:
                 mm_nn(lg, w, out=dh[s0:s1])
-            if need_w:
+            if need_w and not wgrad_into(dw, lg, h[s0:s1], s0 > 0):
                 if s0 == 0:
                     torch.mm(lg.t(), h[s0:s1], out=dw)
                 else:

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 from torch.autograd import Function
 
-from ..ops.fused import _apply_weight_grad, _wgrad_mm, mm_nn, mm_nt
+from ..ops.fused import _apply_weight_grad, _wgrad_mm, mm_nn, mm_nt, wgrad_into
 from ..ops.native import lib, use_native
 
 
@@ -91,7 +91,7 @@ class _VPFusedCE(Function):
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), None, inv_n, native)
             if need_h:
                 mm_nn(lg, w, out=dh[s0:s1])
-            if need_w:
+            if need_w and not wgrad_into(dw, lg, h[s0:s1], s0 > 0):
                 if s0 == 0:
                     torch.mm(lg.t(), h[s0:s1], out=dw)
                 else:

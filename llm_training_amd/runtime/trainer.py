@@ -183,7 +183,7 @@ class Trainer:
         self.lm, self.datamodule = lm, datamodule
         for cb in self.callbacks:
             _call(cb, "setup", self, lm, "fit")
-        datamodule.prepare_data()
+        self._prepare_data(datamodule, rank, local)
         datamodule.setup("fit")
         resuming = ckpt_path is not None
         lm.configure_model(self.pc, device, self.param_dtype, seed=seed, resuming=resuming)
@@ -210,6 +210,18 @@ class Trainer:
         self.profiler = StepProfiler(out_dir=self.log_dir, rank=self.pc.rank)
         self.watchdog = StallWatchdog(path=os.path.join(self.log_dir, f"stall_rank{self.pc.rank}.txt"))
         self.collectives = collective_debug.maybe_enable_from_env()
+
+    @staticmethod
+    def _prepare_data(datamodule, rank: int, local_rank: int):
+        """Run ``prepare_data`` (download / tokenize into the cache) on one rank — local rank 0 of each
+        node with ``prepare_data_per_node`` (node-local caches), else global rank 0 (shared file system)
+        — while the others wait, so ``num_proc`` workers of one rank fill the cache instead of every
+        rank mapping concurrently into the same files (reference: Lightning's prepare_data contract)."""
+        per_node = bool(getattr(datamodule.config, "prepare_data_per_node", False))
+        if (local_rank if per_node else rank) == 0:
+            datamodule.prepare_data()
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.barrier()
 
     def resolve_last_checkpoint(self) -> str | None:
         """``ckpt_path: last``: newest complete checkpoint under the checkpoint directories (or None)."""

@@ -302,3 +302,43 @@ def test_checkpoint_dp4_zero3_to_dp2_zero2_and_offload(tmp_path):
         assert torch.allclose(lo[0]["sd"][k], v), k
     for u in so[0]["state"]:
         assert torch.equal(lo[1]["state"][u][1], so[1]["state"][u][1])
+
+
+def _prepare_worker(rank, world, data_file, cache_dir, marker_dir):
+    import llm_training_amd.data.pre_training as ptm
+    from llm_training_amd.data.pre_training import PreTrainingDataModule
+    from llm_training_amd.runtime.trainer import Trainer
+    from tests.helpers import toy_tokenizer
+    orig = ptm.pre_process_batch
+
+    def counted(*a, **kw):  # leaves a marker per rank that actually tokenized
+        open(os.path.join(marker_dir, f"rank{rank}_{os.getpid()}"), "a").write("x")
+        return orig(*a, **kw)
+
+    counted.__name__ = orig.__name__
+    ptm.pre_process_batch = counted
+    dm = PreTrainingDataModule({"dataset_kwargs": {"path": "json", "data_files": data_file, "cache_dir": cache_dir},
+                                "tokenizer": toy_tokenizer(), "max_length": 32, "batch_size": 2})
+    Trainer._prepare_data(dm, rank, rank)
+    dm.setup()
+    return {"n": torch.tensor(len(dm.datasets["train"])),
+            "first": torch.tensor(list(dm.datasets["train"][0]["input_ids"]))}
+
+
+def test_prepare_data_runs_on_one_rank_and_others_hit_the_cache(tmp_path):
+    """Trainer._prepare_data: rank 0 tokenizes into the datasets cache, rank 1 only reads it
+    (reference hf_based_datamodule.py:61-65 + Lightning's prepare_data contract)."""
+    import json
+    import random
+    rng = random.Random(0)
+    words = "hello world how are you the a of to and is it in that good bad yes no".split()
+    f = tmp_path / "d.jsonl"
+    f.write_text("\n".join(json.dumps({"text": " ".join(rng.choice(words) for _ in range(rng.randint(3, 30)))})
+                           for _ in range(40)))
+    markers = tmp_path / "markers"
+    markers.mkdir()
+    out = run_gloo(_prepare_worker, 2, (str(f), str(tmp_path / "cache"), str(markers)))
+    ran = sorted(p.name.split("_")[0] for p in markers.iterdir())
+    assert ran == ["rank0"], ran  # one process tokenized: the prepare on rank 0
+    assert int(out[0]["n"]) == int(out[1]["n"]) > 0
+    assert torch.equal(out[0]["first"], out[1]["first"])

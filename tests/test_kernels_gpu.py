@@ -261,9 +261,12 @@ def test_gemm_strided_operands():
     assert cw[:, N:].abs().max().item() == 0
 
 
-def test_linear_hip_gemm_grads_into_grad_buffer(monkeypatch):
+@pytest.mark.parametrize("mode", ["hip", "lt", "blas"])
+def test_linear_gemm_paths_grads_into_grad_buffer(monkeypatch, mode):
+    """Every GEMM path (own kernel, tuned hipBLASLt, torch) through the linear op, with fp32 weight-grad
+    accumulation into the flat gradient buffer across two micro-batches."""
     import llm_training_amd.ops.fused as fused
-    monkeypatch.setattr(fused, "HIP_GEMM_LAYOUTS", {"fwd", "dgrad", "wgrad"})  # the library is the default
+    monkeypatch.setattr(fused, "GEMM_MODES", {"fwd": mode, "dgrad": mode, "wgrad": mode})
     torch.manual_seed(0)
     T, K, N = 320, 256, 384
     w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16().requires_grad_(True)
@@ -303,3 +306,35 @@ def test_int8_quant_dequant_matches_torch(dtype):
     dequant_sum(torch.cat(qs), torch.cat(ss), out, k, True)
     want = 1 + sum((qq.float().reshape(-1, QBLOCK) * s[:, None]).reshape(-1) for qq, s in zip(qs, ss))
     assert torch.allclose(out, want, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("out", ["bf16", "bf16_acc", "fp32_acc"])
+def test_gemm_lt_tuned_layouts(layout, out):
+    """csrc/blaslt.cpp: tuned hipBLASLt solution per problem, all three linear layouts; the tuning pass
+    must not disturb an accumulating output."""
+    from llm_training_amd.ops.fused import mm_nn, mm_nt, wgrad_into
+    torch.manual_seed(0)
+    M, N, K = 1024, 768, 512
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    import llm_training_amd.ops.fused as fused
+    old = dict(fused.GEMM_MODES)
+    fused.GEMM_MODES.update(fwd="lt", dgrad="lt", wgrad="lt")
+    try:
+        if layout == "nt":
+            assert _rel(mm_nt(x, w), x.float() @ w.float().t()) < 1e-2
+        elif layout == "nn":
+            assert _rel(mm_nn(dy, w), dy.float() @ w.float()) < 1e-2
+        else:
+            dt = torch.float32 if out.startswith("fp32") else torch.bfloat16
+            acc = out.endswith("acc")
+            c0 = torch.randn(N, K, device=DEV).to(dt)
+            c = c0.clone()
+            assert wgrad_into(c, dy, x, acc)
+            want = dy.float().t() @ x.float() + (c0.float() if acc else 0)
+            assert _rel(c, want) < (1e-4 if dt == torch.float32 else 1e-2)
+    finally:
+        fused.GEMM_MODES.update(old)
+    assert "_acc" in lib().gemm_lt_export() or layout != "tn" or not out.endswith("acc")

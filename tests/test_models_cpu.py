@@ -206,3 +206,26 @@ def test_activation_checkpointing_matches(granularity):
     assert grads[0].keys() == grads[1].keys()
     for k in grads[0]:
         assert torch.allclose(grads[0][k], grads[1][k], atol=1e-6), k
+
+
+def test_streamed_hf_weight_load_matches_and_is_layer_bounded(tmp_path):
+    """ckpt/hf.py: sharded HF safetensors are read one decoder layer at a time (mmap) and the result
+    equals the full in-memory load."""
+    from llm_training_amd.ckpt.hf import iter_weight_groups, load_hf_weights, save_hf_folder
+    from llm_training_amd.parallel.context import ParallelContext
+    cfg = tiny_llama_cfg(num_hidden_layers=3)
+    src = Llama(cfg, ParallelContext.single(), dtype=torch.float32)
+    src.init_weights(3)
+    full = {k: v.detach().clone() for k, v in src.state_dict().items()}
+    out = save_hf_folder(Llama, cfg, full, str(tmp_path / "hf"), dtype=torch.float32,
+                         hf_config=src.hf_config_dict(), max_shard_bytes=60_000)
+    assert len(list((tmp_path / "hf").glob("*.safetensors"))) > 1  # really sharded
+    groups = list(iter_weight_groups(out))
+    assert len(groups) == cfg.num_hidden_layers + 1
+    for g in groups[:-1]:  # each layer group holds exactly one layer's tensors
+        assert len({k.split(".")[2] for k in g}) == 1
+    dst = Llama(cfg, ParallelContext.single(), dtype=torch.float32)
+    dst.init_weights(4)
+    assert load_hf_weights(dst, out)
+    for k, v in dst.state_dict().items():
+        assert torch.equal(v, full[k]), k
