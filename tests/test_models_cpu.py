@@ -229,3 +229,35 @@ def test_streamed_hf_weight_load_matches_and_is_layer_bounded(tmp_path):
     assert load_hf_weights(dst, out)
     for k, v in dst.state_dict().items():
         assert torch.equal(v, full[k]), k
+
+
+@pytest.mark.parametrize("model_type", ["llama", "qwen2", "mistral"])
+def test_hf_causal_lm_segment_attention_matches_dense_mask(model_type):
+    """HFCausalLM routes attention through the flash op with packed segment ids (kwarg threading through
+    transformers' AttentionInterface); equals the same HF model run with SDPA + a dense block-diagonal
+    causal mask, per packed document."""
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    kw = dict(model_type=model_type, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+              num_attention_heads=4, num_key_value_heads=2, vocab_size=100, max_position_embeddings=64)
+    if model_type == "mistral":
+        kw["sliding_window"] = 6
+    ours = HFCausalLM(HFCausalLMConfig(hf_config=kw))
+    assert ours.uses_hip_attention
+    ours.init_weights(0)
+    dense = HFCausalLM(HFCausalLMConfig(hf_config=kw, attn_implementation="sdpa"))
+    dense.load_state_dict(ours.state_dict())
+    ours.eval()
+    dense.eval()
+    ids = torch.randint(0, 100, (2, 24))
+    seg = torch.tensor([[1] * 10 + [2] * 9 + [3] * 5, [1] * 24])
+    pos = torch.cat([torch.arange(10), torch.arange(9), torch.arange(5)])[None].repeat(2, 1)
+    pos[1] = torch.arange(24)
+    with torch.no_grad():
+        a = ours.hidden_states(ids, pos, seg)
+        if model_type != "mistral":  # the dense packed mask carries no sliding window
+            b = dense.hidden_states(ids, pos, seg)
+            assert torch.allclose(a, b, atol=1e-5), (a - b).abs().max()
+        # every packed document == that document run alone through HF's own mask construction
+        for row, (s0, s1) in [(0, (0, 10)), (0, (10, 19)), (0, (19, 24)), (1, (0, 24))]:
+            c = dense.hidden_states(ids[row:row + 1, s0:s1], torch.arange(s1 - s0)[None], None)
+            assert torch.allclose(a[s0:s1, row:row + 1], c, atol=1e-5), (row, s0, (a[s0:s1, row:row + 1] - c).abs().max())
