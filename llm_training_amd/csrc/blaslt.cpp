@@ -6,7 +6,7 @@
 // (profiles/r2_llama8b_1gpu_forced_zero2_kernel_stats.md). This op asks hipBLASLt for its top
 // candidates for the exact problem, times each on the live operands (random-like training data, not
 // constant fill — constant data makes every kernel look faster through DVFS) writing into a scratch
-// output, and caches the winner per problem key for the process. Winners can be exported / imported
+// output, and caches the winner per problem key for the process (timing is opt-in: LLMT_GEMM_TUNE=1). Winners can be exported / imported
 // as "key -> rank in the heuristic list" lines, which are stable for one library build.
 //
 // Column-major convention (hipBLASLt's): D[m, n] = alpha * op(A)[m, k] * op(B)[k, n] + beta * C.
@@ -19,6 +19,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <fstream>
 #include <map>
 #include <mutex>
@@ -48,7 +49,13 @@ struct State {
   std::map<int, hipblasLtHandle_t> handles;
   std::map<std::string, Choice> cache;
   std::map<std::string, int> preset;  // imported winners: key -> heuristic rank
-  bool tune = true;
+  // Timing the candidates is opt-in (LLMT_GEMM_TUNE=1): on the Llama-3-8B shapes the heuristic's first
+  // choice won every problem (benchmarks/bench_gemm_paths.py), and timing ~15 problems x 24 candidates
+  // costs seconds of start-up.
+  bool tune = [] {
+    const char* e = std::getenv("LLMT_GEMM_TUNE");
+    return e != nullptr && e[0] == '1';
+  }();
 };
 
 State& st() {
