@@ -8,8 +8,8 @@
 One process per GPU (RCCL over xGMI between them). Every step is a full training step of the real
 Llama-3-8B architecture (h 4096, I 14336, 32 layers, 32 q / 8 kv heads, vocab 128256, random init,
 bf16 weights + fp32 master/Adam state): forward, backward, gradient reduction, norm clipping (1.0)
-and the fused AdamW update. Data is synthetic: three packed sequences of S=8192 random tokens per GPU
-per step (micro-batch 3 by default, weak scaling). W untimed warm-up steps, then exactly K timed steps between
+and the fused AdamW update. Data is synthetic: four sequences of S=8192 random tokens per GPU per
+step (micro-batch 4 by default: 260 GiB peak of the 268 GiB HBM at dp=1, weak scaling). W untimed warm-up steps, then exactly K timed steps between
 a barrier + device synchronize on both sides; the reported time is the MAX over ranks. Rank 0
 prints one JSON line.
 
@@ -47,7 +47,7 @@ PHI3_MINI = dict(vocab_size=32064, hidden_size=3072, intermediate_size=8192, num
 
 # workload -> (metric, model name, default seq len, default micro-batch)
 WORKLOADS = {
-    "pt": ("tokens/sec (whole node) Llama-3-8B CLM pre-train", "Llama-3-8B", 8192, 3),
+    "pt": ("tokens/sec (whole node) Llama-3-8B CLM pre-train", "Llama-3-8B", 8192, 4),
     "pt-packed": ("tokens/sec (whole node) Llama-3-8B CLM pre-train, isolated packed documents", "Llama-3-8B",
                   8192, 3),
     "it": ("tokens/sec (whole node) Phi-3-mini instruction tuning, NEFTune + varlen packing", "Phi-3-mini-128k",

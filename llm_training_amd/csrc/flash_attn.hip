@@ -1565,6 +1565,226 @@ __global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
   }
 }
 
+// ============================================================================ forward, D = 128, v3
+// grid: ceil(S/128) * Hq * B blocks (1-D, kv-head-major, heaviest query blocks first), 4 waves x 32
+// queries, two workgroups per CU. Differences from fa_fwd_kernel<128>, each aimed at the exposed LDS
+// latency that capped it near 600 TF/s (its ISA waited on every K read one MFMA ahead):
+//  * K / V tiles arrive by LDS-DMA (no staging registers) into a 2-slot ring of dual-use swizzled
+//    images; the DMA of tile t+1 flies under tile t's compute, one raw barrier per tile.
+//  * all 16 K row fragments of a tile are read in one batch ahead of the 16 S^T MFMAs, and the 32
+//    V^T transposed reads are issued right behind those MFMAs (into the same registers) so they land
+//    while the softmax runs; the P.V MFMAs then run back to back.
+//  * the softmax works on raw scores: row max first, then p = exp2(fma(s, scale*log2e, -m)) — one
+//    FMA + one exp per score instead of mul + sub + exp.
+// single-instruction VALU helpers for MFMA-output math: plain fmaxf makes hipcc canonicalise each MFMA
+// result with an extra v_max first, and adjacent f32 adds get SLP-packed into v_pk_add_f32 (slower
+// than two v_add_f32 beside MFMAs, cdna guide T12 / cycle constants)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vadd(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+__global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
+  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
+  using KI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  const int nqb = (S + 127) / 128;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  const int h = hk * grp + L % grp;
+  L /= grp;
+  const int b = L % a.B;
+  const int mb = nqb - 1 - L / a.B;
+  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
+  const float sl2 = a.scale * kLog2e;
+  int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
+
+  bfv8 qf[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+  // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
+  asm volatile("" : "+v"(sq));
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(qf[kk]));
+  f32v16 ot[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;  // running max in scaled log2 units
+
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
+  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+
+  if (T > 0) {
+    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
+    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
+    const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
+    auto issue = [&](int t) {
+      const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
+      const int n0 = kv_beg + t * BN;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int row0 = 16 * wid + 4 * n, row = row0 + (lane >> 4);
+        const int ch = (lane & 15) ^ KI::swz(row);
+        dma16(krs, slot + row0 * 256, ((n0 + row) * a.k_ss + ch * 8) * 2);
+        dma16(vrs, slot + IMG + row0 * 256, ((n0 + row) * a.v_ss + ch * 8) * 2);
+      }
+      dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
+    };
+    // loop-invariant LDS offsets: K row reads (two 32-key halves) and V^T transposed reads
+    int ro[8], to[4][2];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        to[dt][0] = KI::toff(BN, row, dt * 32 + col);
+        to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
+      }
+    }
+
+    issue(0);
+    wait_vm<0>();
+    ring_barrier();
+    for (int t = 0; t < T; ++t) {
+      const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
+      const int n0 = kv_beg + t * BN;
+      if (t + 1 < T) issue(t + 1);
+      bfv8 fr[16];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) fr[8 * tt + kk] = lds_b128(slot + 8192 * tt + ro[kk]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the batch: one LDS latency per tile, not per MFMA
+      f32v16 st[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) st[tt][i] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) st[tt] = mfma32(fr[8 * tt + kk], qf[kk], st[tt]);
+      }
+      // V^T operands of the P.V product (keys 32tt + 16s2 .., columns 32dt ..) into the same registers
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const char* base = slot + IMG + 256 * (32 * tt + 16 * s2);
+            const s16v4 lo = lds_tr(base + to[dt][0]), hi = lds_tr(base + to[dt][1]);
+            fr[8 * tt + 4 * s2 + dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+      __builtin_amdgcn_sched_barrier(0);
+      // masking only where needed: diagonal (causal), window edge, sequence end, packed segments
+      const bool m_causal = a.causal && (n0 + BN - 1 > qw);
+      const bool m_window = a.window >= 0 && (n0 < qw + 31 - a.window);
+      const bool m_end = n0 + BN > S;
+      const bool m_seg = seg_mask(a, qr, n0, n0 + BN - 1);
+      if (m_causal || m_window || m_end || m_seg || qw + 31 >= S) {
+        const int* Ss = reinterpret_cast<const int*>(slot + 2 * IMG);
+        const int lim = qrow - n0 - 4 * hh, lo = qrow - a.window - n0 - 4 * hh, hi = S - 1 - n0 - 4 * hh;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            int4 sk = make_int4(sq, sq, sq, sq);
+            if (m_seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * tt + 8 * c + 4 * hh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int ko = 32 * tt + 8 * c + j;
+              bool ok = (ko <= hi) && (qrow < S);
+              if (a.causal) ok = ok && (ko <= lim);
+              if (a.window >= 0) ok = ok && (ko >= lo);
+              if (m_seg) ok = ok && ((&sk.x)[j] == sq);
+              if (!ok) st[tt][4 * c + j] = -INFINITY;
+            }
+          }
+      }
+      float mx0 = vmax3(st[0][0], st[0][1], st[0][2]), mx1 = vmax3(st[1][0], st[1][1], st[1][2]);
+#pragma unroll
+      for (int i = 3; i < 15; i += 2) {
+        mx0 = vmax3(mx0, st[0][i], st[0][i + 1]);
+        mx1 = vmax3(mx1, st[1][i], st[1][i + 1]);
+      }
+      float smax = vmax3(mx0, st[0][15], vmax3(mx1, st[1][15], mx1));
+      smax = fmaxf(smax, __shfl_xor(smax, 32, 64)) * sl2;
+      // deferred rescale: keep the running max unless some row grew by more than kThr
+      if (__any(smax > m + kThr)) {
+        const float mnew = fmaxf(m, smax);
+        const float alpha = (mnew == -INFINITY) ? 1.f : fexp2(m - mnew);
+        m = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
+      }
+      const float nm = (m == -INFINITY) ? 0.f : -m;
+      float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          st[tt][i] = fexp2(fmaf(st[tt][i], sl2, nm));
+          st[tt][i + 1] = fexp2(fmaf(st[tt][i + 1], sl2, nm));
+          rs0 = vadd(rs0, st[tt][i]);
+          rs1 = vadd(rs1, st[tt][i + 1]);
+        }
+      l += rs0 + rs1;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bfv8 pb = acc_as_b(st[tt], s2);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) ot[dt] = mfma32(fr[8 * tt + 4 * s2 + dt], pb, ot[dt]);
+        }
+      __builtin_amdgcn_sched_barrier(0);  // the P.V work stays ahead of the wait: the DMA flies under it
+      wait_vm<0>();  // this wave's DMA of tile t + 1
+      ring_barrier();
+    }
+  }
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < S) {
+    bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint2 w;
+        w.x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
+        w.y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
+        *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
+      }
+    if (hh == 0) {
+      const float mu = (m == -INFINITY) ? 0.f : m;
+      a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (mu + __log2f(lt)) * kLn2 : -INFINITY;
+    }
+  }
+}
+
 }  // namespace llmt
 
 using namespace llmt;
@@ -1611,10 +1831,13 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
     case 128: {
       static const int variant = [] {
         const char* e = getenv("LLMT_FA_FWD_VARIANT");
-        return e ? atoi(e) : 0;  // the pipelined fwd128 measured 0.976 ms vs 0.906 ms (B1 S8192 Hq32 Hkv8)
+        // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907, fwd128 1.043
+        return e ? atoi(e) : 2;
       }();
       if (variant == 1)
         fa_fwd128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else if (variant == 2)
+        fa_fwd3_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
     } break;
