@@ -105,7 +105,8 @@ class LlamaAttention(nn.Module):
         def core(t):
             return F_.rope_attention(t, rt["positions"], rt["cos"], rt["sin"], self.nq, self.nkv, causal=True,
                                      segment_ids=rt["segment_ids"], window=rt.get("window", -1), impl=rt["impl"],
-                                     seg_info=rt.get("seg_info"))
+                                     seg_info=rt.get("seg_info"),
+                                     dropout_p=self.cfg.attention_dropout if self.training else 0.0)
 
         if rt.get("selective") and rt["impl"] != "flash" and self.training and torch.is_grad_enabled():
             # selective recompute (reference llama_model.py:506-534): keep only the attention inputs and

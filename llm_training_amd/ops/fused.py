@@ -18,6 +18,7 @@ flash-attn calls of src/llm_training/ops/attention_op.py.
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
 
@@ -440,17 +441,32 @@ def rope_tables_to_full(cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor)
     return torch.cat([c, c], -1), torch.cat([s, s], -1)
 
 
+_DROPOUT_WARNED = [False]
+
+
 def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool = True, segment_ids=None,
-                   window: int = -1, scale: float | None = None, impl: str = "flash", seg_info=None):
+                   window: int = -1, scale: float | None = None, impl: str = "flash", seg_info=None,
+                   dropout_p: float = 0.0):
     """Fused RoPE + attention on the SEQ-MAJOR fused QKV buffer [S, B, n_q + 2 n_kv, D] -> [S, B, n_q, D].
 
     ``cos``/``sin``: fp32 half-width tables [max_pos, D/2]; ``positions``: [B, S] int;
     ``segment_ids``: optional [B, S] (tokens attend only within their contiguous run of equal ids);
-    ``seg_info``: its precomputed :func:`segment_info` (shared across layers).
+    ``seg_info``: its precomputed :func:`segment_info` (shared across layers); ``dropout_p``: attention
+    dropout on the probabilities (reference ``attention_dropout``, llama_model.py:593-621 — FA2 / SDPA
+    ``dropout_p``). The HIP flash kernels have no dropout: a non-zero ``dropout_p`` runs torch SDPA with
+    the same visibility mask (logged once).
     """
     D = qkv.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     win = -1 if window is None else int(window)
+    if dropout_p > 0:
+        if not _DROPOUT_WARNED[0]:
+            _DROPOUT_WARNED[0] = True
+            logging.getLogger("llm_training").warning(
+                "attention_dropout=%g: attention runs torch SDPA with dropout (the HIP flash kernels have none)",
+                dropout_p)
+        return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win,
+                                   scale, "sdpa", dropout_p).transpose(0, 1)
     if use_native(qkv) and impl in ("flash", "flash_attention_2", "hip"):
         qkv = qkv.contiguous()
         pos = positions.t().contiguous().reshape(-1)
@@ -460,7 +476,8 @@ def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool =
                                impl).transpose(0, 1)
 
 
-def _ref_rope_attention(qkv, positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale, impl):
+def _ref_rope_attention(qkv, positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale, impl,
+                        dropout_p: float = 0.0):
     q, k, v = qkv[:, :, :n_q], qkv[:, :, n_q:n_q + n_kv], qkv[:, :, n_q + n_kv:]
     cf, sf = rope_tables_to_full(cos, sin, positions)
     q, k = ref.apply_rope(q, k, cf.to(q.dtype) if q.dtype != torch.float32 else cf,
@@ -471,7 +488,8 @@ def _ref_rope_attention(qkv, positions, cos, sin, n_q, n_kv, causal, segment_ids
         if rep > 1:
             kh = kh.repeat_interleave(rep, dim=1)
             vh = vh.repeat_interleave(rep, dim=1)
-        o = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh, is_causal=causal, scale=scale)
+        o = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh, is_causal=causal, scale=scale,
+                                                             dropout_p=dropout_p)
         return o.transpose(1, 2)
     if impl == "sdpa":
         mask = ref.visibility_mask(q.shape[1], q.device, causal, segment_ids, win, q.shape[0])
@@ -480,7 +498,8 @@ def _ref_rope_attention(qkv, positions, cos, sin, n_q, n_kv, causal, segment_ids
         if rep > 1:
             kh = kh.repeat_interleave(rep, dim=1)
             vh = vh.repeat_interleave(rep, dim=1)
-        o = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask[:, None], scale=scale)
+        o = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask[:, None], scale=scale,
+                                                             dropout_p=dropout_p)
         return o.transpose(1, 2)
     return ref.attention(q, k, v, causal, segment_ids, win, scale)
 

@@ -261,3 +261,23 @@ def test_hf_causal_lm_segment_attention_matches_dense_mask(model_type):
         for row, (s0, s1) in [(0, (0, 10)), (0, (10, 19)), (0, (19, 24)), (1, (0, 24))]:
             c = dense.hidden_states(ids[row:row + 1, s0:s1], torch.arange(s1 - s0)[None], None)
             assert torch.allclose(a[s0:s1, row:row + 1], c, atol=1e-5), (row, s0, (a[s0:s1, row:row + 1] - c).abs().max())
+
+
+def test_attention_dropout_applies_in_training_only():
+    """``attention_dropout`` (reference llama_model.py:593-621) is applied in train mode, not in eval."""
+    from llm_training_amd.parallel.context import ParallelContext
+    ids = torch.randint(0, 128, (2, 16))
+    base = Llama(tiny_llama_cfg(), ParallelContext.single(), dtype=torch.float32)
+    base.init_weights(0)
+    drop = Llama(tiny_llama_cfg(attention_dropout=0.5), ParallelContext.single(), dtype=torch.float32)
+    drop.load_state_dict(base.state_dict())
+    base.eval()
+    drop.eval()
+    with torch.no_grad():
+        assert torch.allclose(base(input_ids=ids).logits, drop(input_ids=ids).logits, atol=1e-6)
+        drop.train()
+        torch.manual_seed(1)
+        a = drop(input_ids=ids).logits
+        torch.manual_seed(2)
+        b = drop(input_ids=ids).logits
+    assert not torch.allclose(a, b)
