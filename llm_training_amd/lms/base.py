@@ -171,7 +171,7 @@ class BaseLM:
         if model.pc.tp:
             from ..parallel.vocab_parallel import vocab_parallel_cross_entropy
             return vocab_parallel_cross_entropy(h, w, labels_sb, model.embed_tokens.v0, model.pc.tp_group,
-                                                ignore_index, chunk)
+                                                ignore_index, chunk, vocab_size=model.embed_tokens.vocab_size)
         return fused_linear_cross_entropy(h, w, labels_sb, ignore_index, chunk)
 
     def token_logps_from_hidden(self, model: BaseModel, h, labels_sb, ignore_index: int):
@@ -181,5 +181,5 @@ class BaseLM:
         if model.pc.tp:
             from ..parallel.vocab_parallel import vocab_parallel_token_logps
             return vocab_parallel_token_logps(h, w, labels_sb, model.embed_tokens.v0, model.pc.tp_group,
-                                              ignore_index, chunk)
+                                              ignore_index, chunk, vocab_size=model.embed_tokens.vocab_size)
         return linear_token_logps(h, w, labels_sb, ignore_index, chunk)

@@ -55,6 +55,8 @@ class LlamaConfig(BaseModelConfig):
     rope_scaling: dict[str, Any] | None = None
     attention_bias: bool = False
     attention_dropout: float = 0.0
+    # TP + SP: overlap the sequence all-gather / reduce-scatter with the projection GEMMs
+    tp_comm_overlap: bool = True
     mlp_bias: bool = False
     enable_gradient_checkpointing: bool = False
     recompute_granularity: Literal["full", "selective"] = "full"
@@ -99,9 +101,15 @@ class LlamaAttention(nn.Module):
         self.qkv_proj = Linear(cfg.hidden_size, (self.nq + 2 * self.nkv) * self.hd, cfg.attention_bias, dtype, device)
         self.o_proj = Linear(self.nq * self.hd, cfg.hidden_size, cfg.attention_bias, dtype, device)
 
-    def forward(self, h, rt):
-        S, B, _ = h.shape
-        qkv = self.qkv_proj(h).view(S, B, self.nq + 2 * self.nkv, self.hd)
+    def forward(self, h, rt, sp_group=None):
+        """h: [S, B, H]; with ``sp_group`` h is this rank's sequence shard and the gather / scatter run
+        inside the projections, overlapped with their GEMMs (tensor_parallel.ag_linear / linear_rs)."""
+        if sp_group is not None:
+            qkv = tpl.ag_linear(h, self.qkv_proj.weight, self.qkv_proj.bias, sp_group)
+        else:
+            qkv = self.qkv_proj(h)
+        S, B = qkv.shape[:2]
+        qkv = qkv.view(S, B, self.nq + 2 * self.nkv, self.hd)
         def core(t):
             return F_.rope_attention(t, rt["positions"], rt["cos"], rt["sin"], self.nq, self.nkv, causal=True,
                                      segment_ids=rt["segment_ids"], window=rt.get("window", -1), impl=rt["impl"],
@@ -114,7 +122,10 @@ class LlamaAttention(nn.Module):
             a = ckpt.checkpoint(core, qkv, use_reentrant=False)
         else:
             a = core(qkv)
-        return self.o_proj(a.reshape(S, B, self.nq * self.hd))
+        a = a.reshape(S, B, self.nq * self.hd)
+        if sp_group is not None:
+            return tpl.linear_rs(a, self.o_proj.weight, self.o_proj.bias, sp_group)
+        return self.o_proj(a)
 
 
 class LlamaMLP(nn.Module):
@@ -124,7 +135,10 @@ class LlamaMLP(nn.Module):
         self.gate_up_proj = Linear(cfg.hidden_size, 2 * self.inter, cfg.mlp_bias, dtype, device)
         self.down_proj = Linear(self.inter, cfg.hidden_size, cfg.mlp_bias, dtype, device)
 
-    def forward(self, h):
+    def forward(self, h, sp_group=None):
+        if sp_group is not None:
+            gu = tpl.ag_linear(h, self.gate_up_proj.weight, self.gate_up_proj.bias, sp_group)
+            return tpl.linear_rs(F_.swiglu(gu), self.down_proj.weight, self.down_proj.bias, sp_group)
         return self.down_proj(F_.swiglu(self.gate_up_proj(h)))
 
 
@@ -137,6 +151,22 @@ class LlamaDecoderLayer(nn.Module):
         self.self_attn = LlamaAttention(cfg, pc, dtype, device)
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, dtype, device)
         self.mlp = LlamaMLP(cfg, pc, dtype, device)
+        self.sp_overlap = bool(getattr(cfg, "tp_comm_overlap", True))
+
+    def attn_block(self, h, rt, g):
+        """Attention on the (sequence-sharded when TP) normed input; returns the sharded output."""
+        if g is None:
+            return self.self_attn(h, rt)
+        if self.sp_overlap:
+            return self.self_attn(h, rt, sp_group=g)
+        return tpl.scatter_seq(self.self_attn(tpl.gather_seq(h, g), rt), g)
+
+    def mlp_block(self, h, g):
+        if g is None:
+            return self.mlp(h)
+        if self.sp_overlap:
+            return self.mlp(h, sp_group=g)
+        return tpl.scatter_seq(self.mlp(tpl.gather_seq(h, g)), g)
 
     def forward(self, x, residual, rt):
         g = self.pc.tp_group if self.pc.tp else None
@@ -144,12 +174,9 @@ class LlamaDecoderLayer(nn.Module):
             h, residual = self.input_layernorm(x), x
         else:
             h, residual = self.input_layernorm(x, residual)
-        a = self.self_attn(tpl.gather_seq(h, g) if g else h, rt)
-        a = tpl.scatter_seq(a, g) if g else a
+        a = self.attn_block(h, rt, g)
         h, residual = self.post_attention_layernorm(a, residual)
-        m = self.mlp(tpl.gather_seq(h, g) if g else h)
-        m = tpl.scatter_seq(m, g) if g else m
-        return m, residual
+        return self.mlp_block(h, g), residual
 
 
 class Llama(BaseModel):

@@ -92,13 +92,11 @@ class Phi3DecoderLayer(LlamaDecoderLayer):
             h, residual = self.input_layernorm(x), x
         else:
             h, residual = self.input_layernorm(x, residual)
-        a = self.self_attn(tpl.gather_seq(h, g) if g else h, rt)
-        a = tpl.scatter_seq(a, g) if g else a
+        a = self.attn_block(h, rt, g)
         if drop > 0:
             a = F.dropout(a, drop, True)
         h, residual = self.post_attention_layernorm(a, residual)
-        m = self.mlp(tpl.gather_seq(h, g) if g else h)
-        m = tpl.scatter_seq(m, g) if g else m
+        m = self.mlp_block(h, g)
         if drop > 0:
             m = F.dropout(m, drop, True)
         return m, residual

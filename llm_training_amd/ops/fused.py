@@ -71,14 +71,16 @@ def _path(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> str:
     return mode
 
 
-def mm_nt(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """x2 [M, K] @ w[N, K]^T -> [M, N] (forward of a linear layer)."""
+def mm_nt(x2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """x2 [M, K] @ w[N, K]^T -> [M, N] (forward of a linear layer); ``out``: contiguous [M, N] target."""
     path = _path("fwd", x2.shape[1], w.shape[0], x2, w)
+    if out is not None and path != "blas" and not _gemm_operand_ok(out):
+        path = "blas"
     if path == "blas":
-        return torch.matmul(x2, w.t())
+        return torch.matmul(x2, w.t()) if out is None else torch.matmul(x2, w.t(), out=out)
     M, K = x2.shape
     N = w.shape[0]
-    y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
+    y = out if out is not None else torch.empty(M, N, device=x2.device, dtype=x2.dtype)
     if path == "lt":  # column-major: y^T (N x M) = w^T (from K x N) . x^T (K x M)
         lib().gemm_lt(w, x2, y, True, False, N, M, K, _ld(w), _ld(x2), N, False)
     else:

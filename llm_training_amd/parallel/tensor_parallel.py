@@ -11,6 +11,16 @@ residual stream sharded on the sequence dim. The reference expresses it with DTe
 - ``scatter_seq``  fwd reduce-scatter(seq) bwd all-gather(seq)       (leave o_proj / down_proj)
 - ``copy_to_tp``   fwd identity            bwd all-reduce            (non-SP input)
 - ``reduce_tp``    fwd all-reduce          bwd identity
+
+With SP the collectives next to the projection GEMMs are overlapped with GEMM work instead of
+running back to back with it (``ag_linear`` / ``linear_rs``, used by the decoder layers):
+
+- ``ag_linear``  (q/k/v, gate/up):  forward all-gathers the sequence shards asynchronously while the GEMM
+  of this rank's own rows runs, then the GEMM of the other ranks' rows; backward starts the
+  reduce-scatter of the input gradient and runs the weight-gradient GEMM under it.
+- ``linear_rs``  (o, down):  backward all-gathers the output gradient asynchronously while the
+  input-gradient GEMM of this rank's own rows runs. (The forward reduce-scatter has no independent
+  GEMM work beside it.)
 """
 from __future__ import annotations
 
@@ -125,6 +135,119 @@ def copy_to_tp(x, group):
 
 def reduce_tp(x, group):
     return _ReduceTP.apply(x, group) if _ws(group) > 1 else x
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    return t.reshape(-1, t.shape[-1])
+
+
+class _AGLinear(Function):
+    """y = all_gather_seq(x) @ W^T (+ b) for seq-major x [S/n, B, K] -> [S, B, N]."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, group):
+        from ..ops.fused import mm_nt
+        n, r = _ws(group), dist.get_rank(group)
+        x = x.contiguous()
+        c = x.shape[0]
+        full = torch.empty((c * n, *x.shape[1:]), dtype=x.dtype, device=x.device)
+        work = dist.all_gather_into_tensor(full, x, group=group, async_op=True)
+        y = torch.empty((c * n, *x.shape[1:-1], w.shape[0]), dtype=x.dtype, device=x.device)
+        y2, f2 = _rows(y), _rows(full)
+        per = y2.shape[0] // n
+        mm_nt(_rows(x), w, out=y2[r * per:(r + 1) * per])  # own rows while the others arrive
+        work.wait()
+        if r > 0:
+            mm_nt(f2[:r * per], w, out=y2[:r * per])
+        if r < n - 1:
+            mm_nt(f2[(r + 1) * per:], w, out=y2[(r + 1) * per:])
+        if b is not None:
+            y += b
+        ctx.save_for_backward(full)
+        ctx.w, ctx.group, ctx.has_bias = w, group, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops.fused import _wgrad_mm, mm_nn
+        (full,) = ctx.saved_tensors
+        w, group = ctx.w, ctx.group
+        n = _ws(group)
+        dy2 = _rows(dy.contiguous())
+        dx = db = dw = None
+        work = None
+        if ctx.needs_input_grad[0]:
+            dx_full = mm_nn(dy2, w).view(*full.shape)
+            dx = torch.empty((full.shape[0] // n, *full.shape[1:]), dtype=full.dtype, device=full.device)
+            work = dist.reduce_scatter_tensor(dx, dx_full, group=group, async_op=True)
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad_mm(w, dy2.t(), _rows(full))  # runs under the reduce-scatter
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        if work is not None:
+            work.wait()
+        return dx, dw, db, None
+
+
+class _LinearRS(Function):
+    """y = reduce_scatter_seq(x @ W^T) (+ b once) for seq-major x [S, B, K] -> [S/n, B, N]."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, group):
+        from ..ops.fused import mm_nt
+        x = x.contiguous()
+        y = mm_nt(_rows(x), w).view(*x.shape[:-1], w.shape[0])
+        y = reduce_scatter_seq(y, group)
+        if b is not None:
+            y = y + b
+        ctx.save_for_backward(x)
+        ctx.w, ctx.group, ctx.has_bias = w, group, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops.fused import _wgrad_mm, mm_nn
+        (x,) = ctx.saved_tensors
+        w, group = ctx.w, ctx.group
+        n, r = _ws(group), dist.get_rank(group)
+        dy = dy.contiguous()
+        full = torch.empty((dy.shape[0] * n, *dy.shape[1:]), dtype=dy.dtype, device=dy.device)
+        work = dist.all_gather_into_tensor(full, dy, group=group, async_op=True)
+        dx = dw = db = None
+        f2 = _rows(full)
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            dx2 = _rows(dx)
+            per = dx2.shape[0] // n
+            mm_nn(_rows(dy), w, out=dx2[r * per:(r + 1) * per])  # own rows while the others arrive
+            work.wait()
+            if r > 0:
+                mm_nn(f2[:r * per], w, out=dx2[:r * per])
+            if r < n - 1:
+                mm_nn(f2[(r + 1) * per:], w, out=dx2[(r + 1) * per:])
+        else:
+            work.wait()
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad_mm(w, f2.t(), _rows(x))
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = _rows(dy).sum(0)
+        return dx, dw, db, None
+
+
+def ag_linear(x, w, b, group):
+    """Column-parallel projection of the sequence-gathered input, gather overlapped with the GEMM."""
+    if _ws(group) == 1:
+        from ..ops.fused import linear
+        return linear(x, w, b)
+    return _AGLinear.apply(x, w, b, group)
+
+
+def linear_rs(x, w, b, group):
+    """Row-parallel projection reduce-scattered over the sequence, backward gather overlapped."""
+    if _ws(group) == 1:
+        from ..ops.fused import linear
+        return linear(x, w, b)
+    return _LinearRS.apply(x, w, b, group)
 
 
 def shard_rows(w: torch.Tensor, rank: int, n: int) -> torch.Tensor:

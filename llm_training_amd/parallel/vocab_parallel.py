@@ -9,6 +9,10 @@ HIP CE kernel produces the LOCAL log-sum-exp and target logit per row, ONE all-g
 [tp, N] lse rows and ONE all-reduce of the target logits (N fp32 each) combine them, and a second
 kernel pass writes the local dlogits in place. dh is returned as a per-rank partial: the
 sequence-gather that produced h reduce-scatters (sums) it on the way back.
+
+When the vocabulary does not divide by the TP degree the last shard carries zero padding rows
+(``ceil(V / tp)`` rows per rank); only the first ``n_valid`` rows of a shard are multiplied, so the
+padding never enters the softmax normaliser and its gradient rows stay zero.
 """
 from __future__ import annotations
 
@@ -65,9 +69,10 @@ class _VPFusedCE(Function):
     and dW contribution immediately (one extra GEMM instead of O(N * V/tp) saved logits)."""
 
     @staticmethod
-    def forward(ctx, h, w, labels, v0, ignore_index, group, chunk):
+    def forward(ctx, h, w_full, labels, v0, ignore_index, group, chunk, n_valid):
         native = use_native(h)
         N = h.shape[0]
+        w = w_full[:n_valid]
         inv_n = (1.0 / (labels != ignore_index).sum().clamp(min=1).float()).reshape(1)
         lses, tgts = [], []
         for s0 in range(0, N, chunk):
@@ -84,7 +89,10 @@ class _VPFusedCE(Function):
         loss = ((lse - tgt) * valid).sum() * inv_n[0]
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dh = torch.empty_like(h) if need_h else None
-        dw = torch.empty(w.shape, device=w.device, dtype=w.dtype) if need_w else None
+        dw_full = torch.empty(w_full.shape, device=w.device, dtype=w.dtype) if need_w else None
+        dw = dw_full[:n_valid] if need_w else None
+        if need_w and n_valid < w_full.shape[0]:
+            dw_full[n_valid:].zero_()
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
@@ -97,9 +105,9 @@ class _VPFusedCE(Function):
                 else:
                     dw.addmm_(lg.t(), h[s0:s1])
             del lg
-        ctx.save_for_backward(*(t for t in (dh, dw) if t is not None))
+        ctx.save_for_backward(*(t for t in (dh, dw_full) if t is not None))
         ctx.has = (need_h, need_w)
-        ctx.w = w
+        ctx.w = w_full
         return loss
 
     @staticmethod
@@ -111,14 +119,15 @@ class _VPFusedCE(Function):
         if dh is not None:
             dh = dh * g.to(dh.dtype)
         dwr = _apply_weight_grad(ctx.w, dw, g) if dw is not None else None
-        return dh, dwr, None, None, None, None, None
+        return dh, dwr, None, None, None, None, None, None
 
 
 class _VPLogps(Function):
     @staticmethod
-    def forward(ctx, h, w, labels, v0, ignore_index, group, chunk):
+    def forward(ctx, h, w_full, labels, v0, ignore_index, group, chunk, n_valid):
         native = use_native(h)
         N = h.shape[0]
+        w = w_full[:n_valid]
         lses, tgts = [], []
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
@@ -131,40 +140,49 @@ class _VPLogps(Function):
         dist.all_reduce(tgt, group=group)
         valid = labels != ignore_index
         ctx.save_for_backward(h, labels, lse)
-        ctx.w = w
-        ctx.cfg = (v0, ignore_index, chunk)
+        ctx.w = w_full
+        ctx.cfg = (v0, ignore_index, chunk, n_valid)
         return (tgt - lse) * valid
 
     @staticmethod
     def backward(ctx, g):
         h, labels, lse = ctx.saved_tensors
-        w = ctx.w
-        v0, ignore_index, chunk = ctx.cfg
+        w_full = ctx.w
+        v0, ignore_index, chunk, n_valid = ctx.cfg
+        w = w_full[:n_valid]
         native = use_native(h)
         N = h.shape[0]
         dh = torch.empty_like(h)
         coef = (-g).float().contiguous()
-        dw = None
+        dw = torch.zeros(w_full.shape, device=w.device, dtype=torch.float32)
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), coef[s0:s1], None, native)
             mm_nn(lg, w, out=dh[s0:s1])
-            r = _wgrad_mm(w, lg.t(), h[s0:s1])
-            if r is not None:
-                dw = r if dw is None else dw + r
-        return dh, dw, None, None, None, None, None
+            dw[:n_valid].addmm_(lg.t().float(), h[s0:s1].float()) if not lg.is_cuda else \
+                dw[:n_valid].add_(torch.mm(lg.t(), h[s0:s1], out_dtype=torch.float32))
+        one = torch.ones((), device=dw.device, dtype=torch.float32)
+        return dh, _apply_weight_grad(w_full, dw, one), None, None, None, None, None, None
 
 
-def vocab_parallel_cross_entropy(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192):
+def _n_valid(w_local, vocab_start, vocab_size):
+    n = w_local.shape[0]
+    return n if vocab_size is None else max(0, min(n, int(vocab_size) - int(vocab_start)))
+
+
+def vocab_parallel_cross_entropy(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192,
+                                 vocab_size: int | None = None):
+    """``vocab_size``: the real vocabulary (rows of w_local past it are padding)."""
     h = h.reshape(-1, h.shape[-1]).contiguous()
     return _VPFusedCE.apply(h, w_local, labels.reshape(-1).contiguous(), int(vocab_start), ignore_index, group,
-                            chunk_size)
+                            chunk_size, _n_valid(w_local, vocab_start, vocab_size))
 
 
-def vocab_parallel_token_logps(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192):
+def vocab_parallel_token_logps(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192,
+                               vocab_size: int | None = None):
     shape = labels.shape
     h = h.reshape(-1, h.shape[-1]).contiguous()
     out = _VPLogps.apply(h, w_local, labels.reshape(-1).contiguous(), int(vocab_start), ignore_index, group,
-                         chunk_size)
+                         chunk_size, _n_valid(w_local, vocab_start, vocab_size))
     return out.view(shape)

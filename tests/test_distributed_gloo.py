@@ -199,15 +199,24 @@ def test_stage2_gradient_memory_is_sharded():
     assert o1["mem"]["persistent"] > 3 * o2["mem"]["persistent"] - 4 * o2["other"] * el
 
 
-@pytest.mark.parametrize("world,tp", [(2, 2), (4, 2)])
-def test_tensor_sequence_parallel_matches_single_process(world, tp):
-    cfg_kw = dict(vocab_size=130)  # not divisible by tp: exercises vocab padding of the last shard
+@pytest.mark.parametrize("world,tp,overlap", [(2, 2, True), (4, 2, True), (2, 2, False), (4, 4, True), (4, 4, False)])
+def test_tensor_sequence_parallel_matches_single_process(world, tp, overlap):
+    """TP x DP (+SP) == one process; ``overlap`` = gather / reduce-scatter fused into the projections
+    (tensor_parallel.ag_linear / linear_rs) or the plain collectives around them."""
+    cfg_kw = dict(vocab_size=130, tp_comm_overlap=overlap)  # 130 % tp != 0: vocab padding of the last shard
+    if tp == 4:
+        cfg_kw.update(num_attention_heads=4, num_key_value_heads=4)
     gb = _batches(130, STEPS, B=world // tp * 2)
     full0, ref, ref_losses = _single_reference(cfg_kw, gb)
     out = run_gloo(_tp_worker, world, (tp, cfg_kw, full0, gb))
+    # AdamW (lr 1e-2) turns fp32 summation-order noise on near-zero gradients into ~1e-4 parameter
+    # differences on a few elements at tp 4; the losses agree to 1e-6
+    atol = 5e-5 if tp == 2 else 5e-4
     for r in range(world):
+        if world == tp:  # (with dp > 1 each rank reports its local batch's loss)
+            assert max(abs(a - b) for a, b in zip(out[r]["losses"], ref_losses)) < 1e-5
         for k, v in ref.items():
-            assert torch.allclose(out[r]["params"][k], v, atol=5e-5, rtol=1e-4), (r, k)
+            assert torch.allclose(out[r]["params"][k], v, atol=atol, rtol=1e-4), (r, k)
 
 
 def _vp_worker(rank, world, h, w, labels):
