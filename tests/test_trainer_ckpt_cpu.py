@@ -116,3 +116,81 @@ def test_dpo_resume_rebuilds_reference_from_pretrained(tmp_path):
         refs.append({k: v.clone() for k, v in lm.ref_model.state_dict().items()})
     for k, v in src.model.state_dict().items():
         assert torch.equal(refs[0][k], v) and torch.equal(refs[1][k], v), k
+
+
+def _reference_style_state(seed=0):
+    """A tiny Llama's weights under the reference LightningModule's names (``model.`` + HF-style module
+    names, lm_head inside the model), plus the YAML config that describes it."""
+    from collections import OrderedDict
+
+    from llm_training_amd.models.llama import Llama, LlamaConfig
+    from llm_training_amd.parallel.context import ParallelContext
+    mc = {"vocab_size": 96, "hidden_size": 32, "intermediate_size": 64, "num_hidden_layers": 2,
+          "num_attention_heads": 4, "num_key_value_heads": 2}
+    m = Llama(LlamaConfig(**mc), ParallelContext.single(), dtype=torch.float32)
+    m.init_weights(seed)
+    hf = Llama.convert_state_dict_to_hf({k: v.detach().clone() for k, v in m.state_dict().items()}, m.config)
+    lm_keys = OrderedDict(("model." + (k[len("model."):] if k.startswith("model.") else k), v) for k, v in hf.items())
+    cfg = {"trainer": {"precision": "32-true"},
+           "model": {"class_path": "llm_training.lms.CLM",
+                     "init_args": {"config": {"model": {"model_class": "llm_training.models.Llama",
+                                                        "model_config": mc}}}}}
+    return hf, lm_keys, cfg
+
+
+def _write_deepspeed(d, lm_keys, stage, world):
+    """Synthetic DeepSpeed ZeRO checkpoint with DeepSpeed's on-disk layout (param_shapes + per-rank flat
+    fp32 partitions), parameter names as Lightning's DeepSpeed wrapper records them."""
+    from collections import OrderedDict
+    names = ["_forward_module." + k for k in lm_keys]
+    tensors = [v.float() for v in lm_keys.values()]
+    shapes = OrderedDict((n, t.shape) for n, t in zip(names, tensors))
+    tag = d / "checkpoint"
+    tag.mkdir(parents=True)
+    (d / "latest").write_text("checkpoint")
+    torch.save({"module": {}, "buffer_names": [], "param_shapes": [shapes], "ds_version": "0.14.0"},
+               tag / "mp_rank_00_model_states.pt")
+    if stage <= 2:
+        flat = torch.cat([t.reshape(-1) for t in tensors])
+        align = 2 * world
+        flat = torch.cat([flat, flat.new_zeros((-flat.numel()) % align)])
+        parts = flat.chunk(world)
+        key = "single_partition_of_fp32_groups"
+    else:
+        per_rank = [[] for _ in range(world)]
+        for t in tensors:
+            f = t.reshape(-1)
+            f = torch.cat([f, f.new_zeros((-f.numel()) % world)])
+            for r, c in enumerate(f.chunk(world)):
+                per_rank[r].append(c)
+        parts = [torch.cat(p) for p in per_rank]
+        key = "fp32_flat_groups"
+    for r in range(world):
+        torch.save({"optimizer_state_dict": {"zero_stage": stage, "partition_count": world, key: [parts[r].clone()]}},
+                   tag / f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt")
+
+
+@pytest.mark.parametrize("fmt", ["zero2_w2", "zero3_w3", "dcp", "plain_pt"])
+def test_convert_to_hf_from_reference_checkpoints(tmp_path, fmt):
+    """convert-to-hf on checkpoints in the reference framework's formats (DeepSpeed ZeRO-2/3 directories,
+    FSDP2 distributed checkpoints, plain Lightning state dicts): the HF export equals the weights."""
+    import yaml
+    from safetensors.torch import load_file
+
+    from llm_training_amd.tools.convert_to_hf import convert
+    hf, lm_keys, cfg = _reference_style_state()
+    (tmp_path / "cfg.yaml").write_text(yaml.safe_dump(cfg))
+    ck = tmp_path / "ck"
+    if fmt.startswith("zero"):
+        _write_deepspeed(ck, lm_keys, int(fmt[4]), int(fmt[-1]))
+    elif fmt == "dcp":
+        import torch.distributed.checkpoint as dcp
+        dcp.save({"state_dict." + k: v for k, v in lm_keys.items()}, checkpoint_id=str(ck), no_dist=True)
+    else:
+        ck = tmp_path / "ck.pt"
+        torch.save({"state_dict": dict(lm_keys), "global_step": 3}, ck)
+    out = convert(str(ck), str(tmp_path / "hf"), config_path=str(tmp_path / "cfg.yaml"), dtype="float32")
+    got = load_file(os.path.join(out, "model.safetensors"))
+    assert set(got) == set(hf)
+    for k, v in hf.items():
+        assert torch.equal(got[k], v.float()), k
