@@ -19,6 +19,7 @@ Other BASELINE.json configs (``--workload``; same JSON schema, their own metric 
              4096 tokens with segment ids (no cross-contamination), loss on ~half the tokens
   dpo / orpo Llama-3-8B preference tuning: chosen + rejected sequences of 4096 tokens each per
              micro-batch (DPO adds the frozen reference model's forward)
+  gpt2-cpu   GPT-2 small CLM on the CPU, one process (plumbing; config #1, no GPU needed)
 TP / SP: ``--tp 2`` (the driver's scaling runs use the default data-parallel layout).
 """
 from __future__ import annotations
@@ -54,7 +55,57 @@ WORKLOADS = {
            4096, 8),
     "dpo": ("tokens/sec (whole node) Llama-3-8B DPO preference tuning", "Llama-3-8B", 4096, 2),
     "orpo": ("tokens/sec (whole node) Llama-3-8B ORPO preference tuning", "Llama-3-8B", 4096, 2),
+    "gpt2-cpu": ("tokens/sec GPT-2 small CLM pre-train on CPU (plumbing)", "GPT-2-small", 1024, 2),
 }
+# GPT-2 small (124 M) through HFCausalLM: BASELINE.json config #1, a CPU plumbing run
+GPT2_SMALL = dict(model_type="gpt2", n_layer=12, n_head=12, n_embd=768, vocab_size=50257, n_positions=1024)
+
+
+def bench_gpt2_cpu(args):
+    """One process, no GPU: the whole stack (HF model wrapper, fused-loss CLM head, flat-buffer engine
+    with AdamW, clipping) on the CPU torch reference ops. Not a performance number."""
+    from llm_training_amd.lms.clm import CLM
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+    metric, model_name, S_def, mb_def = WORKLOADS["gpt2-cpu"]
+    S, B = args.seq or S_def, args.micro_batch or mb_def
+    torch.manual_seed(1234)
+    model = HFCausalLM(HFCausalLMConfig(hf_config=dict(GPT2_SMALL), loss_chunk_size=args.loss_chunk))
+    model.init_weights(1234)
+    engine = DataParallelEngine(model, ParallelContext.single(), 0, lr=3e-4, weight_decay=0.1)
+    lm = CLM({"model": None})
+    lm.model = model
+    lm.train()
+    g = torch.Generator().manual_seed(1000)
+    batches = [torch.randint(0, GPT2_SMALL["vocab_size"], (B, S), generator=g) for _ in range(args.warmup + args.steps)]
+
+    def step(ids):
+        engine.begin_step(1)
+        engine.zero_grad()
+        engine.begin_micro(0)
+        loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+        loss.backward()
+        engine.finish_backward()
+        engine.clip_and_scale(1.0)
+        engine.step(3e-4)
+        return loss
+
+    for i in range(args.warmup):
+        step(batches[i])
+    t0 = time.perf_counter()
+    losses = [float(step(batches[args.warmup + i]).detach()) for i in range(args.steps)]
+    el = time.perf_counter() - t0
+    tps = B * S * args.steps / el
+    print(json.dumps({
+        "metric": metric, "value": round(tps, 2), "unit": "tokens/s", "n_gpus": 0, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1000, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (random tokens, random-init weights)",
+        "config": {"model": model_name, "global_batch": B, "seq_len": S, "parallelism": "cpu-1proc",
+                   "zero_stage": 0, "optimizer": "AdamW fp32 (torch reference ops)", "grad_clip": 1.0,
+                   "workload": "gpt2-cpu", "torch_threads": torch.get_num_threads()},
+        "final_loss": round(losses[-1], 4), "losses": [round(x, 4) for x in losses]}), flush=True)
 
 
 def flops_per_token(cfg: dict, S: int, attn_frac: float = 1.0) -> float:
@@ -95,6 +146,9 @@ def main():
     ap.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
                     help="hipBLASLt solution selection (default: shipped TunableOp results)")
     args = ap.parse_args()
+    if args.workload == "gpt2-cpu":
+        bench_gpt2_cpu(args)
+        return
 
     from llm_training_amd.ops.native import lib
     from llm_training_amd.parallel.context import ParallelContext, init_distributed
