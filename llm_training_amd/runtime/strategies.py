@@ -35,6 +35,7 @@ class Strategy:
     zero_hpz_partition_size: int = 1
     zero_quantized_weights: bool = False
     zero_quantized_gradients: bool = False
+    param_dtype: str | None = None  # FSDP2 MixedPrecisionPolicy.param_dtype (overrides the precision's)
     extra: dict = field(default_factory=dict)
 
     def engine_kwargs(self) -> dict:
@@ -72,6 +73,15 @@ class FSDP2Strategy(Strategy):
                  process_group_backend=None, timeout=datetime.timedelta(minutes=30), reshard_after_forward=True,
                  mp_policy=None, offload_policy=None, use_master_weights=True, zero_stage: int | None = None, **kw):
         stage = 3 if zero_stage is None else int(zero_stage)
+        hpz = 1
+        if not isinstance(reshard_after_forward, bool):
+            # FSDP2: an int is the world size to reshard to after forward (a non-trivial divisor of the
+            # shard group) = a secondary partition over that many ranks, kept for the backward re-gather:
+            # the engine's hpZ partition (ZeRO++), sized to one node's xGMI-connected GPUs
+            hpz = int(reshard_after_forward)
+            if hpz < 1:
+                raise ValueError(f"reshard_after_forward must be a bool or a positive int, got {reshard_after_forward!r}")
+            reshard_after_forward = True
         if zero_stage is None and reshard_after_forward is False:
             # reference TP examples set reshard_after_forward=false: params stay gathered across the
             # step; with 288 GB of HBM that is exactly ZeRO-2 (sharded grads + optimizer state)
@@ -85,6 +95,11 @@ class FSDP2Strategy(Strategy):
         # (ZeRO-3) the bf16 parameter shards too (CPUOffloadPolicy offloads parameters, fsdp2_strategy.py:58)
         self.offload_optimizer = _wants_offload(offload_policy)
         self.offload_parameters = self.offload_optimizer and stage >= 3
+        self.zero_hpz_partition_size = hpz
+        # FSDP2 MixedPrecisionPolicy (object, dict or {class_path, init_args}): param_dtype = the dtype
+        # parameters are gathered / computed in, reduce_dtype = the gradient reduce-scatter dtype
+        pd, rd = _mp_policy_dtypes(mp_policy)
+        self.param_dtype, self.grad_reduce_dtype = pd, rd
         _check_kwargs("FSDP2Strategy", kw, FSDP2_PASSIVE)
         self.extra = {"mp_policy": mp_policy, "use_master_weights": use_master_weights, **kw}
 
@@ -128,7 +143,38 @@ DEEPSPEED_PASSIVE = {
     "raise_error_at_min_scale", "zero3_leaf_modules", "stage3_max_live_parameters", "stage3_max_reuse_distance",
     "stage3_prefetch_bucket_size", "stage3_param_persistence_threshold"}
 FSDP2_PASSIVE = {"accelerator", "parallel_devices", "cluster_environment", "checkpoint_io", "precision_plugin",
-                 "precision", "mp_policy", "use_master_weights"}
+                 "precision", "use_master_weights"}
+
+
+def _dtype_name(d) -> str | None:
+    if d is None:
+        return None
+    import torch
+    if isinstance(d, torch.dtype):
+        return str(d).replace("torch.", "")
+    name = str(d).replace("torch.", "")
+    name = {"bf16": "bfloat16", "fp32": "float32", "fp16": "float16", "half": "float16", "float": "float32"}.get(
+        name, name)
+    if not isinstance(getattr(torch, name, None), torch.dtype):
+        raise ValueError(f"not a dtype: {d!r}")
+    return name
+
+
+def _mp_policy_dtypes(mp) -> tuple[str | None, str | None]:
+    """(param_dtype, reduce_dtype) names of an FSDP2 MixedPrecisionPolicy given as the torch object, a
+    plain dict or a {class_path, init_args} dict; output_dtype / cast_forward_inputs have no separate
+    meaning here (activations are in the parameter dtype)."""
+    if mp is None:
+        return None, None
+    if isinstance(mp, dict):
+        args = mp.get("init_args", mp) if "class_path" in mp else mp
+        pd, rd = args.get("param_dtype"), args.get("reduce_dtype")
+    else:
+        pd, rd = getattr(mp, "param_dtype", None), getattr(mp, "reduce_dtype", None)
+    pd, rd = _dtype_name(pd), _dtype_name(rd)
+    if pd is not None and pd not in ("bfloat16", "float32"):
+        raise ValueError(f"mp_policy.param_dtype {pd}: the MI355X kernels run bf16 (or fp32 via torch ops)")
+    return pd, rd
 
 
 def _check_kwargs(cls_name: str, kw: dict, allowed: set):

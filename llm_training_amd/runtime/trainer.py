@@ -159,10 +159,14 @@ class Trainer:
 
     @property
     def param_dtype(self):
-        return PRECISIONS[self.precision][0]
+        pd = getattr(self.strategy, "param_dtype", None)  # FSDP2 mp_policy.param_dtype wins
+        return getattr(torch, pd) if pd else PRECISIONS[self.precision][0]
 
     @property
     def grad_dtype(self):
+        pd = getattr(self.strategy, "param_dtype", None)
+        if pd and PRECISIONS[self.precision][0] != getattr(torch, pd):
+            return None  # gradients in the parameter dtype (reduce dtype from mp_policy.reduce_dtype)
         return PRECISIONS[self.precision][1]
 
     # ------------------------------------------------------------------ setup

@@ -87,3 +87,26 @@ data:
     assert main(["fit", "--config", str(cfg)]) == 0
     assert os.path.exists(tmp_path / "logs" / "t" / "metrics.csv")
     assert os.path.exists(tmp_path / "logs" / "t" / "config.yaml")
+
+
+def test_fsdp2_mp_policy_and_int_reshard_map_to_the_engine():
+    """FSDP2Strategy(mp_policy=MixedPrecisionPolicy(...), reshard_after_forward=<int>) (reference
+    fsdp2_strategy.py:56-58,94-99): param/reduce dtypes reach the engine; an int reshard size becomes the
+    engine's secondary (hpZ) partition."""
+    import torch
+    from torch.distributed.fsdp import MixedPrecisionPolicy
+
+    from llm_training_amd.runtime.strategies import FSDP2Strategy
+    from llm_training_amd.runtime.trainer import Trainer
+    s = FSDP2Strategy(mp_policy=MixedPrecisionPolicy(param_dtype=torch.bfloat16, reduce_dtype=torch.float32),
+                      reshard_after_forward=4)
+    assert (s.param_dtype, s.grad_reduce_dtype, s.zero_hpz_partition_size, s.zero_stage) == \
+        ("bfloat16", "float32", 4, 3)
+    assert s.engine_kwargs()["hpz_partition_size"] == 4
+    s2 = FSDP2Strategy(mp_policy={"class_path": "torch.distributed.fsdp.MixedPrecisionPolicy",
+                                  "init_args": {"param_dtype": "bf16", "reduce_dtype": "float32"}})
+    assert (s2.param_dtype, s2.grad_reduce_dtype, s2.zero_hpz_partition_size) == ("bfloat16", "float32", 1)
+    t = Trainer(strategy=s2, precision="32-true", max_steps=1)
+    assert t.param_dtype == torch.bfloat16 and t.grad_dtype is None
+    with pytest.raises(ValueError):
+        FSDP2Strategy(mp_policy={"param_dtype": "float16"})

@@ -196,3 +196,50 @@ def test_forced_sharded_zero3_offload_and_zeropp(rccl_group, monkeypatch, offloa
     else:
         for a, b in zip(l, ref_l):
             assert abs(a - b) < 1e-2 * abs(b), (l, ref_l)
+
+
+@pytest.mark.parametrize("stage,forced,packed", [(0, False, False), (2, True, False), (3, True, True)])
+def test_training_step_has_no_host_sync(rccl_group, stage, forced, packed):
+    """a steady-state training step (forward, fused loss, backward, reduce-scatter /
+    all-gather, clipping, fused AdamW) never blocks the host on the GPU. torch's sync debug mode turns
+    any implicit synchronisation (a D2H copy, .item(), a blocking allocator retry, nonzero) into an
+    error; the batch (incl. packed segment ids and the collator's ``attention_mask_trivial`` flag) is
+    built before the window, as the data loader does."""
+    dev = rccl_group
+    torch.manual_seed(0)
+    cfg = _cfg()
+    m = Llama(cfg, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
+    m.init_weights(5)
+    eng = DataParallelEngine(m, ParallelContext.single(dev), stage, lr=1e-3, force_sharded=forced)
+    lm = CLM({"model": None})
+    lm.model = m
+    lm.train()
+    S = 512
+    ids = torch.randint(0, cfg.vocab_size, (2, S), device=dev)
+    batch = {"input_ids": ids, "labels": ids}
+    if packed:
+        seg = torch.repeat_interleave(torch.tensor([1, 2, 3]), torch.tensor([200, 100, 212]))
+        batch.update(attention_mask=seg.expand(2, S).to(dev), attention_mask_trivial=False,
+                     position_ids=torch.cat([torch.arange(200), torch.arange(100), torch.arange(212)])
+                     .expand(2, S).to(dev))
+
+    def step():
+        eng.begin_step(1)
+        eng.zero_grad()
+        eng.begin_micro(0)
+        loss, _, _ = lm.training_step(batch)
+        loss.backward()
+        eng.finish_backward()
+        eng.clip_and_scale(1.0)
+        eng.step(1e-3)
+        return loss
+
+    step()  # warm-up: allocator pools, GEMM solution lookup, ring buffers
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        loss = step()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()
