@@ -27,6 +27,7 @@ from ..parallel import debug as collective_debug
 from ..parallel.context import ParallelContext, init_distributed
 from ..parallel.engine import DataParallelEngine, freeze_modules
 from .monitor import (StallWatchdog, StepProfiler, ThroughputMeter, find_last_checkpoint, model_flops_per_token,
+                      trace_range,
                       record_failure)
 from .strategies import Strategy, resolve_strategy
 
@@ -80,8 +81,9 @@ class Trainer:
                  devices: Any = "auto", accelerator: Any = "auto", limit_train_batches: Any = None,
                  limit_val_batches: Any = None, enable_checkpointing: bool = True, enable_progress_bar: bool = True,
                  default_root_dir: str = "logs", num_sanity_val_steps: int = 0, seed: int | None = None,
-                 deterministic: bool = False, benchmark: Any = None, **unused):
+                 deterministic: bool = False, benchmark: Any = None, gemm_tuning: str | None = None, **unused):
         self.strategy: Strategy = resolve_strategy(strategy)
+        self.gemm_tuning = gemm_tuning  # runtime/gemm_tuning.py modes; applied in setup()
         self.deterministic = bool(deterministic)
         self.precision = precision
         self.loggers = [] if logger in (None, False) else (list(logger) if isinstance(logger, list) else [logger])
@@ -174,6 +176,9 @@ class Trainer:
         st = self.strategy
         rank, local, world, device = init_distributed(st.process_group_backend, st.timeout_minutes)
         self.device = device
+        if self.gemm_tuning is not None:
+            from .gemm_tuning import setup_gemm_tuning
+            setup_gemm_tuning(self.gemm_tuning)
         self.pc = ParallelContext.create(st.data_parallel_size, st.tensor_parallel_size, device)
         seed = self.seed if self.seed is not None else 42
         if self.deterministic:
@@ -334,16 +339,19 @@ class Trainer:
         for i, b in enumerate(batches):
             eng.begin_micro(i)
             b = self.to_device(b)
-            loss, metrics, cnt = lm.training_step(b, self.state.batch_idx + i)
-            loss.backward()
+            with trace_range("forward"):
+                loss, metrics, cnt = lm.training_step(b, self.state.batch_idx + i)
+            with trace_range("backward"):
+                loss.backward()
             for k, v in metrics.items():
                 metrics_acc[k] = metrics_acc.get(k, 0) + v.detach().float().to(self.device) / len(batches)
             for k, v in cnt.items():
                 counters[k] = counters.get(k, 0) + v
-        eng.finish_backward()
-        eng.clip_and_scale(self.gradient_clip_val)
-        lr = self.scheduler.get_lr()
-        eng.step(lr)
+        with trace_range("optimizer"):
+            eng.finish_backward()
+            eng.clip_and_scale(self.gradient_clip_val)
+            lr = self.scheduler.get_lr()
+            eng.step(lr)
         self.scheduler.step()
         self.state.global_step += 1
         for k, v in counters.items():
