@@ -80,8 +80,9 @@ def collect_shard(trainer) -> tuple[dict[str, torch.Tensor], dict[str, list]]:
         if b <= a:
             continue
         sa, _ = eng.shard_range(u)  # where the locally held optimizer state starts in flat coords
-        for p, o in zip(u.params, u.offsets):
-            s, e = max(o, a), min(o + p.numel(), b)
+        # u.shapes, not p.shape: a ZeRO-3 unit's parameters are empty views while it is not gathered
+        for p, o, shp in zip(u.params, u.offsets, u.shapes):
+            s, e = max(o, a), min(o + shp.numel(), b)
             if e <= s:
                 continue
             n = names[id(p)]
@@ -89,7 +90,7 @@ def collect_shard(trainer) -> tuple[dict[str, torch.Tensor], dict[str, list]]:
                 src = getattr(u, kind)
                 piece = src[s - sa:e - sa]
                 tensors[f"{kind}.{n}"] = piece.detach().to("cpu", copy=True)
-                index[f"{kind}.{n}"] = [s - o, e - o, list(p.shape)]
+                index[f"{kind}.{n}"] = [s - o, e - o, list(shp)]
     if eng.pc.dp_rank == 0:  # frozen parameters are not engine units: always resident in full
         for n, p in model.named_parameters():
             if not p.requires_grad:
@@ -273,8 +274,8 @@ def load_checkpoint(trainer, path: str, load_optimizer: bool = True):
             if kind != "master" and not load_optimizer:
                 continue
             tgt = getattr(u, kind)
-            for p, o in zip(u.params, u.offsets):
-                s, e = max(o, a), min(o + p.numel(), b)
+            for p, o, shp in zip(u.params, u.offsets, u.shapes):
+                s, e = max(o, a), min(o + shp.numel(), b)
                 if e <= s:
                     continue
                 key = f"{kind}.{names[id(p)]}"

@@ -16,6 +16,7 @@
 #include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 #include <torch/library.h>
 
 #include <algorithm>
@@ -96,16 +97,27 @@ void make_desc(Desc& d, bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64
 }
 
 std::string key_of(bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
-                   hipDataType ctype, bool beta) {
+                   hipDataType ctype, bool beta, bool streamk) {
   std::ostringstream o;
   o << (ta ? 't' : 'n') << (tb ? 't' : 'n') << "_" << m << "_" << n << "_" << k << "_ld" << lda << "_" << ldb << "_"
-    << ldc << (ctype == HIP_R_32F ? "_f32" : "_bf16") << (beta ? "_acc" : "");
+    << ldc << (ctype == HIP_R_32F ? "_f32" : "_bf16") << (beta ? "_acc" : "") << (streamk ? "" : "_nosk");
   return o.str();
+}
+
+// Stream-K solutions (kernel names with "_SK") split a tile's K range over workgroups that hand partial
+// sums to each other through the workspace, spinning until the partner's flag appears: they assume
+// every workgroup of the launch (one per CU) is resident. When another kernel holds CUs at the same
+// time (an RCCL collective or an AdamW on a side stream) the spin can wait on a workgroup that cannot
+// start — one forward GEMM of a ZeRO-3 step was measured at 2.37 s instead of 3.7 ms
+// (profiles/r2_zero3_streamk_stall.md). Callers that overlap communication ask for non-stream-K solutions.
+bool is_streamk(hipblasLtHandle_t h, hipblasLtMatmulAlgo_t& algo) {
+  const std::string name = hipblaslt_ext::getKernelNameFromAlgo(h, algo);
+  return name.find("_SK") != std::string::npos;
 }
 
 // C (m x n, column-major) = op(A) . op(B) (+ C when accumulate)
 void gemm_lt(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bool tb, int64_t m, int64_t n,
-             int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool accumulate) {
+             int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool accumulate, bool streamk) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm_lt: GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_lt: bf16 A/B");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm_lt: C bf16/fp32");
@@ -120,23 +132,35 @@ void gemm_lt(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bo
   make_desc(d, ta, tb, m, n, k, lda, ldb, ldc, ctype);
   const float alpha = 1.f, beta = accumulate ? 1.f : 0.f;
   auto ws = at::empty({(int64_t)kWorkspace}, C.options().dtype(at::kByte));
-  const std::string key = key_of(ta, tb, m, n, k, lda, ldb, ldc, ctype, accumulate);
+  const std::string key = key_of(ta, tb, m, n, k, lda, ldb, ldc, ctype, accumulate, streamk);
   auto it = s.cache.find(key);
   if (it == s.cache.end()) {
     hipblasLtMatmulPreference_t pref;
     LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
     uint64_t wsz = kWorkspace;
     LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz)));
-    std::vector<hipblasLtMatmulHeuristicResult_t> res(kCandidates);
+    // without stream-K the heuristic's first candidates can all be stream-K: ask for the whole list
+    const int want = streamk ? kCandidates : 512;
+    std::vector<hipblasLtMatmulHeuristicResult_t> res(want);
     int got = 0;
-    LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, d.op, d.a, d.b, d.c, d.c, pref, kCandidates, res.data(), &got));
+    LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, d.op, d.a, d.b, d.c, d.c, pref, want, res.data(), &got));
     hipblasLtMatmulPreferenceDestroy(pref);
+    if (!streamk) {  // drop stream-K solutions, keeping the heuristic order of the rest
+      std::vector<hipblasLtMatmulHeuristicResult_t> keep;
+      for (int i = 0; i < got; ++i)
+        if (!is_streamk(h, res[i].algo)) keep.push_back(res[i]);
+      if (!keep.empty()) {  // (on gfx950 some layouts have stream-K solutions only: then they stay)
+        std::copy(keep.begin(), keep.end(), res.begin());
+        got = (int)keep.size();
+      }
+      got = std::min(got, kCandidates);
+    }
     TORCH_CHECK(got > 0, "gemm_lt: no hipBLASLt solution for ", key);
     Choice best{res[0].algo, 0, -1.f};
     auto pre = s.preset.find(key);
     if (pre != s.preset.end() && pre->second < got) {
       best = Choice{res[pre->second].algo, pre->second, 0.f};
-    } else if (s.tune && got > 1) {
+    } else if ((s.tune || !streamk) && got > 1) {  // non-stream-K candidates are always timed
       // time every candidate on the live operands; the output goes to a scratch tensor so an
       // accumulating call (beta = 1) is not disturbed
       auto scratch = at::empty_like(C);
@@ -175,7 +199,11 @@ std::string gemm_lt_export() {
   auto& s = st();
   std::lock_guard<std::mutex> lock(s.mu);
   std::ostringstream o;
-  for (auto& kv : s.cache) o << kv.first << " " << kv.second.rank << " " << kv.second.ms << "\n";
+  for (auto& kv : s.cache) {
+    hipblasLtMatmulAlgo_t a = kv.second.algo;
+    o << kv.first << " " << kv.second.rank << " " << kv.second.ms << " "
+      << hipblaslt_ext::getKernelNameFromAlgo(s.handles.begin()->second, a) << "\n";
+  }
   return o.str();
 }
 
@@ -203,7 +231,7 @@ int64_t gemm_lt_import(const std::string& text, bool tune_unknown) {
 TORCH_LIBRARY_FRAGMENT(llmt, m) {
   m.def(
       "gemm_lt(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, int m, int n, int k, int lda, int ldb, int ldc, "
-      "bool accumulate) -> ()");
+      "bool accumulate, bool streamk=True) -> ()");
   m.def("gemm_lt_export() -> str", &gemm_lt_export);
   m.def("gemm_lt_import(str text, bool tune_unknown) -> int", &gemm_lt_import);
 }

@@ -51,6 +51,17 @@ def _gemm_modes() -> dict:
 
 
 GEMM_MODES = _gemm_modes()
+# Stream-K hipBLASLt solutions spin on partner workgroups and stall when another kernel holds CUs
+# (csrc/blaslt.cpp): the engine turns them off whenever collectives or the optimizer overlap compute.
+# LLMT_GEMM_STREAMK=0/1 forces the choice.
+_SK_ENV = os.environ.get("LLMT_GEMM_STREAMK", "auto").strip().lower()
+ALLOW_STREAMK = [_SK_ENV not in ("0", "false", "off")]
+
+
+def set_streamk(allowed: bool) -> None:
+    """Allow stream-K GEMM solutions unless LLMT_GEMM_STREAMK pins the choice."""
+    if _SK_ENV == "auto":
+        ALLOW_STREAMK[0] = bool(allowed)
 
 
 def _gemm_operand_ok(t: torch.Tensor) -> bool:
@@ -82,7 +93,7 @@ def mm_nt(x2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) ->
     N = w.shape[0]
     y = out if out is not None else torch.empty(M, N, device=x2.device, dtype=x2.dtype)
     if path == "lt":  # column-major: y^T (N x M) = w^T (from K x N) . x^T (K x M)
-        lib().gemm_lt(w, x2, y, True, False, N, M, K, _ld(w), _ld(x2), N, False)
+        lib().gemm_lt(w, x2, y, True, False, N, M, K, _ld(w), _ld(x2), N, False, ALLOW_STREAMK[0])
     else:
         lib().gemm_(x2, w, y, False, False, False)
     return y
@@ -102,7 +113,7 @@ def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -
     if out is None:
         out = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
     if path == "lt":  # column-major: dx^T (K x M) = w^T (K x N) . dy^T (N x M)
-        lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False)
+        lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
     else:
         lib().gemm_(dy2, w, out, False, True, False)
     return out
@@ -116,7 +127,7 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
     M, N = dy.shape
     K = x.shape[1]
     if path == "lt":  # column-major: dW^T (K x N) = x^T (K x M) . dy (M x N)
-        lib().gemm_lt(x, dy, out.view(N, K), False, True, K, N, M, _ld(x), _ld(dy), K, accumulate)
+        lib().gemm_lt(x, dy, out.view(N, K), False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, ALLOW_STREAMK[0])
         return True
     if path == "hip":
         lib().gemm_(dy, x, out.view(N, K), True, True, accumulate)

@@ -33,6 +33,11 @@ optim/master_weight_wrapper.py) — with one engine designed around MI355X:
   re-gathers it when its output gradient arrives (prefetching the previous unit) and frees it again
   once its backward is done. Activation-checkpoint recomputation runs inside backward and is detected
   (autograd graph task active): it neither prefetches forward nor releases the unit it recomputes.
+  The gathered decoder-layer parameters live in a small fixed ring of buffers (PARAM_POOL slots of the
+  largest layer) instead of being freed to and re-allocated from the caching allocator per layer:
+  at ~230 GB in use the allocator's cache misses turned into hipFree / hipMalloc storms (one hipMalloc
+  measured 2.1 s in a sys-trace of the ZeRO-3 step). The embedding and lm_head units keep one resident
+  full buffer each (2 GB for Llama-3-8B) that every gather overwrites.
 * **Sharded mode at dp = 1.** ``force_sharded=True`` (env ``LLMT_FORCE_SHARDED=1``) runs every
   dp > 1 code path — comm stream, events, reduce-scatter / all-gather, stage-3 free / regather /
   prefetch, transient gradients — over a one-rank process group, so a single GPU executes exactly
@@ -83,6 +88,7 @@ logger = logging.getLogger("llm_training")
 
 ALIGN = 64  # elements
 GRAD_POOL = 3  # transient gradient buffers (stage >= 2): layer being written + reductions in flight
+PARAM_POOL = 4  # stage-3 gathered-parameter buffers: current + prefetched layer, +2 for backward / recompute
 
 
 def _round_up(n: int, m: int) -> int:
@@ -123,6 +129,9 @@ class _Unit:
     g_host: torch.Tensor | None = None    # optimizer offload: pinned gradient shard
     p_host: torch.Tensor | None = None    # optimizer offload: pinned bf16 parameter shard
     sec: torch.Tensor | None = None       # hpZ: secondary (intra-node) partition of the gathered params
+    param_ring: bool = False        # stage 3: gathered params live in a slot of the parameter ring
+    shapes: list = field(default_factory=list)  # parameter shapes (ring units re-bind their views)
+    pslot: object = None            # the parameter ring slot currently held
 
     @property
     def shard_numel(self):
@@ -268,6 +277,7 @@ class DataParallelEngine:
         if not params:
             gaps = [(0, numel)]
         u = _Unit(i, m, params, offs, numel, dp=dp)
+        u.shapes = [p.shape for p in params]
         u.replicated = replicated
         u.keep_gathered = keep
         u.grad_gaps = gaps
@@ -331,6 +341,9 @@ class DataParallelEngine:
                         u.pshard = u.pshard.pin_memory()
             else:
                 u.pshard = pflat[r * sn:(r + 1) * sn].clone()
+            # decoder layers gather into the parameter ring; the embedding / lm_head units (large, used
+            # outside a single hooked forward window) keep a resident buffer
+            u.param_ring = (not keep and i > 0 and m is not None and _hookable(m))
             self._free_full(u)
         return u
 
@@ -367,14 +380,46 @@ class DataParallelEngine:
             return r * sn, (r + 1) * sn
         return 0, u.numel
 
+    def _bind_params(self, u: _Unit, flat: torch.Tensor):
+        u.pflat = flat
+        for p, o, shp in zip(u.params, u.offsets, u.shapes):
+            p.data = flat[o:o + shp.numel()].view(shp)
+
     def _free_full(self, u: _Unit):
-        u.pflat.untyped_storage().resize_(0)
         u.gathered = False
+        if not u.param_ring:
+            return  # resident buffer: the next gather overwrites it
+        slot = u.pslot
+        if slot is not None:
+            if self.cuda:  # the slot's next owner gathers into it only after this unit's last use
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream())
+                slot["event"] = ev
+            slot["owner"] = None
+            u.pslot = None
+        empty = u.pflat.new_empty(0)
+        u.pflat = empty
+        for p in u.params:
+            p.data = empty
 
     def _alloc_full(self, u: _Unit):
-        st = u.pflat.untyped_storage()
-        if st.size() == 0:
-            st.resize_(u.numel * u.pflat.element_size())
+        if not u.param_ring or u.pslot is not None:
+            return
+        if getattr(self, "_ppool", None) is None:
+            n = max(v.numel for v in self.units if v.param_ring)
+            self._ppool = [{"buf": torch.empty(n, device=self.device, dtype=self.param_dtype), "event": None,
+                            "owner": None} for _ in range(PARAM_POOL)]
+        free = [sl for sl in self._ppool if sl["owner"] is None]
+        if not free:  # more units gathered at once than the ring holds (e.g. full_params_context)
+            self._bind_params(u, torch.empty(u.numel, device=self.device, dtype=self.param_dtype))
+            return
+        slot = free[0]
+        if slot["event"] is not None and self.cuda:
+            torch.cuda.current_stream().wait_event(slot["event"])  # the comm stream waits on this stream
+            slot["event"] = None
+        slot["owner"] = u.idx
+        u.pslot = slot
+        self._bind_params(u, slot["buf"][:u.numel])
 
     # ------------------------------------------------------------------ transient gradient buffers
     def _grad_allocated(self, u: _Unit) -> bool:
@@ -397,8 +442,8 @@ class DataParallelEngine:
         slot["owner"] = u.idx
         u.gslot = slot
         u.gflat = slot["buf"][:u.numel]
-        for p, o in zip(u.params, u.offsets):
-            p.main_grad = u.gflat[o:o + p.numel()].view(p.shape)
+        for p, o, shp in zip(u.params, u.offsets, u.shapes):
+            p.main_grad = u.gflat[o:o + shp.numel()].view(shp)
             p.grad_added = False  # fresh buffer: the first gradient written is a copy, not an add
         for a, b in u.grad_gaps:  # alignment padding is reduced too: keep it zero
             u.gflat[a:b].zero_()
@@ -539,10 +584,14 @@ class DataParallelEngine:
         if keep_secondary and self.hpz_group is not None:
             n = u.numel // self.hpz
             u.sec = u.pflat[self.hpz_rank * n:(self.hpz_rank + 1) * n].clone()
-        if self.cuda:
+        if self.cuda and u.param_ring and u.pslot is None and u.pflat.numel():
+            # a fallback buffer from the allocator (ring exhausted): keep it alive for pending stream uses
             u.pflat.record_stream(torch.cuda.current_stream())
             if self.comm_stream is not None:
                 u.pflat.record_stream(self.comm_stream)
+        if self.cuda and u.ag_event is not None:
+            # an unfinished prefetch still writes this buffer: later work on this stream orders after it
+            torch.cuda.current_stream().wait_event(u.ag_event)
         u.ag_event = None
         self._free_full(u)
 
