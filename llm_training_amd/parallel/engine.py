@@ -254,7 +254,7 @@ class DataParallelEngine:
         for i, (m, params, replicated) in enumerate(groups):
             u = self._make_unit(i, m, params, replicated, keep=(i in multi or i == n_named - 1))
             self.units.append(u)
-        nparams = sum(p.numel() for u in self.units for p in u.params)
+        nparams = sum(s.numel() for u in self.units for s in u.shapes)
         logger.info("engine: %d units, %.3f B trainable params (local), zero stage %d, dp %d, tp %d%s%s",
                     len(self.units), nparams / 1e9, self.stage, self.dp, self.pc.tp_size,
                     ", sharded(forced)" if self.sharded and self.dp == 1 else "",
