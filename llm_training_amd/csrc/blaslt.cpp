@@ -30,7 +30,12 @@
 
 namespace {
 
-constexpr int kCandidates = 24;                  // heuristic candidates timed per new problem
+// heuristic candidates timed per new problem (LLMT_GEMM_TUNE_TOPK overrides)
+const int kCandidates = [] {
+  const char* e = std::getenv("LLMT_GEMM_TUNE_TOPK");
+  const int v = e ? std::atoi(e) : 24;
+  return v > 0 ? v : 24;
+}();
 constexpr size_t kWorkspace = 128ull << 20;      // stream-K / split-K scratch
 
 #define LT_CHECK(expr)                                                                    \
