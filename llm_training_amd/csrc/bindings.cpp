@@ -33,7 +33,7 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
                                int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss, int64_t q_sh,
                                int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh,
                                int64_t o_sb, int64_t o_ss, int64_t o_sh, float scale, int causal, int window,
-                               int seg_runs, hipStream_t stream);
+                               int seg_runs, float drop_p, uint32_t drop_seed, hipStream_t stream);
 hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N, int K,
                      int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream);
 int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D);
@@ -48,7 +48,7 @@ hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
                                int64_t v_sh, int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss,
                                int64_t dq_sh, int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb,
                                int64_t dv_ss, int64_t dv_sh, float scale, int causal, int window, int seg_runs,
-                               hipStream_t stream);
+                               float drop_p, uint32_t drop_seed, hipStream_t stream);
 }
 
 namespace {
@@ -348,7 +348,7 @@ static int seg_layout(const c10::optional<at::Tensor>& seg, int64_t B, int64_t S
 }
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                                   const c10::optional<at::Tensor>& seg, double scale, bool causal,
-                                                  int64_t window) {
+                                                  int64_t window, double dropout_p, int64_t seed) {
   check_bf16_cuda(q, "q");
   check_bf16_cuda(k, "k");
   check_bf16_cuda(v, "v");
@@ -368,7 +368,8 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   check(llmt_flash_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), sp, (int)B,
                             (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                             k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1),
-                            o.stride(2), (float)scale, causal ? 1 : 0, (int)window, runs, cur_stream()),
+                            o.stride(2), (float)scale, causal ? 1 : 0, (int)window, runs, (float)dropout_p,
+                            (uint32_t)seed, cur_stream()),
         "flash_attn_fwd");
   return {o, lse};
 }
@@ -376,7 +377,8 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
 // dq/dk/dv are written into caller-provided tensors (so they can be views of one fused dQKV buffer).
 void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
                     const at::Tensor& dout, const at::Tensor& lse, const c10::optional<at::Tensor>& seg, at::Tensor dq,
-                    at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window) {
+                    at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window, double dropout_p,
+                    int64_t seed) {
   const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
   const int64_t Hkv = k.size(2);
   check_bf16_cuda(dout, "dout");
@@ -390,7 +392,8 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   auto delta = at::empty({llmt_flash_attn_bwd_ws((int)B, (int)S, (int)Hq, (int)D)}, q.options().dtype(at::kFloat));
   TORCH_CHECK(dout.strides() == o.strides(), "flash_attn_bwd: dout must share O's layout");
   at::Tensor work;  // fp32 per-q-head dK/dV partials, only needed for GQA
-  if (Hq != Hkv && D != 128) work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
+  if (Hq != Hkv && (D != 128 || dropout_p > 0))  // (dropout runs the generic kernels at every D)
+    work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
   check(llmt_flash_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                             lse.data_ptr<float>(), delta.data_ptr<float>(), sp, dq.data_ptr(), dk.data_ptr(),
                             dv.data_ptr(), work.defined() ? work.data_ptr<float>() : nullptr, (int)B, (int)S, (int)Hq, (int)Hkv, (int)D,
@@ -398,7 +401,7 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
                             v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
                             dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0),
                             dv.stride(1), dv.stride(2), (float)scale, causal ? 1 : 0, (int)window, runs,
-                            cur_stream()),
+                            (float)dropout_p, (uint32_t)seed, cur_stream()),
         "flash_attn_bwd");
 }
 
@@ -424,11 +427,11 @@ TORCH_LIBRARY(llmt, m) {
   m.def("dequant_sum_(Tensor q, Tensor scale, Tensor(a!) out, int k, bool accumulate) -> ()");
   m.def("gemm_(Tensor a, Tensor b, Tensor(a!) c, bool a_mn, bool b_mn, bool accumulate) -> ()");
   m.def(
-      "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window) -> (Tensor, "
-      "Tensor)");
+      "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window, "
+      "float dropout_p=0., int seed=0) -> (Tensor, Tensor)");
   m.def(
       "flash_attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor? seg, Tensor(a!) dq, "
-      "Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int window) -> ()");
+      "Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int window, float dropout_p=0., int seed=0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(llmt, CUDA, m) {

@@ -179,7 +179,25 @@ struct AttnArgs {
   int dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
   float scale;
   int causal, window;
+  // attention dropout (reference attention_dropout, FA2 dropout_p): a probability is kept iff
+  // drop_hash(seed, b * Hq + h, q, k) >= drop_thresh (= p * 2^32) and then scaled by 1 / (1 - p); the
+  // backward regenerates the same mask from the same counters. drop_thresh = 0: no dropout.
+  uint32_t drop_seed, drop_thresh;
+  float drop_scale;
 };
+
+__device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q, uint32_t k) {
+  uint32_t x = seed ^ (bh * 0x9E3779B1u);
+  x ^= q * 0x85EBCA6Bu;
+  x = (x ^ (x >> 15)) * 0x2C1B3C6Du;
+  x ^= k * 0xC2B2AE35u;
+  x = (x ^ (x >> 12)) * 0x297A2D39u;
+  return x ^ (x >> 15);
+}
+// dropout multiplier of probability (q, k): 0 or 1 / (1 - p)
+__device__ __forceinline__ float drop_z(const AttnArgs& a, uint32_t bh, int q, int k) {
+  return drop_hash(a.drop_seed, bh, (uint32_t)q, (uint32_t)k) >= a.drop_thresh ? a.drop_scale : 0.f;
+}
 
 constexpr float kThr = 6.0f;  // defer-max threshold (log2 units): P <= 2^6 before a forced rescale
 
@@ -349,7 +367,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(AttnArgs a) {
         st[t][i] = p;
         rs += p;
       }
-    l += rs;
+    l += rs;  // the normaliser sums the undropped probabilities
+    if (a.drop_thresh) {
+      const uint32_t bh = (uint32_t)(b * a.Hq + h);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          st[t][i] *= drop_z(a, bh, qrow, n0 + 32 * t + 8 * (i >> 2) + 4 * hh + (i & 3));
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -502,7 +528,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
         st = mfma32(KI::row_read(Ks, 32 * t + r, 2 * kk + hh), qf[kk], st);
         dpt = mfma32(lds_b128(Vs + (32 * t + r) * G::KP + (kk * 16 + hh * 8) * 2), df[kk], dpt);
       }
-      if (need_mask) {
+      if (need_mask || a.drop_thresh) {
+        // dropout: dS = P * (Z * dP - delta), Z the forward's keep mask / (1 - p)
+        const uint32_t bh = (uint32_t)(b * a.Hq + h);
         const int lim = qrow - n0 - 32 * t - 4 * hh;
         const int lo = qrow - a.window - n0 - 32 * t - 4 * hh;
         const int hi = S - 1 - n0 - 32 * t - 4 * hh;
@@ -518,7 +546,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(AttnArgs a) {
             if (a.window >= 0) ok = ok && (ko >= lo);
             if (m_seg) ok = ok && ((&sk.x)[j] == sq);
             const float p = ok ? fexp2(st[i] * sl2 - lse2) : 0.f;
-            st[i] = p * (dpt[i] - dlt);
+            const float dp = a.drop_thresh ? dpt[i] * drop_z(a, bh, qrow, n0 + 32 * t + 4 * hh + ko) : dpt[i];
+            st[i] = p * (dp - dlt);
           }
         }
       } else {
@@ -663,6 +692,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
     const bool m_seg = seg_mask(a, kr_run, q0, q0 + BM - 1);
     const bool need_mask = m_seg || (q0 + BM > S) || (kw + 31 >= S) || (a.causal && kw + 31 > q0) ||
                            (a.window >= 0 && q0 + BM - 1 > kw + a.window);
+    const uint32_t bh = (uint32_t)(b * a.Hq + h);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float4 l4 = *reinterpret_cast<const float4*>(Ls + 8 * c + 4 * hh);
@@ -680,8 +710,14 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(AttnArgs a) {
           if (m_seg) ok = ok && (Sg[qloc] == sk);
           p = ok ? p : 0.f;
         }
-        sacc[i] = p;                                 // P
-        dpacc[i] = p * (dpacc[i] - (&d4.x)[j]);      // dS
+        if (a.drop_thresh) {  // dV takes the dropped P, dS = P * (Z * dP - delta)
+          const float z = drop_z(a, bh, q0 + qloc, kr);
+          sacc[i] = p * z;
+          dpacc[i] = p * (dpacc[i] * z - (&d4.x)[j]);
+        } else {
+          sacc[i] = p;                                 // P
+          dpacc[i] = p * (dpacc[i] - (&d4.x)[j]);      // dS
+        }
       }
     }
 #pragma unroll
@@ -1789,6 +1825,17 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 
 using namespace llmt;
 
+static void set_dropout(AttnArgs& a, float p, uint32_t seed) {
+  if (p <= 0.f) {
+    a.drop_thresh = 0;
+    return;
+  }
+  const double t = (double)p * 4294967296.0;
+  a.drop_thresh = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : (t < 1.0 ? 1.0 : t));
+  a.drop_seed = seed;
+  a.drop_scale = 1.f / (1.f - p);
+}
+
 // buffer-load offsets are 32-bit: every row of one (batch, head) slice must be addressable
 static bool fits32(int64_t S, int64_t row_stride) { return S * row_stride * 2 < 0x7fffffffLL; }
 static bool strides32(std::initializer_list<int64_t> xs) {
@@ -1806,11 +1853,12 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
                                           int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh,
                                           int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
                                           int64_t o_sh, float scale, int causal, int window, int seg_runs,
-                                          hipStream_t stream) {
+                                          float drop_p, uint32_t drop_seed, hipStream_t stream) {
   if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
   if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
       !aligned16(o, o_sb, o_ss, o_sh))
     return hipErrorInvalidValue;
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return hipErrorInvalidValue;
   if (B == 0 || S == 0) return hipSuccess;
   if (!fits32(S, q_ss) || !fits32(S, k_ss) || !fits32(S, v_ss)) return hipErrorInvalidValue;
   if (!strides32({q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh})) return hipErrorInvalidValue;
@@ -1824,6 +1872,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   a.q_sb = q_sb; a.q_ss = q_ss; a.q_sh = q_sh; a.k_sb = k_sb; a.k_ss = k_ss; a.k_sh = k_sh;
   a.v_sb = v_sb; a.v_ss = v_ss; a.v_sh = v_sh; a.o_sb = o_sb; a.o_ss = o_ss; a.o_sh = o_sh;
   a.scale = scale; a.causal = causal; a.window = window;
+  set_dropout(a, drop_p, drop_seed);
   dim3 grid((S + 127) / 128, Hq, B);
   switch (D) {
     case 64: fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a); break;
@@ -1834,7 +1883,9 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
         // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907, fwd128 1.043
         return e ? atoi(e) : 2;
       }();
-      if (variant == 1)
+      if (a.drop_thresh)  // dropout lives in the generic kernels
+        fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
+      else if (variant == 1)
         fa_fwd128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (variant == 2)
         fa_fwd3_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
@@ -1860,7 +1911,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
                                           int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss, int64_t dq_sh,
                                           int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb, int64_t dv_ss,
                                           int64_t dv_sh, float scale, int causal, int window, int seg_runs,
-                                          hipStream_t stream) {
+                                          float drop_p, uint32_t drop_seed, hipStream_t stream) {
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return hipErrorInvalidValue;
   if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
   if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
       !aligned16(o, o_sb, o_ss, o_sh) || !aligned16(dout, o_sb, o_ss, o_sh) || !aligned16(dq, dq_sb, dq_ss, dq_sh) ||
@@ -1888,11 +1940,12 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   a.dq_sb = dq_sb; a.dq_ss = dq_ss; a.dq_sh = dq_sh; a.dk_sb = dk_sb; a.dk_ss = dk_ss; a.dk_sh = dk_sh;
   a.dv_sb = dv_sb; a.dv_ss = dv_ss; a.dv_sh = dv_sh;
   a.scale = scale; a.causal = causal; a.window = window;
+  set_dropout(a, drop_p, drop_seed);
   const bool gqa = Hq != Hkv;
   const int64_t nrows = (int64_t)B * S * Hq;
   dim3 grid((S + 127) / 128, Hq, B);
   const int dgrid = stream_grid(nrows, 256);
-  if (D == 128) {
+  if (D == 128 && !a.drop_thresh) {
     // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws)
     float* ld = delta + nrows;
     const int64_t nT = (S + 31) / 32;

@@ -9,8 +9,8 @@ The model body runs through transformers; its attention is routed to our gfx950 
 ``llmt_hip``: the packed segment ids travel as a forward kwarg down to every attention call, so
 packed rows take the varlen kernel instead of a dense [B, 1, S, S] mask — the reference reaches the
 same end by patching ``_get_unpad_data`` for FA2 (hf_causal_lm.py:19-20). Calls the kernel cannot
-serve (attention dropout while training, logit soft-capping, head dims other than 64/96/128,
-non-causal modules) run transformers' SDPA with the equivalent dense mask. The loss heads use our
+serve (logit soft-capping, head dims other than 64/96/128, non-causal modules) run transformers'
+SDPA with the equivalent dense mask; attention dropout runs in the kernels. The loss heads use our
 fused lm_head + cross-entropy on the final hidden states, and the ZeRO engine shards the HF model by
 its ``_no_split_modules`` blocks. ``hf_config`` builds a random-init model from a config dict (no
 checkpoint needed); ``hf_path`` loads a LOCAL checkpoint.
@@ -50,9 +50,7 @@ def hf_attention(module, query, key, value, attention_mask, scaling=None, dropou
     seg = kwargs.get("llmt_segment_ids")
     D = query.shape[-1]
     why = None
-    if dropout and dropout > 0:
-        why = "attention dropout"
-    elif softcap is not None:
+    if softcap is not None:
         why = "logit soft-capping"
     elif D not in (64, 96, 128) and query.is_cuda:
         why = f"head dim {D}"
@@ -61,7 +59,7 @@ def hf_attention(module, query, key, value, attention_mask, scaling=None, dropou
     if why is None:
         window = None if sliding_window is None else int(sliding_window) - 1  # HF: q - k < sliding_window
         o = flash_attention(query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2), causal=True,
-                            segment_ids=seg, window=window, scale=scaling)
+                            segment_ids=seg, window=window, scale=scaling, dropout_p=float(dropout or 0.0))
         return o, None
     if why not in _FALLBACK_WARNED:
         _FALLBACK_WARNED.add(why)

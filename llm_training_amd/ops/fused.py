@@ -18,7 +18,6 @@ flash-attn calls of src/llm_training/ops/attention_op.py.
 """
 from __future__ import annotations
 
-import logging
 import math
 import os
 
@@ -352,20 +351,20 @@ class _RopeFlashAttnFn(Function):
     # kernels see [B, S, H, D] strided views (transpose(0, 1)) and return O in the same seq-major memory
     # order, so the output projection consumes it without a copy.
     @staticmethod
-    def forward(ctx, qkv, pos, cos, sin, seg, nq, nkv, causal, window, scale):
+    def forward(ctx, qkv, pos, cos, sin, seg, nq, nkv, causal, window, scale, dropout_p=0.0, seed=0):
         L = lib()
         L.rope_(qkv, pos, cos, sin, nq + nkv, False)
         x = qkv.transpose(0, 1)
         q, k, v = x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:]
-        o, lse = L.flash_attn_fwd(q, k, v, seg, scale, causal, window)
+        o, lse = L.flash_attn_fwd(q, k, v, seg, scale, causal, window, dropout_p, seed)
         ctx.save_for_backward(qkv, o, lse, pos, cos, sin, seg)
-        ctx.cfg = (nq, nkv, causal, window, scale)
+        ctx.cfg = (nq, nkv, causal, window, scale, dropout_p, seed)
         return o.transpose(0, 1)
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse, pos, cos, sin, seg = ctx.saved_tensors
-        nq, nkv, causal, window, scale = ctx.cfg
+        nq, nkv, causal, window, scale, dropout_p, seed = ctx.cfg
         L = lib()
         do = do.transpose(0, 1)
         if not _same_layout(do, o):
@@ -375,9 +374,9 @@ class _RopeFlashAttnFn(Function):
         dqkv = torch.empty_like(qkv)
         x, dx = qkv.transpose(0, 1), dqkv.transpose(0, 1)
         L.flash_attn_bwd(x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:], o, do, lse, seg, dx[:, :, :nq],
-                         dx[:, :, nq:nq + nkv], dx[:, :, nq + nkv:], scale, causal, window)
+                         dx[:, :, nq:nq + nkv], dx[:, :, nq + nkv:], scale, causal, window, dropout_p, seed)
         L.rope_(dqkv, pos, cos, sin, nq + nkv, True)
-        return dqkv, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -391,23 +390,23 @@ class _FlashAttnFn(Function):
     """Plain flash attention on separate q/k/v [B, S, H, D] tensors."""
 
     @staticmethod
-    def forward(ctx, q, k, v, seg, causal, window, scale):
-        o, lse = lib().flash_attn_fwd(q, k, v, seg, scale, causal, window)
+    def forward(ctx, q, k, v, seg, causal, window, scale, dropout_p=0.0, seed=0):
+        o, lse = lib().flash_attn_fwd(q, k, v, seg, scale, causal, window, dropout_p, seed)
         ctx.save_for_backward(q, k, v, o, lse, seg)
-        ctx.cfg = (causal, window, scale)
+        ctx.cfg = (causal, window, scale, dropout_p, seed)
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse, seg = ctx.saved_tensors
-        causal, window, scale = ctx.cfg
+        causal, window, scale, dropout_p, seed = ctx.cfg
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         if not _same_layout(do, o):
             do = torch.empty_like(o).copy_(do)
         elif do.stride() != o.stride():
             do = do.as_strided(o.shape, o.stride())
-        lib().flash_attn_bwd(q, k, v, o, do, lse, seg, dq, dk, dv, scale, causal, window)
-        return dq, dk, dv, None, None, None, None
+        lib().flash_attn_bwd(q, k, v, o, do, lse, seg, dq, dk, dv, scale, causal, window, dropout_p, seed)
+        return dq, dk, dv, None, None, None, None, None, None
 
 
 def segment_info(segment_ids: torch.Tensor) -> torch.Tensor:
@@ -436,14 +435,27 @@ def _native_seg(segment_ids, seg_info):
     return segment_info(segment_ids)
 
 
+def dropout_seed() -> int:
+    """Seed of one attention call's dropout mask (from torch's CPU generator: reproducible under
+    torch.manual_seed, no device sync); the backward regenerates the mask from it."""
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+
 def flash_attention(q, k, v, causal: bool = True, segment_ids=None, window: int = -1, scale: float | None = None,
-                    seg_info=None):
+                    seg_info=None, dropout_p: float = 0.0, seed: int | None = None):
     """q: [B, S, Hq, D]; k/v: [B, S, Hkv, D]; segment_ids: optional int [B, S] — tokens attend within
-    their contiguous run of equal ids (packed documents; 0 = padding)."""
+    their contiguous run of equal ids (packed documents; 0 = padding). ``dropout_p``: attention
+    dropout on the probabilities, in the kernels (mask from a counter hash of (seed, b, h, q, k))."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if use_native(q):
         seg = _native_seg(segment_ids, seg_info)
-        return _FlashAttnFn.apply(q, k, v, seg, causal, -1 if window is None else int(window), scale)
+        if dropout_p > 0 and seed is None:
+            seed = dropout_seed()
+        return _FlashAttnFn.apply(q, k, v, seg, causal, -1 if window is None else int(window), scale,
+                                  float(dropout_p), int(seed or 0))
+    if dropout_p > 0:
+        return ref.attention_dropout(q, k, v, causal, segment_ids, -1 if window is None else window, scale,
+                                     dropout_p, dropout_seed() if seed is None else seed)
     return ref.attention(q, k, v, causal, segment_ids, -1 if window is None else window, scale)
 
 
@@ -452,9 +464,6 @@ def rope_tables_to_full(cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor)
     c = cos[pos]
     s = sin[pos]
     return torch.cat([c, c], -1), torch.cat([s, s], -1)
-
-
-_DROPOUT_WARNED = [False]
 
 
 def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool = True, segment_ids=None,
@@ -466,25 +475,21 @@ def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool =
     ``segment_ids``: optional [B, S] (tokens attend only within their contiguous run of equal ids);
     ``seg_info``: its precomputed :func:`segment_info` (shared across layers); ``dropout_p``: attention
     dropout on the probabilities (reference ``attention_dropout``, llama_model.py:593-621 — FA2 / SDPA
-    ``dropout_p``). The HIP flash kernels have no dropout: a non-zero ``dropout_p`` runs torch SDPA with
-    the same visibility mask (logged once).
+    ``dropout_p``): in the HIP kernels on the GPU (the generic forward / backward kernels, which carry the
+    keep-mask hash), SDPA with dropout on the CPU / SDPA paths.
     """
     D = qkv.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     win = -1 if window is None else int(window)
-    if dropout_p > 0:
-        if not _DROPOUT_WARNED[0]:
-            _DROPOUT_WARNED[0] = True
-            logging.getLogger("llm_training").warning(
-                "attention_dropout=%g: attention runs torch SDPA with dropout (the HIP flash kernels have none)",
-                dropout_p)
-        return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win,
-                                   scale, "sdpa", dropout_p).transpose(0, 1)
     if use_native(qkv) and impl in ("flash", "flash_attention_2", "hip"):
         qkv = qkv.contiguous()
         pos = positions.t().contiguous().reshape(-1)
         seg = _native_seg(segment_ids, seg_info)
-        return _RopeFlashAttnFn.apply(qkv, pos, cos, sin, seg, n_q, n_kv, causal, win, scale)
+        seed = dropout_seed() if dropout_p > 0 else 0
+        return _RopeFlashAttnFn.apply(qkv, pos, cos, sin, seg, n_q, n_kv, causal, win, scale, float(dropout_p), seed)
+    if dropout_p > 0:
+        return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win,
+                                   scale, "sdpa", dropout_p).transpose(0, 1)
     return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale,
                                impl).transpose(0, 1)
 

@@ -70,6 +70,42 @@ def attention(q, k, v, causal: bool = True, segment_ids=None, window: int = -1, 
     return o.transpose(1, 2).to(q.dtype)
 
 
+def dropout_keep_scale(seed: int, B: int, Hq: int, S: int, p: float, device=None) -> torch.Tensor:
+    """[B, Hq, S(q), S(k)] fp32 multipliers (0 or 1 / (1 - p)) of the HIP kernels' attention-dropout mask:
+    the same 32-bit counter hash of (seed, b * Hq + h, q, k) as csrc/flash_attn.hip drop_hash (uint32
+    arithmetic emulated in int64, low 32 bits kept)."""
+    M = 0xFFFFFFFF
+    bh = torch.arange(B * Hq, device=device, dtype=torch.int64).view(B, Hq, 1, 1)
+    q = torch.arange(S, device=device, dtype=torch.int64).view(1, 1, S, 1)
+    k = torch.arange(S, device=device, dtype=torch.int64).view(1, 1, 1, S)
+    x = (int(seed) ^ ((bh * 0x9E3779B1) & M)) & M
+    x = x ^ ((q * 0x85EBCA6B) & M)
+    x = ((x ^ (x >> 15)) * 0x2C1B3C6D) & M
+    x = x ^ ((k * 0xC2B2AE35) & M)
+    x = ((x ^ (x >> 12)) * 0x297A2D39) & M
+    x = x ^ (x >> 15)
+    t = p * 4294967296.0
+    thresh = int(min(max(t, 1.0), 4294967295.0))
+    scale = float(torch.tensor(1.0 / (1.0 - p), dtype=torch.float32))
+    return (x >= thresh).float() * scale
+
+
+def attention_dropout(q, k, v, causal=True, segment_ids=None, window=-1, scale=None, p=0.0, seed=0):
+    """Eager attention with the kernels' dropout mask applied to the probabilities (oracle)."""
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    rep = Hq // Hkv
+    qh = q.transpose(1, 2).float()
+    kh = k.transpose(1, 2).float().repeat_interleave(rep, dim=1)
+    vh = v.transpose(1, 2).float().repeat_interleave(rep, dim=1)
+    s = torch.matmul(qh, kh.transpose(-1, -2)) * scale
+    mask = visibility_mask(S, q.device, causal, segment_ids, window, B)
+    s = s.masked_fill(~mask[:, None], float("-inf"))
+    pr = torch.softmax(s, -1).nan_to_num(0.0) * dropout_keep_scale(seed, B, Hq, S, p, q.device)
+    return torch.matmul(pr, vh).transpose(1, 2).to(q.dtype)
+
+
 def visibility_mask(S, device, causal=True, segment_ids=None, window=-1, B=1):
     i = torch.arange(S, device=device)
     m = torch.ones(S, S, dtype=torch.bool, device=device)

@@ -338,3 +338,34 @@ def test_gemm_lt_tuned_layouts(layout, out):
     finally:
         fused.GEMM_MODES.update(old)
     assert "_acc" in lib().gemm_lt_export() or layout != "tn" or not out.endswith("acc")
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,segs", [(128, 4, 2, False), (64, 2, 2, True), (128, 2, 2, True)])
+def test_flash_attention_dropout_matches_oracle(D, Hq, Hkv, segs):
+    """Attention dropout inside the HIP kernels (generic fwd / dQ / dK-dV kernels): the keep mask is a
+    counter hash of (seed, b, h, q, k); the fp32 oracle rebuilds the same mask (reference.py
+    dropout_keep_scale), so output and all three gradients must match, and the backward must use the
+    forward's mask (a different seed gives a different output)."""
+    from llm_training_amd.ops import reference as ref
+    from llm_training_amd.ops.fused import flash_attention
+    torch.manual_seed(0)
+    B, S, p = 2, 300, 0.3
+    q = torch.randn(B, S, Hq, D, device=DEV).bfloat16().requires_grad_(True)
+    k = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_(True)
+    v = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_(True)
+    seg = None
+    if segs:
+        seg = torch.repeat_interleave(torch.tensor([1, 2, 3]), torch.tensor([100, 120, 80])).expand(B, S).to(DEV)
+    o = flash_attention(q, k, v, causal=True, segment_ids=seg, dropout_p=p, seed=1234)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    orf = ref.attention_dropout(qr, kr, vr, True, seg, -1, None, p, 1234)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 2e-2
+    for a_, b_ in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        assert _rel(a_, b_) < 3e-2
+    o2 = flash_attention(q, k, v, causal=True, segment_ids=seg, dropout_p=p, seed=99)
+    assert _rel(o2, orf) > 0.1
+    o0 = flash_attention(q, k, v, causal=True, segment_ids=seg, dropout_p=0.0)
+    assert _rel(o0, ref.attention(q.float(), k.float(), v.float(), True, seg, -1, None)) < 2e-2
