@@ -1626,7 +1626,9 @@ __device__ __forceinline__ float vadd(float a, float b) {
   return r;
 }
 
+template <int D>
 __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
+  constexpr int NKK = D / 16, NDT = D / 32;  // k-steps of a D-deep product, 32-wide output tiles
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
   using KI = Img<128>;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
@@ -1647,16 +1649,16 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
   const float sl2 = a.scale * kLog2e;
   int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
 
-  bfv8 qf[8];
+  bfv8 qf[NKK];
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+  for (int kk = 0; kk < NKK; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
   // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
   asm volatile("" : "+v"(sq));
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(qf[kk]));
-  f32v16 ot[4];
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
+  f32v16 ot[NDT];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;  // running max in scaled log2 units
@@ -1685,14 +1687,14 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
       dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
     };
     // loop-invariant LDS offsets: K row reads (two 32-key halves) and V^T transposed reads
-    int ro[8], to[4][2];
+    int ro[NKK], to[NDT][2];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
+    for (int kk = 0; kk < NKK; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
     {
       const int g = lane >> 4, i16 = lane & 15;
       const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt) {
         to[dt][0] = KI::toff(BN, row, dt * 32 + col);
         to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
       }
@@ -1709,7 +1711,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) fr[8 * tt + kk] = lds_b128(slot + 8192 * tt + ro[kk]);
+        for (int kk = 0; kk < NKK; ++kk) fr[8 * tt + kk] = lds_b128(slot + 8192 * tt + ro[kk]);
       __builtin_amdgcn_sched_barrier(0);  // keep the batch: one LDS latency per tile, not per MFMA
       f32v16 st[2];
 #pragma unroll
@@ -1717,7 +1719,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) st[tt][i] = 0.f;
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) st[tt] = mfma32(fr[8 * tt + kk], qf[kk], st[tt]);
+        for (int kk = 0; kk < NKK; ++kk) st[tt] = mfma32(fr[8 * tt + kk], qf[kk], st[tt]);
       }
       // V^T operands of the P.V product (keys 32tt + 16s2 .., columns 32dt ..) into the same registers
 #pragma unroll
@@ -1725,7 +1727,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
+          for (int dt = 0; dt < NDT; ++dt) {
             const char* base = slot + IMG + 256 * (32 * tt + 16 * s2);
             const s16v4 lo = lds_tr(base + to[dt][0]), hi = lds_tr(base + to[dt][1]);
             fr[8 * tt + 4 * s2 + dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -1771,7 +1773,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
         m = mnew;
         l *= alpha;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+        for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
       }
@@ -1793,7 +1795,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
         for (int s2 = 0; s2 < 2; ++s2) {
           const bfv8 pb = acc_as_b(st[tt], s2);
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) ot[dt] = mfma32(fr[8 * tt + 4 * s2 + dt], pb, ot[dt]);
+          for (int dt = 0; dt < NDT; ++dt) ot[dt] = mfma32(fr[8 * tt + 4 * s2 + dt], pb, ot[dt]);
         }
       __builtin_amdgcn_sched_barrier(0);  // the P.V work stays ahead of the wait: the DMA flies under it
       wait_vm<0>();  // this wave's DMA of tile t + 1
@@ -1806,7 +1808,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
   if (qrow < S) {
     bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         uint2 w;
@@ -1827,7 +1829,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 // V row reads -> dP^T = V.dO^T, dS = P (dP - delta) with P = exp2(S * scale * log2e - lse * log2e)
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
 // dQ = scale * sum; the row constants come straight from lse / delta (delta written by the prep kernel).
+template <int D>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
+  constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
   using KI = Img<128>;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
@@ -1852,19 +1856,19 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   float dlt = qrow < S ? a.delta[lrow] : 0.f;
   int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
 
-  bfv8 qf[8], df[8];
+  bfv8 qf[NKK], df[NKK];
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
+  for (int kk = 0; kk < NKK; ++kk) {
     qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
     df[kk] = gload8(dop + (int64_t)min(qrow, S - 1) * a.d_ss + kk * 16 + hh * 8, qrow < S);
   }
   // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
   asm volatile("" : "+v"(sq), "+v"(lse2), "+v"(dlt));
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(df[kk]));
-  f32v16 dqt[4];
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(df[kk]));
+  f32v16 dqt[NDT];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqt[dt][i] = 0.f;
 
@@ -1891,14 +1895,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
       }
       dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
     };
-    int ro[8], to[4][2];
+    int ro[NKK], to[NDT][2];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
+    for (int kk = 0; kk < NKK; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
     {
       const int g = lane >> 4, i16 = lane & 15;
       const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt) {
         to[dt][0] = KI::toff(BN, row, dt * 32 + col);
         to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
       }
@@ -1918,7 +1922,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
       for (int tt = 0; tt < 2; ++tt) {
         bfv8 fr[8];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) fr[kk] = lds_b128(slot + 8192 * tt + ro[kk]);
+        for (int kk = 0; kk < NKK; ++kk) fr[kk] = lds_b128(slot + 8192 * tt + ro[kk]);
         __builtin_amdgcn_sched_barrier(0);
         f32v16 st, dpt;
 #pragma unroll
@@ -1927,17 +1931,17 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
           dpt[i] = 0.f;
         }
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) st = mfma32(fr[kk], qf[kk], st);
+        for (int kk = 0; kk < NKK; ++kk) st = mfma32(fr[kk], qf[kk], st);
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) fr[kk] = lds_b128(slot + IMG + 8192 * tt + ro[kk]);
+        for (int kk = 0; kk < NKK; ++kk) fr[kk] = lds_b128(slot + IMG + 8192 * tt + ro[kk]);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) dpt = mfma32(fr[kk], df[kk], dpt);
+        for (int kk = 0; kk < NKK; ++kk) dpt = mfma32(fr[kk], df[kk], dpt);
         // K^T operands of the dQ product (keys 32tt + 16s2 .., columns 32dt ..), issued before the VALU
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
+          for (int dt = 0; dt < NDT; ++dt) {
             const char* base = slot + 256 * (32 * tt + 16 * s2);
             const s16v4 lo = lds_tr(base + to[dt][0]), hi = lds_tr(base + to[dt][1]);
             fr[4 * s2 + dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -1970,7 +1974,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
         for (int s2 = 0; s2 < 2; ++s2) {
           const bfv8 db = acc_as_b(st, s2);
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) dqt[dt] = mfma32(fr[4 * s2 + dt], db, dqt[dt]);
+          for (int dt = 0; dt < NDT; ++dt) dqt[dt] = mfma32(fr[4 * s2 + dt], db, dqt[dt]);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1982,7 +1986,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   if (qrow < S) {
     bf16* dqp = a.out + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * a.dq_sh;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         uint2 w;
@@ -2048,7 +2052,12 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   dim3 grid((S + 127) / 128, Hq, B);
   switch (D) {
     case 64: fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a); break;
-    case 96: fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a); break;
+    case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
+      if (a.drop_thresh)
+        fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a);
+      else
+        fa_fwd3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      break;
     case 128: {
       static const int variant = [] {
         const char* e = getenv("LLMT_FA_FWD_VARIANT");
@@ -2060,7 +2069,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
       else if (variant == 1)
         fa_fwd128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (variant == 2)
-        fa_fwd3_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
     } break;
@@ -2128,7 +2137,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       return e ? atoi(e) : 3;
     }();
     if (dq_variant == 3)
-      fa_bwd_dq3_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     else
       fa_bwd_dq128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a, ld);
     static const int variant = [] {
@@ -2144,7 +2153,10 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   if (gqa && !work) return hipErrorInvalidValue;
 #define LLMT_BWD(DD)                                                                              \
   fa_bwd_delta_kernel<DD><<<dgrid, 256, 0, stream>>>(a);                                          \
-  fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                              \
+  if (DD == 96 && !a.drop_thresh) /* Phi-3: the v3 dQ kernel (reads lse / delta directly) */      \
+    fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);                       \
+  else                                                                                            \
+    fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                            \
   if (gqa) {                                                                                      \
     fa_bwd_dkdv_kernel<DD, true><<<grid, 256, 0, stream>>>(a);                                    \
     fa_gqa_reduce_kernel<DD><<<stream_grid((int64_t)B * S * Hkv * (DD / 4), 256), 256, 0, stream>>>(a); \
