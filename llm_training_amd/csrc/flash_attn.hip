@@ -1620,9 +1620,13 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+// The leading s_nop is the trans-use wait state: its inputs are v_exp_f32 results, and hipcc's hazard
+// recognizer does not look inside inline asm. Without it the D=96 instantiation (which schedules an
+// add right behind the exp that produces its operand) read stale values in 4 of every 8 lanes and
+// lost terms of the softmax row sum.
 __device__ __forceinline__ float vadd(float a, float b) {
   float r;
-  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  asm("s_nop 0\n\tv_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
 
@@ -1671,8 +1675,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
   const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
 
   if (T > 0) {
-    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
-    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
+    // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
+    // and past the tensor on the last row of the last head -> zeros instead of a fault
+    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
+    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
     const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
     auto issue = [&](int t) {
       const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
@@ -1880,8 +1886,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
 
   if (T > 0) {
-    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
-    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
+    // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
+    // and past the tensor on the last row of the last head -> zeros instead of a fault
+    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
+    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
     const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
     auto issue = [&](int t) {
       const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
@@ -2050,20 +2058,20 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   a.scale = scale; a.causal = causal; a.window = window;
   set_dropout(a, drop_p, drop_seed);
   dim3 grid((S + 127) / 128, Hq, B);
+  static const int variant = [] {
+    const char* e = getenv("LLMT_FA_FWD_VARIANT");
+    // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907, fwd128 1.043
+    return e ? atoi(e) : 2;
+  }();
   switch (D) {
     case 64: fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a); break;
     case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
-      if (a.drop_thresh)
+      if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a);
       else
         fa_fwd3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       break;
     case 128: {
-      static const int variant = [] {
-        const char* e = getenv("LLMT_FA_FWD_VARIANT");
-        // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907, fwd128 1.043
-        return e ? atoi(e) : 2;
-      }();
       if (a.drop_thresh)  // dropout lives in the generic kernels
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
       else if (variant == 1)
@@ -2151,9 +2159,13 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     return hipGetLastError();
   }
   if (gqa && !work) return hipErrorInvalidValue;
+  static const bool dq96_v3 = [] {
+    const char* e = getenv("LLMT_FA_DQ_VARIANT");
+    return !e || atoi(e) == 3;
+  }();
 #define LLMT_BWD(DD)                                                                              \
   fa_bwd_delta_kernel<DD><<<dgrid, 256, 0, stream>>>(a);                                          \
-  if (DD == 96 && !a.drop_thresh) /* Phi-3: the v3 dQ kernel (reads lse / delta directly) */      \
+  if (DD == 96 && !a.drop_thresh && dq96_v3) /* Phi-3: the v3 dQ kernel (reads lse / delta) */  \
     fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);                       \
   else                                                                                            \
     fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                            \
