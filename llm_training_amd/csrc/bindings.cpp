@@ -19,6 +19,8 @@ hipError_t llmt_rmsnorm_bwd(const void* dy, const void* x, const void* w, const 
                             hipStream_t stream);
 hipError_t llmt_swiglu_fwd(const void* gu, void* c, int64_t T, int I, hipStream_t stream);
 hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu, int64_t T, int I, hipStream_t stream);
+hipError_t llmt_transpose2d(const void* in, void* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo,
+                            hipStream_t stream);
 hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const float* cos_t, const float* sin_t, int64_t T,
                      int nheads, int D, int64_t stride_t, int stride_h, int inverse, hipStream_t stream);
 hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const int64_t* labels,
@@ -171,6 +173,16 @@ at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dc) {
 
 // ---------------------------------------------------------------- RoPE (in place)
 // qkv: [..., T, nh_total, D] with unit stride on D; rotates the first `nheads` heads.
+// out[C, R] = x[R, C]^T for bf16 matrices with R, C multiples of 64 (row-major, unit inner stride)
+void transpose_(const at::Tensor& x, at::Tensor out) {
+  TORCH_CHECK(x.is_cuda() && out.is_cuda() && x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "transpose_: bf16 GPU tensors");
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.stride(1) == 1 && out.stride(1) == 1, "transpose_: 2-D, unit stride");
+  TORCH_CHECK(out.size(0) == x.size(1) && out.size(1) == x.size(0), "transpose_: out must be [C, R]");
+  check(llmt_transpose2d(x.data_ptr(), out.data_ptr(), x.size(0), x.size(1), x.stride(0), out.stride(0), cur_stream()),
+        "transpose2d");
+}
+
 void rope_(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t, int64_t nheads,
            bool inverse) {
   check_bf16_cuda(qkv, "qkv");
@@ -414,6 +426,7 @@ TORCH_LIBRARY(llmt, m) {
       "bool compute_dw) -> (Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dc) -> Tensor");
+  m.def("transpose_(Tensor x, Tensor(a!) out) -> ()");
   m.def("rope_(Tensor(a!) qkv, Tensor pos, Tensor cos, Tensor sin, int nheads, bool inverse) -> ()");
   m.def(
       "cross_entropy_(Tensor(a!) logits, Tensor labels, int vocab_start, int ignore_index, Tensor? lse_in, "
@@ -439,6 +452,7 @@ TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("transpose_", &transpose_);
   m.impl("rope_", &rope_);
   m.impl("cross_entropy_", &cross_entropy_);
   m.impl("adamw_", &adamw_);

@@ -133,3 +133,47 @@ extern "C" hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const
                                                    stride_t, stride_h, sign);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------- 2-D bf16 transpose
+// out[C, R] = in[R, C]^T (row-major, leading dims ldi / ldo in elements). 64 x 64 tiles through LDS:
+// every global access is a 16-byte vector (two per thread each way); the LDS tile rows are padded to
+// 66 elements so the eight 2-byte column reads of one output vector land on distinct banks across the
+// wave. Used to hand hipBLASLt its fastest (TN: both operands contraction-contiguous) layout for the
+// linear-layer input / weight gradients.
+namespace llmt {
+__global__ __launch_bounds__(256) void transpose64_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                          int64_t ldi, int64_t ldo) {
+  __shared__ uint16_t tile[64][66];
+  const int tid = threadIdx.x, cv = (tid & 7) * 8, rr = tid >> 3;
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = rr + 32 * h;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + (r0 + r) * ldi + c0 + cv);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<uint32_t*>(&tile[r][cv + 2 * j]) = w[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int oc = rr + 32 * h;  // output row = input column
+    bf16x8 v;
+    uint16_t* e = reinterpret_cast<uint16_t*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = tile[cv + j][oc];
+    *reinterpret_cast<bf16x8*>(out + (c0 + oc) * ldo + r0 + cv) = v;
+  }
+}
+}  // namespace llmt
+
+extern "C" hipError_t llmt_transpose2d(const void* in, void* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo,
+                                       hipStream_t stream) {
+  if (R % 64 || C % 64 || ldi % 8 || ldo % 8 || ldi < C || ldo < R) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return hipErrorInvalidValue;
+  if (R == 0 || C == 0) return hipSuccess;
+  if (R / 64 > 65535) return hipErrorInvalidValue;
+  llmt::transpose64_kernel<<<dim3((unsigned)(C / 64), (unsigned)(R / 64)), 256, 0, stream>>>(
+      (const llmt::bf16*)in, (llmt::bf16*)out, ldi, ldo);
+  return hipGetLastError();
+}

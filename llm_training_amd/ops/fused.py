@@ -72,6 +72,32 @@ def _ld(t: torch.Tensor) -> int:
     return t.stride(0) if t.size(0) > 1 else max(8, (t.size(1) + 7) // 8 * 8)
 
 
+# Backward layouts through materialised transposes (csrc/elementwise.hip transpose, ~4.7 TB/s).
+# hipBLASLt is fastest when both operands are contraction-contiguous (TN, the forward's layout); the
+# backward GEMMs of a linear layer are NN (dgrad) and NT (wgrad: the contraction runs over tokens, the
+# strided dimension of both token-major operands). Measured at M = 32768 on the Llama-3-8B projections
+# (profiles/r2_gemm_transposed_layouts.jsonl, transposes included):
+#   dgrad  NN -> TN with W^T        qkv 1.41->1.27  o 0.89->0.73  gate_up 5.50->5.08  down 2.92->2.47 ms
+#   wgrad  NT -> NN with dy^T       qkv 1.64->1.45  o 0.95->0.89                      down 3.82->3.61 ms
+#          NT -> TT with x^T                                      gate_up 6.31->5.52 ms
+# The weight transpose costs N*K regardless of M, so the dgrad form needs a large token count.
+# LLMT_GEMM_TRANSPOSE=0 keeps the direct layouts.
+TRANSPOSE_LAYOUTS = [os.environ.get("LLMT_GEMM_TRANSPOSE", "1").strip().lower() not in ("0", "false", "off")]
+_TR_DGRAD_MIN_M = 16384
+_TR_WGRAD_MIN_M = 4096
+
+
+def _tr_ok(*ts: torch.Tensor) -> bool:
+    return all(t.size(0) % 64 == 0 and t.size(1) % 64 == 0 for t in ts)
+
+
+def transpose(x: torch.Tensor) -> torch.Tensor:
+    """[R, C] -> contiguous [C, R] (bf16 GPU tensors with R, C multiples of 64: the HIP kernel)."""
+    out = torch.empty(x.shape[1], x.shape[0], device=x.device, dtype=x.dtype)
+    lib().transpose_(x, out)
+    return out
+
+
 def _path(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> str:
     mode = GEMM_MODES.get(layout, "blas")
     if mode == "blas" or not all(_gemm_operand_ok(t) for t in ts) or not use_native(ts[0]):
@@ -111,7 +137,11 @@ def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
-    if path == "lt":  # column-major: dx^T (K x M) = w^T (K x N) . dy^T (N x M)
+    if path == "lt" and TRANSPOSE_LAYOUTS[0] and M >= _TR_DGRAD_MIN_M and _tr_ok(dy2, w):
+        # TN: dx^T (K x M) = (w^T stored [K, N])^T-op . dy^T, both operands N-contiguous
+        wt = transpose(w)
+        lib().gemm_lt(wt, dy2, out, True, False, K, M, N, N, _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
+    elif path == "lt":  # column-major: dx^T (K x M) = w^T (K x N) . dy^T (N x M)
         lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
     else:
         lib().gemm_(dy2, w, out, False, True, False)
@@ -125,6 +155,14 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
     path = _path("wgrad", dy.shape[0], x.shape[1], dy, x)
     M, N = dy.shape
     K = x.shape[1]
+    if path == "lt" and TRANSPOSE_LAYOUTS[0] and M >= _TR_WGRAD_MIN_M and _tr_ok(dy, x):
+        if N >= 4 * K:  # wide outputs (gate_up, lm_head): TT with x^T (the smaller operand)
+            xt = transpose(x)
+            lib().gemm_lt(xt, dy, out.view(N, K), True, True, K, N, M, M, _ld(dy), K, accumulate, ALLOW_STREAMK[0])
+        else:  # NN with dy^T
+            dyt = transpose(dy)
+            lib().gemm_lt(x, dyt, out.view(N, K), False, False, K, N, M, _ld(x), M, K, accumulate, ALLOW_STREAMK[0])
+        return True
     if path == "lt":  # column-major: dW^T (K x N) = x^T (K x M) . dy (M x N)
         lib().gemm_lt(x, dy, out.view(N, K), False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, ALLOW_STREAMK[0])
         return True

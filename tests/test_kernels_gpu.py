@@ -261,6 +261,39 @@ def test_gemm_strided_operands():
     assert cw[:, N:].abs().max().item() == 0
 
 
+def test_transpose_kernel_strided():
+    """csrc/elementwise.hip transpose: [R, C] (row-strided view) -> [C, R], bit exact."""
+    torch.manual_seed(0)
+    xw = torch.randn(320, 256 + 64, device=DEV).bfloat16()
+    x = xw[:, 32:32 + 256]
+    out = torch.empty(256, 320, device=DEV, dtype=torch.bfloat16)
+    lib().transpose_(x, out)
+    assert torch.equal(out, x.t().contiguous())
+
+
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("N,K", [(256, 192), (1024, 192)])
+def test_backward_gemms_transposed_layouts(monkeypatch, out_dtype, N, K):
+    """dgrad as TN with W^T (M >= 16384) and wgrad as NN with dy^T (N < 4K) / TT with x^T (N >= 4K),
+    both accumulating, against fp32 products; the direct layouts give the same result."""
+    import llm_training_amd.ops.fused as fused
+    monkeypatch.setattr(fused, "GEMM_MODES", {"fwd": "lt", "dgrad": "lt", "wgrad": "lt"})
+    torch.manual_seed(0)
+    M = 16384
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    for tr in (True, False):
+        monkeypatch.setattr(fused, "TRANSPOSE_LAYOUTS", [tr])
+        dx = fused.mm_nn(dy, w)
+        assert _rel(dx, dy.float() @ w.float()) < 1e-2
+        c0 = torch.randn(N, K, device=DEV).to(out_dtype)
+        dw = c0.clone()
+        assert fused.wgrad_into(dw, dy, x, True)
+        want = dy.float().t() @ x.float() + c0.float()
+        assert _rel(dw, want) < (1e-4 if out_dtype == torch.float32 else 1e-2)
+
+
 @pytest.mark.parametrize("mode", ["hip", "lt", "blas"])
 def test_linear_gemm_paths_grads_into_grad_buffer(monkeypatch, mode):
     """Every GEMM path (own kernel, tuned hipBLASLt, torch) through the linear op, with fp32 weight-grad
