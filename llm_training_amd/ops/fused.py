@@ -124,8 +124,20 @@ def mm_nt(x2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) ->
     return y
 
 
-def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """dy2 [M, N] @ w [N, K] -> [M, K] (input gradient of a linear layer)."""
+def weight_t(w: torch.Tensor, rows: int) -> torch.Tensor | None:
+    """w^T for the TN input-gradient GEMM when ``rows`` tokens in total will be multiplied by ``w``
+    (chunked callers such as the fused lm_head + CE transpose once for all chunks); None otherwise."""
+    if not TRANSPOSE_LAYOUTS[0] or rows < _TR_DGRAD_MIN_M or not _tr_ok(w):
+        return None
+    if _path("dgrad", w.shape[0], w.shape[1], w) != "lt":
+        return None
+    return transpose(w)
+
+
+def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+          wt: torch.Tensor | None = None) -> torch.Tensor:
+    """dy2 [M, N] @ w [N, K] -> [M, K] (input gradient of a linear layer); ``wt``: w^T from
+    :func:`weight_t`, shared by the chunks of one product."""
     path = _path("dgrad", dy2.shape[1], w.shape[1], dy2, w)
     if out is not None and path != "blas" and not _gemm_operand_ok(out):
         path = "blas"
@@ -137,10 +149,11 @@ def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
-    if path == "lt" and TRANSPOSE_LAYOUTS[0] and M >= _TR_DGRAD_MIN_M and _tr_ok(dy2, w):
+    if path == "lt" and (wt is not None or (TRANSPOSE_LAYOUTS[0] and M >= _TR_DGRAD_MIN_M and _tr_ok(dy2, w))):
         # TN: dx^T (K x M) = (w^T stored [K, N])^T-op . dy^T, both operands N-contiguous
-        wt = transpose(w)
-        lib().gemm_lt(wt, dy2, out, True, False, K, M, N, N, _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
+        if wt is None:
+            wt = transpose(w)
+        lib().gemm_lt(wt, dy2, out, True, False, K, M, N, _ld(wt), _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
     elif path == "lt":  # column-major: dx^T (K x M) = w^T (K x N) . dy^T (N x M)
         lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
     else:
@@ -599,13 +612,14 @@ class _FusedLinearCEFn(Function):
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dh = torch.empty_like(h) if need_h else None
         dw = torch.empty(w.shape, device=w.device, dtype=w.dtype) if need_w else None
+        wt = weight_t(w, N) if need_h and N > chunk else None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, inv_n, True)
             loss_rows[s0:s1] = lr
             if need_h:
-                mm_nn(lg, w, out=dh[s0:s1])
+                mm_nn(lg, w, out=dh[s0:s1], wt=wt)
             if need_w and not wgrad_into(dw, lg, h[s0:s1], s0 > 0):
                 if s0 == 0:
                     torch.mm(lg.t(), h[s0:s1], out=dw)
@@ -696,11 +710,12 @@ class _LinearLogpsFn(Function):
         dh = torch.empty_like(h)
         coef = (-g).float().contiguous()
         dw_acc = None
+        wt = weight_t(w, N) if N > chunk else None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, coef[s0:s1], None, True)
-            mm_nn(lg, w, out=dh[s0:s1])
+            mm_nn(lg, w, out=dh[s0:s1], wt=wt)
             if ctx.needs_input_grad[1]:
                 r = _wgrad_mm(w, lg.t(), h[s0:s1])
                 if r is not None:

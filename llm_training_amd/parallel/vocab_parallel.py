@@ -20,7 +20,7 @@ import torch
 import torch.distributed as dist
 from torch.autograd import Function
 
-from ..ops.fused import _apply_weight_grad, _wgrad_mm, mm_nn, mm_nt, wgrad_into
+from ..ops.fused import _apply_weight_grad, _wgrad_mm, mm_nn, mm_nt, weight_t, wgrad_into
 from ..ops.native import lib, use_native
 
 
@@ -93,12 +93,13 @@ class _VPFusedCE(Function):
         dw = dw_full[:n_valid] if need_w else None
         if need_w and n_valid < w_full.shape[0]:
             dw_full[n_valid:].zero_()
+        wt = weight_t(w, N) if need_h and native and N > chunk else None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), None, inv_n, native)
             if need_h:
-                mm_nn(lg, w, out=dh[s0:s1])
+                mm_nn(lg, w, out=dh[s0:s1], wt=wt)
             if need_w and not wgrad_into(dw, lg, h[s0:s1], s0 > 0):
                 if s0 == 0:
                     torch.mm(lg.t(), h[s0:s1], out=dw)
