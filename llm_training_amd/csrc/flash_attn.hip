@@ -817,8 +817,8 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 //   ld[((b*Hq + h)*nT + t)*128 + {0..31: -lse/scale | 32..63: -delta | 64..95: segment id}]
 constexpr int kLdTile = 128;
 
+template <int D>
 __global__ __launch_bounds__(256) void fa_bwd_prep128_kernel(AttnArgs a, float* ld) {
-  constexpr int D = 128;
   const int nT = (a.S + 31) / 32;
   const int64_t nrows = (int64_t)a.B * a.Hq * nT * 32;
   const float inv_scale = 1.f / a.scale;
@@ -896,9 +896,13 @@ __device__ __forceinline__ void ring_barrier() { asm volatile("s_waitcnt lgkmcnt
 
 // grid: ceil(S/128) * Hkv * B blocks (1-D), 4 waves x 32 keys; query tiles of 32 rows over all q heads of
 // the kv group; NS-slot LDS-DMA ring.
-template <int V>
+// D = 96 (Phi-3) runs the same structure on 256-byte LDS rows: the DMA rows read 64 bytes past each
+// 192-byte row (never past the tensor: the descriptors end at the last row's D elements) and only the
+// first D / 16 k-steps / D / 32 output tiles are used.
+template <int V, int D = 128>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, const float* ld) {
-  constexpr int D = 128, BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
+  constexpr int NKK = D / 16, NDT = D / 32;
+  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
   constexpr int NDMA = 5;  // DMA instructions per wave per tile: Q 2, dO 2, row constants 1
   using QI = Img<128>;
   __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
@@ -918,18 +922,18 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
   const int sk = (a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;
   const float sl2 = a.scale * kLog2e;
 
-  bfv8 kf[8], vf[8];
+  bfv8 kf[NKK], vf[NKK];
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
+  for (int kk = 0; kk < NKK; ++kk) {
     kf[kk] = gload8(kp + (int64_t)min(kr, S - 1) * a.k_ss + kk * 16 + hh * 8, kr < S);
     vf[kk] = gload8(vp + (int64_t)min(kr, S - 1) * a.v_ss + kk * 16 + hh * 8, kr < S);
   }
   // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
-  f32v16 dkt[4], dvt[4];
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
+  f32v16 dkt[NDT], dvt[NDT];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       dkt[dt][i] = 0.f;
@@ -966,9 +970,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
       const int h = hk * grp + iss_g;
       const int64_t rows_left = S - q0;
       const Rsrc qrs = make_rsrc4(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_ss,
-                                  rows_left * a.q_ss * 2);
+                                  ((rows_left - 1) * a.q_ss + D) * 2);
       const Rsrc drs = make_rsrc4(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh + (int64_t)q0 * a.d_ss,
-                                  rows_left * a.d_ss * 2);
+                                  ((rows_left - 1) * a.d_ss + D) * 2);
       const Rsrc lrs = make_rsrc4(ld + (((int64_t)b * a.Hq + h) * nT + (q0 >> 5)) * kLdTile, kLdTile * 4);
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
@@ -1031,26 +1035,26 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
     };
     // lane-constant LDS byte offsets inside a 32-row image, computed once and kept opaque so hipcc
     // does not re-derive the swizzle for every read inside the loop (it did: ~5 VALU per read)
-    int ro[8], to[4][2];
+    int ro[NKK], to[NDT][2];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) ro[kk] = QI::roff(r, 2 * kk + hh);
+    for (int kk = 0; kk < NKK; ++kk) ro[kk] = QI::roff(r, 2 * kk + hh);
     {
       const int g = lane >> 4, i16 = lane & 15;
       const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt) {
         to[dt][0] = QI::toff(BM, row, dt * 32 + col);
         to[dt][1] = QI::toff(BM, row + 8, dt * 32 + col);
       }
     }
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(ro[kk]));
+    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(ro[kk]));
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
+    for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
     auto rows = [&](int t, bfv8* qr, bfv8* dr) {
       const char* slot = sl(t);
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
+      for (int kk = 0; kk < NKK; ++kk) {
         const char* p = slot + ro[kk];  // one VGPR address; the dO image is an immediate offset away
         qr[kk] = lds_b128(p);
         dr[kk] = lds_b128(p + IMG);
@@ -1058,9 +1062,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
     };
     // A operands of the accumulator-as-B products from tile image pair `slot`: rows 16*s2..,
     // columns 32*dt.. of Q (dK) and dO (dV); 8 VGPR addresses per tile, everything else immediates
-    auto trA2 = [&](const char* slot, bfv8 (&tq)[2][4], bfv8 (&td)[2][4]) {
+    auto trA2 = [&](const char* slot, bfv8 (&tq)[2][NDT], bfv8 (&td)[2][NDT]) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt) {
         const char* p0 = slot + to[dt][0];
         const char* p1 = slot + to[dt][1];
 #pragma unroll
@@ -1079,12 +1083,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
     wait_vm<NDMA * (NS - 4)>();
     ring_barrier();
 
-    bfv8 qr[8], dr[8];
+    bfv8 qr[NKK], dr[NKK];
     f32v16 sacc, dacc;
     rows(0, qr, dr);
     init(0, sacc, dacc);
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
+    for (int kk = 0; kk < NKK; ++kk) {
       sacc = mfma32(qr[kk], kf[kk], sacc);
       dacc = mfma32(dr[kk], vf[kk], dacc);
     }
@@ -1096,10 +1100,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
       f32v16 sn, dn;
       init(t, sn, dn);
       const char* pslot = sl(t - 1);
-      bfv8 trd[2][4], trq[2][4];
+      bfv8 trd[2][NDT], trq[2][NDT];
       trA2(pslot, trq, trd);
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
+      for (int kk = 0; kk < NKK; ++kk) {
         sn = mfma32(qr[kk], kf[kk], sn);
         dn = mfma32(dr[kk], vf[kk], dn);
       }
@@ -1128,7 +1132,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
+        for (int dt = 0; dt < NDT; ++dt) {
           dvt[dt] = mfma32(trd[s2][dt], pb[s2], dvt[dt]);
           dkt[dt] = mfma32(trq[s2][dt], db[s2], dkt[dt]);
         }
@@ -1152,7 +1156,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
     bf16* dkp = a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh;
     bf16* dvp = a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int d = dt * 32 + 8 * c + 4 * hh;
@@ -2089,7 +2093,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
 // floats of the `delta` workspace llmt_flash_attn_bwd needs
 extern "C" int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D) {
   const int64_t n = (int64_t)B * Hq * S;
-  return D == 128 ? n + (int64_t)B * Hq * ((S + 31) / 32) * kLdTile : n;
+  return (D == 128 || D == 96) ? n + (int64_t)B * Hq * ((S + 31) / 32) * kLdTile : n;
 }
 
 extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
@@ -2134,11 +2138,18 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   const int64_t nrows = (int64_t)B * S * Hq;
   dim3 grid((S + 127) / 128, Hq, B);
   const int dgrid = stream_grid(nrows, 256);
-  if (D == 128 && !a.drop_thresh) {
+  static const bool d96_v3 = getenv("LLMT_FA_D96_GENERIC") == nullptr;  // A/B switch for D = 96
+  if ((D == 128 || (D == 96 && d96_v3)) && !a.drop_thresh) {
     // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws)
     float* ld = delta + nrows;
     const int64_t nT = (S + 31) / 32;
-    fa_bwd_prep128_kernel<<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
+    if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
+      fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
+      fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      return hipGetLastError();
+    }
+    fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
     static const int dq_variant = [] {
       // B4 S8192 Hq32 Hkv8 backward: 9.16 ms with dq3 vs 9.66 ms with the dq128 ring kernel
       const char* e = getenv("LLMT_FA_DQ_VARIANT");
@@ -2159,16 +2170,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     return hipGetLastError();
   }
   if (gqa && !work) return hipErrorInvalidValue;
-  static const bool dq96_v3 = [] {
-    const char* e = getenv("LLMT_FA_DQ_VARIANT");
-    return !e || atoi(e) == 3;
-  }();
 #define LLMT_BWD(DD)                                                                              \
   fa_bwd_delta_kernel<DD><<<dgrid, 256, 0, stream>>>(a);                                          \
-  if (DD == 96 && !a.drop_thresh && dq96_v3) /* Phi-3: the v3 dQ kernel (reads lse / delta) */  \
-    fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);                       \
-  else                                                                                            \
-    fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                            \
+  fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                              \
   if (gqa) {                                                                                      \
     fa_bwd_dkdv_kernel<DD, true><<<grid, 256, 0, stream>>>(a);                                    \
     fa_gqa_reduce_kernel<DD><<<stream_grid((int64_t)B * S * Hkv * (DD / 4), 256), 256, 0, stream>>>(a); \

@@ -55,7 +55,7 @@ def _check(B, S, Hq, Hkv, D, seg, causal=True, window=-1):
 @given(S=st.sampled_from([257, 1000, 2048, 3001]),
        lengths=st.lists(st.integers(1, 1500), min_size=1, max_size=6),
        pad=st.integers(0, 200), left=st.booleans(),
-       geo=st.sampled_from([(4, 4, 128), (8, 2, 128), (4, 2, 64), (4, 4, 96)]), causal=st.booleans())
+       geo=st.sampled_from([(4, 4, 128), (8, 2, 128), (4, 2, 64), (4, 4, 96), (8, 2, 96)]), causal=st.booleans())
 def test_varlen_random_layouts(S, lengths, pad, left, geo, causal):
     Hq, Hkv, D = geo
     pad = min(pad, S - 1)
