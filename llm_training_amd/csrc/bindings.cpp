@@ -405,8 +405,8 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   auto delta = at::empty({llmt_flash_attn_bwd_ws((int)B, (int)S, (int)Hq, (int)D)}, q.options().dtype(at::kFloat));
   TORCH_CHECK(dout.strides() == o.strides(), "flash_attn_bwd: dout must share O's layout");
   at::Tensor work;  // fp32 per-q-head dK/dV partials, only needed for GQA
-  // only the generic kernels (D = 64, dropout, or LLMT_FA_D96_GENERIC) reduce GQA through partials
-  if (Hq != Hkv && (D == 64 || dropout_p > 0 || (D == 96 && std::getenv("LLMT_FA_D96_GENERIC"))))
+  // only the generic kernels (dropout, or LLMT_FA_D96_GENERIC at D 64 / 96) reduce GQA through partials
+  if (Hq != Hkv && (dropout_p > 0 || (D != 128 && std::getenv("LLMT_FA_D96_GENERIC"))))
     work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
   check(llmt_flash_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                             lse.data_ptr<float>(), delta.data_ptr<float>(), sp, dq.data_ptr(), dk.data_ptr(),

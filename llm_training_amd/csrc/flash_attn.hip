@@ -2068,7 +2068,12 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
     return e ? atoi(e) : 2;
   }();
   switch (D) {
-    case 64: fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a); break;
+    case 64:  // the v3 structure on 128-byte rows (256-byte LDS pitch)
+      if (a.drop_thresh || variant == 0)
+        fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a);
+      else
+        fa_fwd3_kernel<64><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      break;
     case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a);
@@ -2093,7 +2098,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
 // floats of the `delta` workspace llmt_flash_attn_bwd needs
 extern "C" int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D) {
   const int64_t n = (int64_t)B * Hq * S;
-  return (D == 128 || D == 96) ? n + (int64_t)B * Hq * ((S + 31) / 32) * kLdTile : n;
+  return (D == 128 || D == 96 || D == 64) ? n + (int64_t)B * Hq * ((S + 31) / 32) * kLdTile : n;
 }
 
 extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
@@ -2138,8 +2143,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   const int64_t nrows = (int64_t)B * S * Hq;
   dim3 grid((S + 127) / 128, Hq, B);
   const int dgrid = stream_grid(nrows, 256);
-  static const bool d96_v3 = getenv("LLMT_FA_D96_GENERIC") == nullptr;  // A/B switch for D = 96
-  if ((D == 128 || (D == 96 && d96_v3)) && !a.drop_thresh) {
+  static const bool small_v3 = getenv("LLMT_FA_D96_GENERIC") == nullptr;  // A/B switch for D = 64 / 96
+  if ((D == 128 || ((D == 96 || D == 64) && small_v3)) && !a.drop_thresh) {
     // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws)
     float* ld = delta + nrows;
     const int64_t nT = (S + 31) / 32;
@@ -2147,6 +2152,12 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      return hipGetLastError();
+    }
+    if (D == 64) {
+      fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
+      fa_bwd_dq3_kernel<64><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       return hipGetLastError();
     }
     fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
