@@ -195,6 +195,14 @@ class DataParallelEngine:
         # the optimizer / norm kernels take fp32 or bf16 gradients: native on any GPU
         self.native = self.cuda and use_native(torch.empty(0, device=dev, dtype=torch.bfloat16))
         self.comm_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.overlap) else None
+        if self.cuda and (self.dp > 1 or self.pc.tp_size > 1):
+            # RCCL kernels share the CUs with the GEMMs of the compute stream: hipBLASLt's stream-K
+            # solutions assume every workgroup of their launch is resident (partial tiles are handed
+            # between workgroups that spin on flags), so with a collective holding CUs a fix-up can
+            # wait on a workgroup that has not started. Non-stream-K solutions cost 0.8 % on one GPU
+            # (20.39k vs 20.55k tok/s, profiles/r2_workloads_1gpu.jsonl); LLMT_GEMM_STREAMK=1 overrides.
+            from ..ops.fused import set_streamk
+            set_streamk(False)
         # AdamW runs on its own stream: unit i's update overlaps the next step's forward of units < i
         # (memory-bound optimizer beside compute-bound GEMMs); each unit's forward waits for its own
         # update through the same per-unit event the stage-1/2 all-gather uses
