@@ -17,6 +17,9 @@ from llm_training_amd.ops.native import lib  # noqa: E402
 M0 = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 PROJ = [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
         ("lm_head_chunk8192", 128256, 4096)]
+if len(sys.argv) > 2 and sys.argv[2] == "phi3":  # Phi-3-mini: hidden 3072, intermediate 8192, vocab 32064
+    PROJ = [("qkv", 9216, 3072), ("o", 3072, 3072), ("gate_up", 16384, 3072), ("down", 3072, 8192),
+            ("lm_head_chunk8192", 32064, 3072)]
 dev = torch.device("cuda", 0)
 sk = fused.ALLOW_STREAMK[0]
 fused.TRANSPOSE_LAYOUTS[0] = False  # the *_nn / *_nt baselines below are the direct layouts
@@ -51,7 +54,7 @@ for name, N, K in PROJ:
     dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
     dw = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
     wt, dyt, xt = tr(w), tr(dy), tr(x)
-    r = {"shape": name, "M": M, "N": N, "K": K}
+    r = {"shape": name, "M": M, "N": N, "K": K, "model": sys.argv[2] if len(sys.argv) > 2 else "llama3-8b"}
     f = 2 * M * N * K
     # dgrad
     r["dgrad_nn"] = timeit(lambda: fused.mm_nn(dy, w, dx))

@@ -18,6 +18,7 @@ flash-attn calls of src/llm_training/ops/attention_op.py.
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
 
@@ -26,6 +27,8 @@ from torch.autograd import Function
 
 from . import reference as ref
 from .native import lib, use_native
+
+log = logging.getLogger(__name__)
 
 # ----------------------------------------------------------------------------- GEMM dispatch
 # The three GEMMs of a linear layer (fwd x @ W^T, dgrad dy @ W, wgrad dy^T @ x) go to one of:
@@ -75,16 +78,20 @@ def _ld(t: torch.Tensor) -> int:
 # Backward layouts through materialised transposes (csrc/elementwise.hip transpose, ~4.7 TB/s).
 # hipBLASLt is fastest when both operands are contraction-contiguous (TN, the forward's layout); the
 # backward GEMMs of a linear layer are NN (dgrad) and NT (wgrad: the contraction runs over tokens, the
-# strided dimension of both token-major operands). Measured at M = 32768 on the Llama-3-8B projections
-# (profiles/r2_gemm_transposed_layouts.jsonl, transposes included):
-#   dgrad  NN -> TN with W^T        qkv 1.41->1.27  o 0.89->0.73  gate_up 5.50->5.08  down 2.92->2.47 ms
-#   wgrad  NT -> NN with dy^T       qkv 1.64->1.45  o 0.95->0.89                      down 3.82->3.61 ms
-#          NT -> TT with x^T                                      gate_up 6.31->5.52 ms
-# The weight transpose costs N*K regardless of M, so the dgrad form needs a large token count.
-# LLMT_GEMM_TRANSPOSE=0 keeps the direct layouts.
+# strided dimension of both token-major operands). Measured at M = 32768 (transposes included,
+# profiles/r2_gemm_transposed_layouts*.jsonl):
+#   Llama-3-8B dgrad  NN -> TN with W^T   qkv 1.41->1.27  o 0.89->0.73  gate_up 5.50->5.08  down 2.92->2.47 ms
+#              wgrad  NT -> NN with dy^T  qkv 1.64->1.45  o 0.95->0.89  down 3.82->3.61;  TT with x^T gate_up 6.31->5.52
+#   Phi-3-mini wgrad  o (3072 x 3072): NT 0.61, NN 1.05, TT 1.02 — the best layout is shape-specific
+# so each (kind, shape) is decided once by timing its candidate layouts on the live operands (the first
+# non-accumulating call; 3 runs each, transposes included) and cached; deterministic mode and
+# LLMT_GEMM_LAYOUT_TUNE=0 use the static rule below instead. LLMT_GEMM_TRANSPOSE=0 keeps the direct
+# layouts. The weight transpose costs N*K regardless of M, so the dgrad form needs a large token count.
 TRANSPOSE_LAYOUTS = [os.environ.get("LLMT_GEMM_TRANSPOSE", "1").strip().lower() not in ("0", "false", "off")]
+_LAYOUT_TUNE = os.environ.get("LLMT_GEMM_LAYOUT_TUNE", "1").strip().lower() not in ("0", "false", "off")
 _TR_DGRAD_MIN_M = 16384
 _TR_WGRAD_MIN_M = 4096
+_LAYOUT_CACHE: dict[tuple, str] = {}
 
 
 def _tr_ok(*ts: torch.Tensor) -> bool:
@@ -96,6 +103,33 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.shape[1], x.shape[0], device=x.device, dtype=x.dtype)
     lib().transpose_(x, out)
     return out
+
+
+def _layout(key: tuple, variants: dict, default: str, can_time: bool) -> str:
+    """Cached layout for ``key``; on first sight (and when the call may overwrite its output) every
+    variant in ``variants`` (name -> zero-argument launcher producing the same result) is timed on the
+    current stream and the fastest is kept. Otherwise ``default``."""
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is not None:
+        return hit
+    if not (can_time and _LAYOUT_TUNE and len(variants) > 1) or os.environ.get("LLMT_DETERMINISTIC") == "1" \
+            or torch.cuda.is_current_stream_capturing():
+        return default
+    best, best_ms = default, float("inf")
+    for name, fn in variants.items():
+        fn()  # warm-up (and hipBLASLt's own solution choice for the problem)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            fn()
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / 3
+        if ms < best_ms:
+            best, best_ms = name, ms
+    _LAYOUT_CACHE[key] = best
+    log.debug("GEMM layout %s -> %s (%.3f ms)", key, best, best_ms)
+    return best
 
 
 def _path(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> str:
@@ -150,10 +184,21 @@ def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
     if out is None:
         out = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
     if path == "lt" and (wt is not None or (TRANSPOSE_LAYOUTS[0] and M >= _TR_DGRAD_MIN_M and _tr_ok(dy2, w))):
-        # TN: dx^T (K x M) = (w^T stored [K, N])^T-op . dy^T, both operands N-contiguous
-        if wt is None:
-            wt = transpose(w)
-        lib().gemm_lt(wt, dy2, out, True, False, K, M, N, _ld(wt), _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
+        sk = ALLOW_STREAMK[0]
+
+        def tn():  # dx^T (K x M) = (w^T stored [K, N])^T-op . dy^T, both operands N-contiguous
+            lib().gemm_lt(wt if wt is not None else transpose(w), dy2, out, True, False, K, M, N, N,
+                          _ld(dy2), _ld(out), False, sk)
+
+        def nn():
+            lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, sk)
+
+        if wt is not None:  # transposed once for several chunks: TN
+            tn()
+        elif _layout(("dgrad", M, N, K, _ld(dy2), _ld(out), sk), {"tn": tn, "nn": nn}, "tn", True) == "tn":
+            tn()
+        else:
+            nn()
     elif path == "lt":  # column-major: dx^T (K x M) = w^T (K x N) . dy^T (N x M)
         lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
     else:
@@ -169,12 +214,21 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
     M, N = dy.shape
     K = x.shape[1]
     if path == "lt" and TRANSPOSE_LAYOUTS[0] and M >= _TR_WGRAD_MIN_M and _tr_ok(dy, x):
-        if N >= 4 * K:  # wide outputs (gate_up, lm_head): TT with x^T (the smaller operand)
-            xt = transpose(x)
-            lib().gemm_lt(xt, dy, out.view(N, K), True, True, K, N, M, M, _ld(dy), K, accumulate, ALLOW_STREAMK[0])
-        else:  # NN with dy^T
-            dyt = transpose(dy)
-            lib().gemm_lt(x, dyt, out.view(N, K), False, False, K, N, M, _ld(x), M, K, accumulate, ALLOW_STREAMK[0])
+        sk, o2 = ALLOW_STREAMK[0], out.view(N, K)
+
+        def nt():  # dW^T (K x N) = x^T (K x M) . dy (M x N), straight from the token-major operands
+            lib().gemm_lt(x, dy, o2, False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, sk)
+
+        def tt():  # x^T materialised
+            lib().gemm_lt(transpose(x), dy, o2, True, True, K, N, M, M, _ld(dy), K, accumulate, sk)
+
+        def nn():  # dy^T materialised
+            lib().gemm_lt(x, transpose(dy), o2, False, False, K, N, M, _ld(x), M, K, accumulate, sk)
+
+        # static rule: wide outputs (gate_up, lm_head) transpose the smaller operand x, the rest dy
+        default = "tt" if N >= 4 * K else "nn"
+        key = ("wgrad", M, N, K, _ld(x), _ld(dy), out.dtype, sk)
+        {"nt": nt, "tt": tt, "nn": nn}[_layout(key, {"nt": nt, "tt": tt, "nn": nn}, default, not accumulate)]()
         return True
     if path == "lt":  # column-major: dW^T (K x N) = x^T (K x M) . dy (M x N)
         lib().gemm_lt(x, dy, out.view(N, K), False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, ALLOW_STREAMK[0])

@@ -273,11 +273,16 @@ def test_transpose_kernel_strided():
 
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("N,K", [(256, 192), (1024, 192)])
-def test_backward_gemms_transposed_layouts(monkeypatch, out_dtype, N, K):
-    """dgrad as TN with W^T (M >= 16384) and wgrad as NN with dy^T (N < 4K) / TT with x^T (N >= 4K),
-    both accumulating, against fp32 products; the direct layouts give the same result."""
+@pytest.mark.parametrize("forced", [None, "tn/nt", "nn/tt", "tn/nn"])
+def test_backward_gemms_transposed_layouts(monkeypatch, out_dtype, N, K, forced):
+    """dgrad (NN, or TN with W^T at M >= 16384) and wgrad (NT, NN with dy^T, TT with x^T), each layout
+    forced and the timed per-shape choice, with accumulation, against fp32 products."""
     import llm_training_amd.ops.fused as fused
     monkeypatch.setattr(fused, "GEMM_MODES", {"fwd": "lt", "dgrad": "lt", "wgrad": "lt"})
+    monkeypatch.setattr(fused, "_LAYOUT_CACHE", {})
+    if forced is not None:
+        dg, wg = forced.split("/")
+        monkeypatch.setattr(fused, "_layout", lambda key, variants, default, can_time: dg if key[0] == "dgrad" else wg)
     torch.manual_seed(0)
     M = 16384
     dy = torch.randn(M, N, device=DEV).bfloat16()
@@ -287,11 +292,15 @@ def test_backward_gemms_transposed_layouts(monkeypatch, out_dtype, N, K):
         monkeypatch.setattr(fused, "TRANSPOSE_LAYOUTS", [tr])
         dx = fused.mm_nn(dy, w)
         assert _rel(dx, dy.float() @ w.float()) < 1e-2
+        dw = torch.empty(N, K, device=DEV, dtype=out_dtype)
+        assert fused.wgrad_into(dw, dy, x, False)  # (times the layouts when not forced)
         c0 = torch.randn(N, K, device=DEV).to(out_dtype)
         dw = c0.clone()
         assert fused.wgrad_into(dw, dy, x, True)
         want = dy.float().t() @ x.float() + c0.float()
         assert _rel(dw, want) < (1e-4 if out_dtype == torch.float32 else 1e-2)
+    if forced is None:
+        assert any(k[0] == "wgrad" for k in fused._LAYOUT_CACHE)
 
 
 @pytest.mark.parametrize("mode", ["hip", "lt", "blas"])
