@@ -887,6 +887,14 @@ __device__ __forceinline__ void dma4(const Rsrc& r, const char* lds, int voff) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "s"(lds_addr(lds)), "v"(voff), "s"(r.w) : "memory");
 }
+// the same with the descriptor forced to SGPRs (a kernel under SGPR pressure may keep it in VGPRs,
+// which the asm's "s" operand does not accept)
+__device__ __forceinline__ Rsrc sgpr_rsrc(const Rsrc& r) {
+  Rsrc o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o.w[i] = __builtin_amdgcn_readfirstlane(r.w[i]);
+  return o;
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -1167,6 +1175,257 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
         wv.y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
         *reinterpret_cast<uint2*>(dkp + d) = wk;
         *reinterpret_cast<uint2*>(dvp + d) = wv;
+      }
+  }
+}
+
+// ============================================================================ backward dK/dV, role-split pairs
+// grid: ceil(S/128) * Hkv * B blocks (1-D), 8 waves = 4 pairs x 32 keys, two waves per SIMD (<= 256
+// registers each; the 4-wave kernel above holds K, V, dK and dV in one wave: 404 registers, one wave per
+// SIMD, and its MFMAs idle whenever that wave waits). The two waves of a pair own the same 32 keys and
+// split each 32-query tile by role:
+//   P-wave   S = Q.K^T - lse/scale (8 MFMAs), P = exp2(S * scale * log2e) -> LDS (fp32),
+//            dV^T += dO^T . P (8 MFMAs)
+//   dS-wave  dP = dO.V^T - delta (8 MFMAs); one tile behind, dS = P . (dP - delta) with the partner's P
+//            of that tile (published by the tile barrier), dK^T += Q^T . dS (8 MFMAs)
+// so each wave keeps one of K / V and one of the dK / dV accumulators. The same 6-slot LDS-DMA ring as
+// above (each wave fetches 4 rows of Q and of dO per tile); the P exchange is double-buffered by tile
+// parity, written and read lane-linearly (16-byte columns, conflict-free).
+// Measured (opt-in, LLMT_FA_BWD_VARIANT=2): B4 S8192 Hq32 Hkv8 backward 10.81 ms vs 9.89 ms with the
+// 4-wave kernel — the per-tile barrier keeps both waves of a SIMD in the same phase (LDS reads together,
+// MFMAs together), so the second wave adds little overlap; kept for the record, not dispatched.
+template <int D>
+__global__ __launch_bounds__(512, 1) void fa_bwd_dkdv2_kernel(AttnArgs a, const float* ld) {
+  constexpr int NKK = D / 16, NDT = D / 32;
+  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
+  constexpr int NDMA = 3;              // DMA instructions per wave per tile: Q 1, dO 1, row constants 1
+  constexpr int PPAIR = 4 * 64 * 16;   // one pair's P of one tile: 4 x (64 lanes x 16 B)
+  constexpr int PBUF = 4 * PPAIR;      // four pairs
+  using QI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + 2 * PBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pair = wid >> 1, role = wid & 1;  // role 0: P / dV, role 1: dS / dK
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  const int b = L % a.B;
+  const int kb = L / a.B;
+  const int ks = kb * 128, kw = ks + pair * 32, kr = kw + r;
+  const int nT = (S + 31) / 32;
+  const int sk = (a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;
+  const float sl2 = a.scale * kLog2e;
+  const bf16* kvp = role == 0 ? a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh
+                              : a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh;
+  const int64_t kv_ss = role == 0 ? a.k_ss : a.v_ss;
+
+  bfv8 kf[NKK];  // K rows (role 0) or V rows (role 1) of this pair's keys: the B operand of S / dP
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) kf[kk] = gload8(kvp + (int64_t)min(kr, S - 1) * kv_ss + kk * 16 + hh * 8, kr < S);
+  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
+  int skv = sk;
+  asm volatile("" : "+v"(skv));
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]));
+  f32v16 acc[NDT];  // dV^T (role 0) or dK^T (role 1)
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+
+  const RunInfo kr_run = block_run(a, b, min(ks, S - 1), min(ks + 127, S - 1));
+  const int q_beg = a.causal ? ks : max(0, kr_run.rs) / 32 * 32;
+  int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+  if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
+  const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
+  const int T = nq * grp;
+
+  if (T > 0) {
+    int dq_off, dd_off;
+    {
+      const int row = 4 * wid + (lane >> 4);
+      const int ch = (lane & 15) ^ QI::swz(row);
+      dq_off = (row * (int)a.q_ss + ch * 8) * 2;
+      dd_off = (row * (int)a.d_ss + ch * 8) * 2;
+    }
+    const int ld_off = ((wid & 1) * 64 + lane) * 4;
+    asm volatile("" : "+v"(dq_off), "+v"(dd_off));
+    auto sl = [&](int t) -> const char* { return smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT); };
+    int iss_g = 0, iss_q = 0, iss_n = 0;
+    auto issue = [&](int t) {
+      const char* slot = sl(t);
+      const int q0 = q_beg + iss_q * BM;
+      const int h = hk * grp + iss_g;
+      const int64_t rows_left = S - q0;
+      const Rsrc qrs = make_rsrc4(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_ss,
+                                  ((rows_left - 1) * a.q_ss + D) * 2);
+      const Rsrc drs = make_rsrc4(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh + (int64_t)q0 * a.d_ss,
+                                  ((rows_left - 1) * a.d_ss + D) * 2);
+      const Rsrc lrs = make_rsrc4(ld + (((int64_t)b * a.Hq + h) * nT + (q0 >> 5)) * kLdTile, kLdTile * 4);
+      dma16(sgpr_rsrc(qrs), slot + 4 * wid * 256, dq_off);
+      dma16(sgpr_rsrc(drs), slot + IMG + 4 * wid * 256, dd_off);
+      dma4(sgpr_rsrc(lrs), slot + 2 * IMG + (wid & 1) * 256, ld_off);
+      if (++iss_n < T) {
+        if (++iss_q == nq) {
+          iss_q = 0;
+          ++iss_g;
+        }
+      }
+    };
+    int ini_g = 0, ini_q = 0, ini_n = 0;
+    auto tile_q0 = [&]() {
+      const int q0 = q_beg + ini_q * BM;
+      if (++ini_n < T) {
+        if (++ini_q == nq) {
+          ini_q = 0;
+          ++ini_g;
+        }
+      }
+      return q0;
+    };
+    int ro[NKK], to[NDT][2];
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) ro[kk] = QI::roff(r, 2 * kk + hh);
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        to[dt][0] = QI::toff(BM, row, dt * 32 + col);
+        to[dt][1] = QI::toff(BM, row + 8, dt * 32 + col);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(ro[kk]));
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
+    // this lane's 64 bytes of a pair's P image: four 16-byte columns, lane-linear within each
+    char* const pmine = smem + NS * SLOT + pair * PPAIR + lane * 16;
+
+#pragma unroll
+    for (int t = 0; t < NS - 2; ++t) issue(t);
+    wait_vm<NDMA * (NS - 3)>();  // tile 0 landed
+    ring_barrier();
+
+    f32v16 dprev;  // role 1: dP - delta of the previous tile
+    // role 1, one tile behind: dS of tile u from the partner's P and dprev, then dK^T += Q^T . dS
+    auto dk_tile = [&](int u) {
+      const char* pp = pmine + (u & 1) * PBUF;
+      f32v16 pv;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 f = *reinterpret_cast<const float4*>(pp + c * 1024);
+        pv[4 * c] = f.x; pv[4 * c + 1] = f.y; pv[4 * c + 2] = f.z; pv[4 * c + 3] = f.w;
+      }
+      bfv8 db[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) db[s2][j] = (__bf16)(pv[8 * s2 + j] * dprev[8 * s2 + j]);
+      const char* slot = sl(u);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const s16v4 lo = lds_tr(slot + to[dt][0] + 4096 * s2), hi = lds_tr(slot + to[dt][1] + 4096 * s2);
+          acc[dt] = mfma32(__builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)),
+                           db[s2], acc[dt]);
+        }
+    };
+
+    for (int t = 0; t < T; ++t) {
+      issue(t + NS - 2);
+      const char* slot = sl(t);
+      const float* Ls = reinterpret_cast<const float*>(slot + 2 * IMG);
+      const int q0 = tile_q0();
+      if (role == 0) {
+        // S - lse/scale (masked rows -inf) -> P
+        f32v16 sc;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 l4 = *reinterpret_cast<const float4*>(Ls + 8 * c + 4 * hh);
+          sc[4 * c] = l4.x; sc[4 * c + 1] = l4.y; sc[4 * c + 2] = l4.z; sc[4 * c + 3] = l4.w;
+        }
+        const bool m_seg = seg_mask(a, kr_run, q0, q0 + 31);
+        if (m_seg || (a.causal && kw + 31 > q0) || (a.window >= 0 && q0 + 31 - a.window > kw)) {
+          const int* Sg = reinterpret_cast<const int*>(Ls + 64);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            int4 s4 = make_int4(skv, skv, skv, skv);
+            if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int qi = q0 + 8 * c + 4 * hh + j;
+              bool ok = true;
+              if (a.causal) ok = ok && (kr <= qi);
+              if (a.window >= 0) ok = ok && (qi - kr <= a.window);
+              if (m_seg) ok = ok && ((&s4.x)[j] == skv);
+              sc[4 * c + j] = ok ? sc[4 * c + j] : -INFINITY;
+            }
+          }
+        }
+        bfv8 qr[NKK];
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) qr[kk] = lds_b128(slot + ro[kk]);
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) sc = mfma32(qr[kk], kf[kk], sc);
+        bfv8 pb[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[i] = fexp2(sc[i] * sl2);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[s2][j] = (__bf16)sc[8 * s2 + j];
+        char* pp = pmine + (t & 1) * PBUF;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          *reinterpret_cast<float4*>(pp + c * 1024) = make_float4(sc[4 * c], sc[4 * c + 1], sc[4 * c + 2], sc[4 * c + 3]);
+        // dV^T += dO^T . P
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const s16v4 lo = lds_tr(slot + IMG + to[dt][0] + 4096 * s2);
+            const s16v4 hi = lds_tr(slot + IMG + to[dt][1] + 4096 * s2);
+            acc[dt] = mfma32(__builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)),
+                             pb[s2], acc[dt]);
+          }
+      } else {
+        if (t > 0) dk_tile(t - 1);
+        f32v16 dn;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
+          dn[4 * c] = d4.x; dn[4 * c + 1] = d4.y; dn[4 * c + 2] = d4.z; dn[4 * c + 3] = d4.w;
+        }
+        bfv8 dr[NKK];
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) dr[kk] = lds_b128(slot + IMG + ro[kk]);
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) dn = mfma32(dr[kk], kf[kk], dn);
+        dprev = dn;
+      }
+      wait_vm<NDMA * (NS - 3)>();
+      ring_barrier();
+    }
+    if (role == 1) dk_tile(T - 1);
+    wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+  }
+
+  if (kr < S) {
+    bf16* op = role == 0 ? a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh
+                         : a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh;
+    const float f = role == 0 ? 1.f : a.scale;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint2 w;
+        w.x = pack_bf16x2(acc[dt][4 * c] * f, acc[dt][4 * c + 1] * f);
+        w.y = pack_bf16x2(acc[dt][4 * c + 2] * f, acc[dt][4 * c + 3] * f);
+        *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
       }
   }
 }
@@ -2176,6 +2435,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     }();
     if (variant == 1)
       fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 2)
+      fa_bwd_dkdv2_kernel<128><<<(S + 127) / 128 * Hkv * B, 512, 0, stream>>>(a, ld);
     else
       fa_bwd_dkdv128_kernel<0><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     return hipGetLastError();
