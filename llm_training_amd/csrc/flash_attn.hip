@@ -814,7 +814,8 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 //    partials and no reduction kernel; blocks are ordered kv-head-fastest (an XCD per kv head at
 //    Hkv = 8), heaviest key blocks first.
 // Per-row constants, packed per 32-row tile for the DMA:
-//   ld[((b*Hq + h)*nT + t)*128 + {0..31: -lse/scale | 32..63: -delta | 64..95: segment id}]
+//   ld[((b*Hq + h)*nT + t)*128 + {0..31: -lse/scale | 32..63: -delta | 64..95: segment id |
+//                                  96..127: -lse*log2(e)}]
 constexpr int kLdTile = 128;
 
 template <int D>
@@ -830,7 +831,7 @@ __global__ __launch_bounds__(256) void fa_bwd_prep128_kernel(AttnArgs a, float* 
     const int h = (int)(bh % a.Hq);
     const int b = (int)(bh / a.Hq);
     const int s = t * 32 + i;
-    float dl = 0.f, ls = -INFINITY;
+    float dl = 0.f, ls = -INFINITY, l2 = -INFINITY;
     int sg = -1;
     if (s < a.S) {
       const bf16x8* op = reinterpret_cast<const bf16x8*>(a.o + (int64_t)b * a.o_sb + (int64_t)s * a.o_ss + (int64_t)h * a.o_sh);
@@ -847,13 +848,14 @@ __global__ __launch_bounds__(256) void fa_bwd_prep128_kernel(AttnArgs a, float* 
       ((float*)a.delta)[lr] = dl;
       const float l = a.lse[lr];
       ls = (l == -INFINITY) ? -INFINITY : -l * inv_scale;
+      l2 = (l == -INFINITY) ? -INFINITY : -l * kLog2e;
       sg = a.seg ? a.seg[(int64_t)b * a.S + s] : 0;
     }
     float* blk = ld + (bh * nT + t) * kLdTile;
     blk[i] = ls;
     blk[32 + i] = -dl;
     reinterpret_cast<int*>(blk)[64 + i] = sg;
-    blk[96 + i] = 0.f;
+    blk[96 + i] = l2;
   }
 }
 
@@ -886,6 +888,25 @@ __device__ __forceinline__ void dma4(const Rsrc& r, const char* lds, int voff) {
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "s"(lds_addr(lds)), "v"(voff), "s"(r.w) : "memory");
+}
+// the five LDS-DMAs of one dK/dV ring tile (Q rows x2, dO rows x2, row constants) in one statement: M0 is
+// saved and restored once instead of around every load
+__device__ __forceinline__ void dma_tile5(const Rsrc& q, const Rsrc& d, const Rsrc& l, const char* lq0,
+                                          const char* lq1, const char* ld0, const char* ld1, const char* ll,
+                                          int vq0, int vq1, int vd0, int vd1, int vl) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %6, %11, 0 offen lds\n\t"
+      "s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %7, %11, 0 offen lds\n\t"
+      "s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %8, %12, 0 offen lds\n\t"
+      "s_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %9, %12, 0 offen lds\n\t"
+      "s_mov_b32 m0, %5\n\ts_nop 0\n\tbuffer_load_dword %10, %13, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_addr(lq0)), "s"(lds_addr(lq1)), "s"(lds_addr(ld0)), "s"(lds_addr(ld1)), "s"(lds_addr(ll)), "v"(vq0),
+        "v"(vq1), "v"(vd0), "v"(vd1), "v"(vl), "s"(q.w), "s"(d.w), "s"(l.w)
+      : "memory");
 }
 // the same with the descriptor forced to SGPRs (a kernel under SGPR pressure may keep it in VGPRs,
 // which the asm's "s" operand does not accept)
@@ -956,9 +977,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
   const int T = nq * grp;
 
   if (T > 0) {
-    // ---- DMA of the next tile (tiles past T-1 repeat the last one) into slot t % NS. The tile
-    // sequence is walked with scalar counters; lane offsets are loop constants and the buffer
-    // descriptor starts at the tile's first row (rows past S fall outside it and read as zeros).
+    // ---- DMA of the next tile (tiles past T-1 repeat the last one) into the ring. The tile sequence
+    // is walked with scalar counters. Each descriptor covers one head from row q_beg on (rows past S
+    // fall outside it and read as zeros) and is rebuilt only when the walk enters the next head; the
+    // tile's byte offset inside the head rides in the lane offsets (one VALU add per DMA instead of
+    // three 64-bit descriptor builds per tile: the old per-tile descriptors were ~90 SALU per tile
+    // in a loop that issues one instruction per cycle from its single wave per SIMD).
     int dq_off[2], dd_off[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
@@ -969,77 +993,52 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
     }
     const int ld_off = ((wid & 1) * 64 + lane) * 4;
     asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]));
-    // slot base as ONE scalar: hipcc otherwise folds (t % NS) * SLOT into every LDS address as two adds
-    auto sl = [&](int t) -> const char* { return smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT); };
-    int iss_g = 0, iss_q = 0, iss_n = 0;  // head within the group, tile within the head, tiles issued
-    auto issue = [&](int t) {
-      const char* slot = sl(t);
-      const int q0 = q_beg + iss_q * BM;
-      const int h = hk * grp + iss_g;
-      const int64_t rows_left = S - q0;
-      const Rsrc qrs = make_rsrc4(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_ss,
-                                  ((rows_left - 1) * a.q_ss + D) * 2);
-      const Rsrc drs = make_rsrc4(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh + (int64_t)q0 * a.d_ss,
-                                  ((rows_left - 1) * a.d_ss + D) * 2);
-      const Rsrc lrs = make_rsrc4(ld + (((int64_t)b * a.Hq + h) * nT + (q0 >> 5)) * kLdTile, kLdTile * 4);
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int row0 = 8 * wid + 4 * n;
-        dma16(qrs, slot + row0 * 256, dq_off[n]);
-        dma16(drs, slot + IMG + row0 * 256, dd_off[n]);
-      }
+    const int64_t q_rows = S - q_beg;
+    const int64_t nrec_q = ((q_rows - 1) * a.q_ss + D) * 2, nrec_d = ((q_rows - 1) * a.d_ss + D) * 2;
+    const int64_t nrec_l = (int64_t)nq * kLdTile * 4;
+    const bf16* qh0 = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * grp) * a.q_sh + (int64_t)q_beg * a.q_ss;
+    const bf16* dh0 = a.dout + (int64_t)b * a.d_sb + (int64_t)(hk * grp) * a.d_sh + (int64_t)q_beg * a.d_ss;
+    const float* lh0 = ld + (((int64_t)b * a.Hq + hk * grp) * nT + (q_beg >> 5)) * kLdTile;
+    const int step_q = BM * a.q_ss * 2, step_d = BM * a.d_ss * 2;
+    Rsrc qrs = make_rsrc4(qh0, nrec_q), drs = make_rsrc4(dh0, nrec_d), lrs = make_rsrc4(lh0, nrec_l);
+    int iss_g = 0, iss_q = 0, iss_n = 0, toff_q = 0, toff_d = 0, toff_l = 0;
+    auto issue = [&](const char* slot) {
       // row constants: waves 0/2 fetch floats 0..63, waves 1/3 floats 64..127 (same bytes twice)
-      dma4(lrs, slot + 2 * IMG + (wid & 1) * 256, ld_off);
+      const char* q0 = slot + 8 * wid * 256;
+      dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, slot + 2 * IMG + (wid & 1) * 256,
+                dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
       if (++iss_n < T) {
+        toff_q += step_q;
+        toff_d += step_d;
+        toff_l += kLdTile * 4;
         if (++iss_q == nq) {
           iss_q = 0;
           ++iss_g;
+          toff_q = toff_d = toff_l = 0;
+          qrs = make_rsrc4(qh0 + (int64_t)iss_g * a.q_sh, nrec_q);
+          drs = make_rsrc4(dh0 + (int64_t)iss_g * a.d_sh, nrec_d);
+          lrs = make_rsrc4(lh0 + (int64_t)iss_g * nT * kLdTile, nrec_l);
         }
       }
     };
-    int ini_g = 0, ini_q = 0, ini_n = 0;  // the same walk for init(), one tile at a time
-    auto tile_q0 = [&](int t) {
-      (void)t;
-      const int q0 = q_beg + ini_q * BM;
-      if (++ini_n < T) {
-        if (++ini_q == nq) {
-          ini_q = 0;
-          ++ini_g;
-        }
-      }
-      return q0;
+    // mask state of a tile: first query row, and whether any element of it needs the compare
+    int cur_q = 0;  // tile index inside its head of the tile whose S/dP is being computed
+    const bool seg_or_window = a.seg != nullptr || a.window >= 0;
+    struct TileMask {
+      int q0;
+      bool need, m_seg;
     };
-    // initial accumulator values of tile t: -lse/scale and -delta per query row, -inf where masked
-    auto init = [&](int t, f32v16& si, f32v16& di) {
-      const char* slot = sl(t);
-      const float* Ls = reinterpret_cast<const float*>(slot + 2 * IMG);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float4 l4 = *reinterpret_cast<const float4*>(Ls + 8 * c + 4 * hh);
-        const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
-        si[4 * c] = l4.x; si[4 * c + 1] = l4.y; si[4 * c + 2] = l4.z; si[4 * c + 3] = l4.w;
-        di[4 * c] = d4.x; di[4 * c + 1] = d4.y; di[4 * c + 2] = d4.z; di[4 * c + 3] = d4.w;
+    auto tile_mask = [&]() {
+      TileMask m;
+      m.q0 = q_beg + cur_q * BM;
+      m.need = a.causal && kw + 31 > m.q0;
+      m.m_seg = false;
+      if (seg_or_window) {
+        m.m_seg = seg_mask(a, kr_run, m.q0, m.q0 + 31);
+        m.need = m.need || m.m_seg || (a.window >= 0 && m.q0 + 31 - a.window > kw);
       }
-      const int q0 = tile_q0(t);
-      const bool m_seg = seg_mask(a, kr_run, q0, q0 + 31);
-      const bool need = m_seg || (a.causal && kw + 31 > q0) || (a.window >= 0 && q0 + 31 - a.window > kw);
-      if (need) {
-        const int* Sg = reinterpret_cast<const int*>(Ls + 64);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          int4 s4 = make_int4(sk, sk, sk, sk);
-          if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int qi = q0 + 8 * c + 4 * hh + j;
-            bool ok = true;
-            if (a.causal) ok = ok && (kr <= qi);
-            if (a.window >= 0) ok = ok && (qi - kr <= a.window);
-            if (m_seg) ok = ok && ((&s4.x)[j] == sk);
-            si[4 * c + j] = ok ? si[4 * c + j] : -INFINITY;
-          }
-        }
-      }
+      if (++cur_q == nq) cur_q = 0;
+      return m;
     };
     // lane-constant LDS byte offsets inside a 32-row image, computed once and kept opaque so hipcc
     // does not re-derive the swizzle for every read inside the loop (it did: ~5 VALU per read)
@@ -1059,8 +1058,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
     for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(ro[kk]));
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
-    auto rows = [&](int t, bfv8* qr, bfv8* dr) {
-      const char* slot = sl(t);
+    auto rows = [&](const char* slot, bfv8* qr, bfv8* dr) {
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
         const char* p = slot + ro[kk];  // one VGPR address; the dO image is an immediate offset away
@@ -1084,46 +1082,87 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
         }
       }
     };
+    // S = Q.K^T and dP = dO.V^T of the tile in `qr` / `dr`, accumulated from zero (the MFMA's inline 0)
+    auto sdp = [&](const bfv8* qr, const bfv8* dr, f32v16& s, f32v16& d) {
+      const f32v16 z = {};
+      s = mfma32(qr[0], kf[0], z);
+      d = mfma32(dr[0], vf[0], z);
+#pragma unroll
+      for (int kk = 1; kk < NKK; ++kk) {
+        s = mfma32(qr[kk], kf[kk], s);
+        d = mfma32(dr[kk], vf[kk], d);
+      }
+    };
+    // P = exp2(S * scale * log2e - lse * log2e) and dS = P (dP - delta) of the tile in `slot` (its row
+    // constants: -lse*log2e at floats 96.., -delta at 32..; rows past S / without keys carry -inf);
+    // masked elements (diagonal / window / segment tiles only) get P = 0
+    auto softmax = [&](const char* slot, const TileMask& m, const f32v16& s, const f32v16& d, bfv8 (&pb)[2],
+                       bfv8 (&db)[2]) {
+      const float* Ls = reinterpret_cast<const float*>(slot + 2 * IMG);
+      float lq[16], nd[16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float4 l4 = *reinterpret_cast<const float4*>(Ls + 96 + 8 * c + 4 * hh);
+        const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
+        lq[4 * c] = l4.x; lq[4 * c + 1] = l4.y; lq[4 * c + 2] = l4.z; lq[4 * c + 3] = l4.w;
+        nd[4 * c] = d4.x; nd[4 * c + 1] = d4.y; nd[4 * c + 2] = d4.z; nd[4 * c + 3] = d4.w;
+      }
+      float p[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) p[i] = fexp2(fmaf(s[i], sl2, lq[i]));
+      if (m.need) {
+        const int* Sg = reinterpret_cast<const int*>(Ls + 64);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int4 s4 = make_int4(sk, sk, sk, sk);
+          if (m.m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int qi = m.q0 + 8 * c + 4 * hh + j;
+            bool ok = true;
+            if (a.causal) ok = ok && (kr <= qi);
+            if (a.window >= 0) ok = ok && (qi - kr <= a.window);
+            if (m.m_seg) ok = ok && ((&s4.x)[j] == sk);
+            p[4 * c + j] = ok ? p[4 * c + j] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * s2 + j;
+          pb[s2][j] = (__bf16)p[i];
+          db[s2][j] = (__bf16)(p[i] * (d[i] + nd[i]));
+        }
+    };
 
+    // ring slots (byte offsets) of tiles t-2 (the DMA target of iteration t), t-1, t, t+1
+    int sl_m2 = (NS - 1) * SLOT, sl_m1 = 0, sl_0 = SLOT, sl_p1 = 2 * SLOT;
     // prologue: tiles 0..NS-2 in flight, wait for 0..2
 #pragma unroll
-    for (int t = 0; t < NS - 1; ++t) issue(t);
+    for (int t = 0; t < NS - 1; ++t) issue(smem + t * SLOT);
     wait_vm<NDMA * (NS - 4)>();
     ring_barrier();
 
     bfv8 qr[NKK], dr[NKK];
     f32v16 sacc, dacc;
-    rows(0, qr, dr);
-    init(0, sacc, dacc);
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {
-      sacc = mfma32(qr[kk], kf[kk], sacc);
-      dacc = mfma32(dr[kk], vf[kk], dacc);
-    }
-    rows(1, qr, dr);
+    rows(smem, qr, dr);
+    TileMask mprev = tile_mask();
+    sdp(qr, dr, sacc, dacc);
+    rows(smem + SLOT, qr, dr);
 
     for (int t = 1; t <= T; ++t) {
-      issue(t + NS - 2);
+      issue(smem + sl_m2);
       // ---- region A: S/dP of tile t  ||  softmax of tile t-1 + its transposed reads
-      f32v16 sn, dn;
-      init(t, sn, dn);
-      const char* pslot = sl(t - 1);
+      const TileMask mcur = tile_mask();
+      const char* pslot = smem + sl_m1;
       bfv8 trd[2][NDT], trq[2][NDT];
       trA2(pslot, trq, trd);
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        sn = mfma32(qr[kk], kf[kk], sn);
-        dn = mfma32(dr[kk], vf[kk], dn);
-      }
+      f32v16 sn, dn;
+      sdp(qr, dr, sn, dn);
       bfv8 pb[2], db[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float p = fexp2(sacc[8 * s2 + j] * sl2);
-          pb[s2][j] = (__bf16)p;
-          db[s2][j] = (__bf16)(p * dacc[8 * s2 + j]);
-        }
+      softmax(pslot, mprev, sacc, dacc, pb, db);
       if constexpr (V == 0) {
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
@@ -1136,7 +1175,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
         __builtin_amdgcn_sched_barrier(0);
       }
       // ---- region B: dV/dK of tile t-1  ||  row reads of tile t+1
-      rows(t + 1, qr, dr);
+      rows(smem + sl_p1, qr, dr);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -1154,6 +1193,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
       }
       sacc = sn;
       dacc = dn;
+      mprev = mcur;
+      sl_m2 = sl_m1;
+      sl_m1 = sl_0;
+      sl_0 = sl_p1;
+      sl_p1 = (sl_p1 + SLOT == NS * SLOT) ? 0 : sl_p1 + SLOT;
       wait_vm<NDMA * (NS - 4)>();
       ring_barrier();
     }
