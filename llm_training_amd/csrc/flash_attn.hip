@@ -908,6 +908,29 @@ __device__ __forceinline__ void dma_tile5(const Rsrc& q, const Rsrc& d, const Rs
         "v"(vq1), "v"(vd0), "v"(vd1), "v"(vl), "s"(q.w), "s"(d.w), "s"(l.w)
       : "memory");
 }
+// the nine LDS-DMAs of one K/V ring tile of the forward / dQ kernels (K rows x4, V rows x4, segment ids) in
+// one statement, M0 saved once; `lds` = the wave's first K row in the slot, rows 4 apart, V `img` bytes on
+__device__ __forceinline__ void dma_tile9(const Rsrc& k, const Rsrc& v, const Rsrc& sg, const char* lds, int img,
+                                          const char* lseg, const int (&vk)[4], const int (&vv)[4], int vs) {
+  uint32_t keep;
+  const uint32_t l0 = lds_addr(lds);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %12, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %7, %13, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %12, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %8, %13, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, 0x800\n\ts_nop 0\n\tbuffer_load_dwordx4 %5, %12, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %9, %13, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, 0xc00\n\ts_nop 0\n\tbuffer_load_dwordx4 %6, %12, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %10, %13, 0 offen lds\n\t"
+      "s_mov_b32 m0, %15\n\ts_nop 0\n\tbuffer_load_dword %11, %14, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(l0), "s"(img), "v"(vk[0]), "v"(vk[1]), "v"(vk[2]), "v"(vk[3]), "v"(vv[0]), "v"(vv[1]), "v"(vv[2]),
+        "v"(vv[3]), "v"(vs), "s"(k.w), "s"(v.w), "s"(sg.w), "s"(lds_addr(lseg))
+      : "memory");
+}
 // the same with the descriptor forced to SGPRs (a kernel under SGPR pressure may keep it in VGPRs,
 // which the asm's "s" operand does not accept)
 __device__ __forceinline__ Rsrc sgpr_rsrc(const Rsrc& r) {
@@ -1990,14 +2013,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
     auto issue = [&](int t) {
       const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
       const int n0 = kv_beg + t * BN;
+      int vk[4], vv[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        const int row0 = 16 * wid + 4 * n, row = row0 + (lane >> 4);
+        const int row = 16 * wid + 4 * n + (lane >> 4);
         const int ch = (lane & 15) ^ KI::swz(row);
-        dma16(krs, slot + row0 * 256, ((n0 + row) * a.k_ss + ch * 8) * 2);
-        dma16(vrs, slot + IMG + row0 * 256, ((n0 + row) * a.v_ss + ch * 8) * 2);
+        vk[n] = ((n0 + row) * a.k_ss + ch * 8) * 2;
+        vv[n] = ((n0 + row) * a.v_ss + ch * 8) * 2;
       }
-      dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
+      dma_tile9(krs, vrs, srs, slot + 16 * wid * 256, IMG, slot + 2 * IMG, vk, vv, (n0 + lane) * 4);
     };
     // loop-invariant LDS offsets: K row reads (two 32-key halves) and V^T transposed reads
     int ro[NKK], to[NDT][2];
@@ -2201,14 +2225,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
     auto issue = [&](int t) {
       const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
       const int n0 = kv_beg + t * BN;
+      int vk[4], vv[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        const int row0 = 16 * wid + 4 * n, row = row0 + (lane >> 4);
+        const int row = 16 * wid + 4 * n + (lane >> 4);
         const int ch = (lane & 15) ^ KI::swz(row);
-        dma16(krs, slot + row0 * 256, ((n0 + row) * a.k_ss + ch * 8) * 2);
-        dma16(vrs, slot + IMG + row0 * 256, ((n0 + row) * a.v_ss + ch * 8) * 2);
+        vk[n] = ((n0 + row) * a.k_ss + ch * 8) * 2;
+        vv[n] = ((n0 + row) * a.v_ss + ch * 8) * 2;
       }
-      dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
+      dma_tile9(krs, vrs, srs, slot + 16 * wid * 256, IMG, slot + 2 * IMG, vk, vv, (n0 + lane) * 4);
     };
     int ro[NKK], to[NDT][2];
 #pragma unroll
