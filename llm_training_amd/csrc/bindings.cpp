@@ -22,6 +22,8 @@ hipError_t llmt_swiglu_fwd(const void* gu, void* c, int64_t T, int I, hipStream_
 hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu, int64_t T, int I, hipStream_t stream);
 hipError_t llmt_transpose2d(const void* in, void* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo,
                             hipStream_t stream);
+hipError_t llmt_splitk_reduce(const float* slabs, int nsplit, int64_t n, void* out, int out_is_fp32, int accumulate,
+                              hipStream_t stream);
 hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const float* cos_t, const float* sin_t, int64_t T,
                      int nheads, int D, int64_t stride_t, int stride_h, int inverse, hipStream_t stream);
 hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const int64_t* labels,
@@ -182,6 +184,17 @@ void transpose_(const at::Tensor& x, at::Tensor out) {
   TORCH_CHECK(out.size(0) == x.size(1) && out.size(1) == x.size(0), "transpose_: out must be [C, R]");
   check(llmt_transpose2d(x.data_ptr(), out.data_ptr(), x.size(0), x.size(1), x.stride(0), out.stride(0), cur_stream()),
         "transpose2d");
+}
+
+// out (+)= slabs.sum(0): split-K partials of a weight gradient (slabs fp32 [nsplit, *out.shape])
+void splitk_reduce_(const at::Tensor& slabs, at::Tensor out, bool accumulate) {
+  TORCH_CHECK(slabs.is_cuda() && out.is_cuda() && slabs.scalar_type() == at::kFloat && slabs.is_contiguous() &&
+                  out.is_contiguous(), "splitk_reduce_: contiguous GPU tensors, fp32 slabs");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "splitk_reduce_: out fp32/bf16");
+  TORCH_CHECK(slabs.dim() >= 1 && slabs.numel() == slabs.size(0) * out.numel(), "splitk_reduce_: slabs [k, *out]");
+  check(llmt_splitk_reduce(slabs.data_ptr<float>(), (int)slabs.size(0), out.numel(), out.data_ptr(),
+                           out.scalar_type() == at::kFloat, accumulate, cur_stream()),
+        "splitk_reduce");
 }
 
 void rope_(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t, int64_t nheads,
@@ -429,6 +442,7 @@ TORCH_LIBRARY(llmt, m) {
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dc) -> Tensor");
   m.def("transpose_(Tensor x, Tensor(a!) out) -> ()");
+  m.def("splitk_reduce_(Tensor slabs, Tensor(a!) out, bool accumulate) -> ()");
   m.def("rope_(Tensor(a!) qkv, Tensor pos, Tensor cos, Tensor sin, int nheads, bool inverse) -> ()");
   m.def(
       "cross_entropy_(Tensor(a!) logits, Tensor labels, int vocab_start, int ignore_index, Tensor? lse_in, "
@@ -455,6 +469,7 @@ TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("transpose_", &transpose_);
+  m.impl("splitk_reduce_", &splitk_reduce_);
   m.impl("rope_", &rope_);
   m.impl("cross_entropy_", &cross_entropy_);
   m.impl("adamw_", &adamw_);

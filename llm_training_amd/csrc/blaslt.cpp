@@ -101,11 +101,25 @@ void make_desc(Desc& d, bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64
   LT_CHECK(hipblasLtMatrixLayoutCreate(&d.c, ctype, m, n, ldc));
 }
 
+// split-K as a strided batch: batch i multiplies the i-th contraction slice (A and B offsets along k) into
+// its own [m, n] fp32 slab of C (batch stride m * n); the caller sums the slabs
+void set_batch(Desc& d, bool ta, bool tb, int64_t m, int64_t n, int64_t kc, int64_t lda, int64_t ldb, int batch) {
+  const int32_t bc = batch;
+  const int64_t sa = ta ? kc : kc * lda, sb = tb ? kc * ldb : kc, sc = m * n;
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(d.a, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(d.b, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(d.c, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(d.a, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sa, sizeof(sa)));
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(d.b, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sb, sizeof(sb)));
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(d.c, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sc, sizeof(sc)));
+}
+
 std::string key_of(bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
-                   hipDataType ctype, bool beta, bool streamk) {
+                   hipDataType ctype, bool beta, bool streamk, int batch = 1) {
   std::ostringstream o;
   o << (ta ? 't' : 'n') << (tb ? 't' : 'n') << "_" << m << "_" << n << "_" << k << "_ld" << lda << "_" << ldb << "_"
     << ldc << (ctype == HIP_R_32F ? "_f32" : "_bf16") << (beta ? "_acc" : "") << (streamk ? "" : "_nosk");
+  if (batch > 1) o << "_b" << batch;
   return o.str();
 }
 
@@ -120,9 +134,10 @@ bool is_streamk(hipblasLtHandle_t h, hipblasLtMatmulAlgo_t& algo) {
   return name.find("_SK") != std::string::npos;
 }
 
-// C (m x n, column-major) = op(A) . op(B) (+ C when accumulate)
-void gemm_lt(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bool tb, int64_t m, int64_t n,
-             int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool accumulate, bool streamk) {
+// C (m x n, column-major) = op(A) . op(B) (+ C when accumulate); batch > 1: split-K into `batch` fp32 slabs
+// of C (C is then [batch, n, m] fp32 with ldc = m, k divisible by batch)
+void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bool tb, int64_t m, int64_t n,
+                  int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool accumulate, bool streamk, int batch) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm_lt: GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_lt: bf16 A/B");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm_lt: C bf16/fp32");
@@ -134,10 +149,15 @@ void gemm_lt(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bo
   std::lock_guard<std::mutex> lock(s.mu);
   hipblasLtHandle_t h = handle_for(dev);
   Desc d;
-  make_desc(d, ta, tb, m, n, k, lda, ldb, ldc, ctype);
+  TORCH_CHECK(batch >= 1 && k % batch == 0, "gemm_lt: k must divide into the split-K batch");
+  make_desc(d, ta, tb, m, n, k / batch, lda, ldb, ldc, ctype);
+  if (batch > 1) {
+    TORCH_CHECK(ctype == HIP_R_32F && ldc == m && C.numel() >= batch * m * n, "gemm_lt: split-K slabs are fp32 [batch, n, m]");
+    set_batch(d, ta, tb, m, n, k / batch, lda, ldb, batch);
+  }
   const float alpha = 1.f, beta = accumulate ? 1.f : 0.f;
   auto ws = at::empty({(int64_t)kWorkspace}, C.options().dtype(at::kByte));
-  const std::string key = key_of(ta, tb, m, n, k, lda, ldb, ldc, ctype, accumulate, streamk);
+  const std::string key = key_of(ta, tb, m, n, k, lda, ldb, ldc, ctype, accumulate, streamk, batch);
   auto it = s.cache.find(key);
   if (it == s.cache.end()) {
     hipblasLtMatmulPreference_t pref;
@@ -199,6 +219,17 @@ void gemm_lt(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bo
                            C.data_ptr(), d.c, &it->second.algo, ws.data_ptr(), kWorkspace, stream));
 }
 
+void gemm_lt(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bool tb, int64_t m, int64_t n,
+             int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool accumulate, bool streamk) {
+  gemm_lt_impl(A, B, C, ta, tb, m, n, k, lda, ldb, ldc, accumulate, streamk, 1);
+}
+
+// split-K form: C fp32 [batch, n, m] slabs, no accumulation (the caller reduces them)
+void gemm_lt_splitk(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bool tb, int64_t m, int64_t n,
+                    int64_t k, int64_t lda, int64_t ldb, int64_t batch, bool streamk) {
+  gemm_lt_impl(A, B, C, ta, tb, m, n, k, lda, ldb, m, false, streamk, (int)batch);
+}
+
 // "key rank ms" lines of every problem tuned / used so far
 std::string gemm_lt_export() {
   auto& s = st();
@@ -237,8 +268,14 @@ TORCH_LIBRARY_FRAGMENT(llmt, m) {
   m.def(
       "gemm_lt(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, int m, int n, int k, int lda, int ldb, int ldc, "
       "bool accumulate, bool streamk=True) -> ()");
+  m.def(
+      "gemm_lt_splitk(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, int m, int n, int k, int lda, int ldb, "
+      "int batch, bool streamk=True) -> ()");
   m.def("gemm_lt_export() -> str", &gemm_lt_export);
   m.def("gemm_lt_import(str text, bool tune_unknown) -> int", &gemm_lt_import);
 }
 
-TORCH_LIBRARY_IMPL(llmt, CUDA, m) { m.impl("gemm_lt", &gemm_lt); }
+TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
+  m.impl("gemm_lt", &gemm_lt);
+  m.impl("gemm_lt_splitk", &gemm_lt_splitk);
+}

@@ -177,3 +177,53 @@ extern "C" hipError_t llmt_transpose2d(const void* in, void* out, int64_t R, int
       (const llmt::bf16*)in, (llmt::bf16*)out, ldi, ldo);
   return hipGetLastError();
 }
+
+// Split-K reduction of the weight-gradient GEMM (ops/fused.py wgrad_into): out (+)= sum of `nsplit` fp32
+// slabs of n elements each, out bf16 or fp32. One float4 group per thread: reads 16 * nsplit bytes and
+// writes 8 (bf16) / 16 (fp32) per group.
+namespace llmt {
+template <typename OutT>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __restrict__ slabs, int nsplit, int64_t n4,
+                                                            OutT* __restrict__ out, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 s = slabs[i];
+  for (int k = 1; k < nsplit; ++k) {
+    const float4 t = slabs[k * n4 + i];
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  if constexpr (sizeof(OutT) == 4) {
+    float4* o = reinterpret_cast<float4*>(out) + i;
+    if (accumulate) {
+      const float4 t = *o;
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    *o = s;
+  } else {
+    uint2* o = reinterpret_cast<uint2*>(out) + i;
+    if (accumulate) {
+      const uint2 t = *o;
+      s.x += bf16_lo(t.x); s.y += bf16_hi(t.x); s.z += bf16_lo(t.y); s.w += bf16_hi(t.y);
+    }
+    uint2 w;
+    w.x = pack_bf16x2(s.x, s.y);
+    w.y = pack_bf16x2(s.z, s.w);
+    *o = w;
+  }
+}
+}  // namespace llmt
+
+extern "C" hipError_t llmt_splitk_reduce(const float* slabs, int nsplit, int64_t n, void* out, int out_is_fp32,
+                                         int accumulate, hipStream_t stream) {
+  if (n % 4 || nsplit < 1) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(slabs) | reinterpret_cast<uintptr_t>(out)) & 15) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4, blocks = (n4 + 255) / 256;
+  if (n4 == 0) return hipSuccess;
+  if (out_is_fp32)
+    llmt::splitk_reduce_kernel<float><<<(unsigned)blocks, 256, 0, stream>>>((const float4*)slabs, nsplit, n4,
+                                                                           (float*)out, accumulate);
+  else
+    llmt::splitk_reduce_kernel<llmt::bf16><<<(unsigned)blocks, 256, 0, stream>>>((const float4*)slabs, nsplit, n4,
+                                                                                (llmt::bf16*)out, accumulate);
+  return hipGetLastError();
+}

@@ -94,6 +94,11 @@ _TR_WGRAD_MIN_M = 4096
 _LAYOUT_CACHE: dict[tuple, str] = {}
 
 
+# largest weight-gradient output (elements) offered the split-K candidates (fp32 slabs: 8 bytes / element)
+_SPLITK_MAX_OUT = int(os.environ.get("LLMT_WGRAD_SPLITK_MAX", str(1 << 26)))
+_SPLITK = (2, 4)  # contraction splits offered (slabs: n_split x N x K fp32)
+
+
 def _tr_ok(*ts: torch.Tensor) -> bool:
     return all(t.size(0) % 64 == 0 and t.size(1) % 64 == 0 for t in ts)
 
@@ -225,10 +230,27 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
         def nn():  # dy^T materialised
             lib().gemm_lt(x, transpose(dy), o2, False, False, K, N, M, _ld(x), M, K, accumulate, sk)
 
+        variants = {"nt": nt, "tt": tt, "nn": nn}
+        if N * K <= _SPLITK_MAX_OUT and M % 256 == 0:
+            # split-K in two along the token (contraction) dimension as a strided batch into fp32 slabs +
+            # one reduction pass: twice the output tiles for outputs that fill the 256 CUs in 1.5 / 3.5
+            # waves of 256x256 tiles (qkv, down)
+            def _split(a, b, ta, tb, lda, ldb, n_split):
+                def run():
+                    slabs = torch.empty(n_split, N, K, device=out.device, dtype=torch.float32)
+                    lib().gemm_lt_splitk(a() if callable(a) else a, b() if callable(b) else b, slabs, ta, tb,
+                                         K, N, M, lda, ldb, n_split, sk)
+                    lib().splitk_reduce_(slabs, o2, accumulate)
+                return run
+
+            for ns in _SPLITK:
+                variants[f"nt{ns}"] = _split(x, dy, False, True, _ld(x), _ld(dy), ns)
+                variants[f"tt{ns}"] = _split(lambda: transpose(x), dy, True, True, M, _ld(dy), ns)
+                variants[f"nn{ns}"] = _split(x, lambda: transpose(dy), False, False, _ld(x), M, ns)
         # static rule: wide outputs (gate_up, lm_head) transpose the smaller operand x, the rest dy
         default = "tt" if N >= 4 * K else "nn"
         key = ("wgrad", M, N, K, _ld(x), _ld(dy), out.dtype, sk)
-        {"nt": nt, "tt": tt, "nn": nn}[_layout(key, {"nt": nt, "tt": tt, "nn": nn}, default, not accumulate)]()
+        variants[_layout(key, variants, default, not accumulate)]()
         return True
     if path == "lt":  # column-major: dW^T (K x N) = x^T (K x M) . dy (M x N)
         lib().gemm_lt(x, dy, out.view(N, K), False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, ALLOW_STREAMK[0])

@@ -273,10 +273,11 @@ def test_transpose_kernel_strided():
 
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("N,K", [(256, 192), (1024, 192)])
-@pytest.mark.parametrize("forced", [None, "tn/nt", "nn/tt", "tn/nn"])
+@pytest.mark.parametrize("forced", [None, "tn/nt", "nn/tt", "tn/nn", "tn/nt2", "nn/tt2", "tn/nn2", "tn/nn4"])
 def test_backward_gemms_transposed_layouts(monkeypatch, out_dtype, N, K, forced):
-    """dgrad (NN, or TN with W^T at M >= 16384) and wgrad (NT, NN with dy^T, TT with x^T), each layout
-    forced and the timed per-shape choice, with accumulation, against fp32 products."""
+    """dgrad (NN, or TN with W^T at M >= 16384) and wgrad (NT, NN with dy^T, TT with x^T, and each of them
+    split-K in two: fp32 slabs + reduction), each layout forced and the timed per-shape choice, with and
+    without accumulation, against fp32 products."""
     import llm_training_amd.ops.fused as fused
     monkeypatch.setattr(fused, "GEMM_MODES", {"fwd": "lt", "dgrad": "lt", "wgrad": "lt"})
     monkeypatch.setattr(fused, "_LAYOUT_CACHE", {})
@@ -294,6 +295,7 @@ def test_backward_gemms_transposed_layouts(monkeypatch, out_dtype, N, K, forced)
         assert _rel(dx, dy.float() @ w.float()) < 1e-2
         dw = torch.empty(N, K, device=DEV, dtype=out_dtype)
         assert fused.wgrad_into(dw, dy, x, False)  # (times the layouts when not forced)
+        assert _rel(dw, dy.float().t() @ x.float()) < (1e-4 if out_dtype == torch.float32 else 1e-2)
         c0 = torch.randn(N, K, device=DEV).to(out_dtype)
         dw = c0.clone()
         assert fused.wgrad_into(dw, dy, x, True)
