@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <tuple>
 #include <vector>
 
@@ -25,11 +27,11 @@ hipError_t llmt_transpose2d(const void* in, void* out, int64_t R, int64_t C, int
 hipError_t llmt_splitk_reduce(const float* slabs, int nsplit, int64_t n, void* out, int out_is_fp32, int accumulate,
                               hipStream_t stream);
 hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const float* cos_t, const float* sin_t, int64_t T,
-                     int nheads, int D, int64_t stride_t, int stride_h, int inverse, hipStream_t stream);
+                     int nheads, int D, int64_t stride_t, int stride_h, int inverse, int64_t P, int* err, hipStream_t stream);
 hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const int64_t* labels,
                               int64_t vocab_start, int64_t ignore_index, const float* lse_in, float* lse_out,
                               float* tgt_out, float* loss_out, const float* coef_row, const float* coef_scalar,
-                              int write_grad, hipStream_t stream);
+                              int write_grad, int64_t vocab_total, int* err, hipStream_t stream);
 hipError_t llmt_adamw(float* p, float* m, float* v, const void* g, int grad_is_fp32, void* pout, int64_t n,
                       float lr, float b1, float b2, float eps, float wd, int64_t step, const float* gscale,
                       hipStream_t stream);
@@ -197,6 +199,23 @@ void splitk_reduce_(const at::Tensor& slabs, at::Tensor out, bool accumulate) {
         "splitk_reduce");
 }
 
+// ---------------------------------------------------------------- device-side index checks
+// Per-device int32 words the kernels set when a data-dependent index is out of range (the kernels clamp or
+// skip, so memory stays safe): [0] a RoPE position outside the cos/sin table, [1] a cross-entropy label
+// that is neither ignore_index nor a vocabulary id. Read (one host sync) by llm_training_amd.ops.native.
+// check_kernel_errors() at the trainer's logging steps.
+at::Tensor kernel_errors() {
+  static std::mutex mu;
+  static std::map<int, at::Tensor> words;
+  const int dev = c10::hip::current_device();
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = words.find(dev);
+  if (it == words.end())
+    it = words.emplace(dev, at::zeros({4}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, dev))).first;
+  return it->second;
+}
+static int* err_words() { return kernel_errors().data_ptr<int>(); }
+
 void rope_(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t, int64_t nheads,
            bool inverse) {
   check_bf16_cuda(qkv, "qkv");
@@ -217,17 +236,19 @@ void rope_(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_t, const
               "rope: cos/sin tables must be fp32 [max_pos, D/2]");
   check(llmt_rope(qkv.data_ptr(), pos.data_ptr(), pos.scalar_type() == at::kLong, cos_t.data_ptr<float>(),
                   sin_t.data_ptr<float>(), T, (int)nheads, (int)D, stride_t, (int)qkv.stride(-2), inverse ? 1 : 0,
-                  cur_stream()),
+                  cos_t.size(0), err_words(), cur_stream()),
         "rope");
 }
 
 // ---------------------------------------------------------------- cross entropy
+// vocab_total: upper bound of a valid label for the error word (-1: the row width when vocab_start == 0, the
+// whole-vocabulary logits of the non-parallel losses; 0: lower bound only, a vocab-parallel shard)
 std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_(at::Tensor logits, const at::Tensor& labels,
                                                              int64_t vocab_start, int64_t ignore_index,
                                                              const c10::optional<at::Tensor>& lse_in,
                                                              const c10::optional<at::Tensor>& coef_row,
                                                              const c10::optional<at::Tensor>& coef_scalar,
-                                                             bool write_grad) {
+                                                             bool write_grad, int64_t vocab_total) {
   check_bf16_cuda(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] with unit column stride");
   const int64_t N = logits.size(0), V = logits.size(1);
@@ -243,7 +264,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_(at::Tensor logits,
   check(llmt_cross_entropy(logits.data_ptr(), N, logits.stride(0), (int)V, labels.data_ptr<int64_t>(), vocab_start,
                            ignore_index, fptr(lse_in, N), lse.data_ptr<float>(), tgt.data_ptr<float>(),
                            loss.data_ptr<float>(), fptr(coef_row, N), fptr(coef_scalar, 1), write_grad ? 1 : 0,
-                           cur_stream()),
+                           vocab_total >= 0 ? vocab_total : (vocab_start == 0 ? V : 0), err_words(), cur_stream()),
         "cross_entropy");
   return {lse, tgt, loss};
 }
@@ -446,7 +467,8 @@ TORCH_LIBRARY(llmt, m) {
   m.def("rope_(Tensor(a!) qkv, Tensor pos, Tensor cos, Tensor sin, int nheads, bool inverse) -> ()");
   m.def(
       "cross_entropy_(Tensor(a!) logits, Tensor labels, int vocab_start, int ignore_index, Tensor? lse_in, "
-      "Tensor? coef_row, Tensor? coef_scalar, bool write_grad) -> (Tensor, Tensor, Tensor)");
+      "Tensor? coef_row, Tensor? coef_scalar, bool write_grad, int vocab_total=-1) -> (Tensor, Tensor, Tensor)");
+  m.def("kernel_errors() -> Tensor", &kernel_errors);
   m.def(
       "adamw_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? pout, float lr, float b1, float b2, "
       "float eps, float wd, int step, Tensor? gscale) -> ()");

@@ -24,7 +24,8 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
                                                  int64_t ignore_index, const float* __restrict__ lse_in,
                                                  float* __restrict__ lse_out, float* __restrict__ tgt_out,
                                                  float* __restrict__ loss_out, const float* __restrict__ coef_row,
-                                                 const float* __restrict__ coef_scalar, int write_grad) {
+                                                 const float* __restrict__ coef_scalar, int write_grad,
+                                                 int64_t vocab_total, int* __restrict__ err) {
   __shared__ float red[4];
   const int64_t row = blockIdx.x;
   bf16* x = logits + row * ld;
@@ -33,6 +34,8 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
   const int64_t lloc = lab - vocab_start;
   const bool local_hit = valid && lloc >= 0 && lloc < V;
   const int tid = threadIdx.x;
+  // a label that is neither ignore_index nor a vocabulary entry: flag it (the row then trains on lse alone)
+  if (err && tid == 0 && valid && (lab < 0 || (vocab_total > 0 && lab >= vocab_total))) err[1] = 1;
 
   float lse;
   if (lse_in) {
@@ -124,15 +127,17 @@ using namespace llmt;
 extern "C" hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const int64_t* labels,
                                          int64_t vocab_start, int64_t ignore_index, const float* lse_in,
                                          float* lse_out, float* tgt_out, float* loss_out, const float* coef_row,
-                                         const float* coef_scalar, int write_grad, hipStream_t stream) {
+                                         const float* coef_scalar, int write_grad, int64_t vocab_total, int* err,
+                                         hipStream_t stream) {
   if (N == 0) return hipSuccess;
   const bool vec = (ld % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) & 15) == 0);
   if (vec)
     ce_kernel<true><<<(unsigned)N, 256, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index, lse_in,
-                                                     lse_out, tgt_out, loss_out, coef_row, coef_scalar, write_grad);
+                                                     lse_out, tgt_out, loss_out, coef_row, coef_scalar, write_grad,
+                                                     vocab_total, err);
   else
     ce_kernel<false><<<(unsigned)N, 256, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index,
                                                       lse_in, lse_out, tgt_out, loss_out, coef_row, coef_scalar,
-                                                      write_grad);
+                                                      write_grad, vocab_total, err);
   return hipGetLastError();
 }

@@ -60,7 +60,7 @@ template <typename PosT>
 __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const PosT* __restrict__ pos,
                                                    const float* __restrict__ cos_t, const float* __restrict__ sin_t,
                                                    int64_t T, int nheads, int D, int64_t stride_t, int stride_h,
-                                                   float sign) {
+                                                   float sign, int64_t P, int* __restrict__ err) {
   const int half = D >> 1;
   const int groups = half >> 3;  // 8 pairs per thread
   const int64_t total = T * nheads * groups;
@@ -69,7 +69,11 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const
     const int64_t th = e / groups;
     const int h = (int)(th % nheads);
     const int64_t t = th / nheads;
-    const int64_t p = (int64_t)pos[t];
+    int64_t p = (int64_t)pos[t];
+    if (p < 0 || p >= P) {  // position outside the cos/sin table: flag it, read a valid row
+      if (err) err[0] = 1;
+      p = p < 0 ? 0 : P - 1;
+    }
     bf16* base = qkv + t * stride_t + (int64_t)h * stride_h + g * 8;
     bf16x8* lo = reinterpret_cast<bf16x8*>(base);
     bf16x8* hi = reinterpret_cast<bf16x8*>(base + half);
@@ -119,18 +123,18 @@ extern "C" hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu,
 // qkv: bf16, element strides stride_t (token) / stride_h (head); pos: int32 (pos_is_64=0) or int64.
 extern "C" hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const float* cos_t, const float* sin_t,
                                 int64_t T, int nheads, int D, int64_t stride_t, int stride_h, int inverse,
-                                hipStream_t stream) {
-  if (D % 16) return hipErrorInvalidValue;
+                                int64_t P, int* err, hipStream_t stream) {
+  if (D % 16 || P <= 0) return hipErrorInvalidValue;
   const int64_t total = T * nheads * (D / 16);
   if (total == 0) return hipSuccess;
   const int grid = stream_grid(total, 256);
   const float sign = inverse ? -1.f : 1.f;
   if (pos_is_64)
     rope_kernel<int64_t><<<grid, 256, 0, stream>>>((bf16*)qkv, (const int64_t*)pos, cos_t, sin_t, T, nheads, D,
-                                                   stride_t, stride_h, sign);
+                                                   stride_t, stride_h, sign, P, err);
   else
     rope_kernel<int32_t><<<grid, 256, 0, stream>>>((bf16*)qkv, (const int32_t*)pos, cos_t, sin_t, T, nheads, D,
-                                                   stride_t, stride_h, sign);
+                                                   stride_t, stride_h, sign, P, err);
   return hipGetLastError();
 }
 

@@ -59,3 +59,30 @@ def use_native(t: torch.Tensor) -> bool:
         lib()
         return t.dtype == torch.bfloat16
     return False
+
+
+_KERNEL_ERRORS = {
+    0: "a position id outside the RoPE cos/sin table (max_position_embeddings too small for the data?)",
+    1: "a label that is neither ignore_index nor a vocabulary id",
+}
+
+
+def check_kernel_errors(device: torch.device | None = None, raise_error: bool = True) -> list[str]:
+    """Read (one host sync) and clear the device-side index-check words the HIP kernels set when a
+    data-dependent index is out of range (csrc/bindings.cpp ``kernel_errors``: the kernels clamp / skip,
+    so memory stays safe, and the condition is reported here). Raises ``RuntimeError`` when any is set
+    unless ``raise_error`` is False; returns the messages."""
+    if device is not None and device.type != "cuda":
+        return []
+    if not torch.cuda.is_available() or not _load():
+        return []
+    with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+        words = torch.ops.llmt.kernel_errors()
+        host = words.tolist()
+        if not any(host):
+            return []
+        words.zero_()
+    msgs = [_KERNEL_ERRORS.get(i, f"kernel error word {i}") for i, v in enumerate(host) if v]
+    if raise_error:
+        raise RuntimeError("HIP kernel index check failed: " + "; ".join(msgs))
+    return msgs

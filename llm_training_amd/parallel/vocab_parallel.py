@@ -34,7 +34,7 @@ def _combine_lse(lse_local: torch.Tensor, group) -> torch.Tensor:
 def _local_stats(lg, lab, v0, ignore_index, native):
     """(lse_local, tgt_local) of logits lg [n, Vl] for global labels lab."""
     if native:
-        lse, tgt, _ = lib().cross_entropy_(lg, lab, v0, ignore_index, None, None, None, False)
+        lse, tgt, _ = lib().cross_entropy_(lg, lab, v0, ignore_index, None, None, None, False, 0)
         return lse, tgt
     lf = lg.float()
     lse = torch.logsumexp(lf, -1)
@@ -47,7 +47,7 @@ def _local_stats(lg, lab, v0, ignore_index, native):
 def _local_grad(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, native):
     """Overwrite lg with coef * (softmax_global - onehot)."""
     if native:
-        lib().cross_entropy_(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, True)
+        lib().cross_entropy_(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, True, 0)
         return lg
     p = torch.exp(lg.float() - lse.unsqueeze(1))
     loc = lab - v0

@@ -22,6 +22,7 @@ from typing import Any
 import torch
 import torch.distributed as dist
 
+from ..ops.native import check_kernel_errors
 from ..optim import resolve_optimizer
 from ..parallel import debug as collective_debug
 from ..parallel.context import ParallelContext, init_distributed
@@ -399,6 +400,9 @@ class Trainer:
             dist.all_reduce(mat, group=self.pc.dp_group)
             mat = mat / self.pc.dp_size
         mat = mat.cpu().tolist()
+        # device-side index checks of the HIP kernels (RoPE positions, CE labels): the host already
+        # synchronised above, so reading the error words costs one small copy per logging interval
+        check_kernel_errors(self.device)
         consumed = dict(self.state.consumed)
         if self.pc.dp and consumed:
             t = torch.tensor([float(consumed[k]) for k in sorted(consumed)], device=self.device)

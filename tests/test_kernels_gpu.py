@@ -84,6 +84,43 @@ def test_rope_inplace_roundtrip(D):
     assert _rel(x, qkv) < 2e-2
 
 
+def test_kernel_index_checks():
+    """Data-dependent indices out of range: the RoPE kernel clamps a position past its cos/sin table and
+    the CE kernel skips a label outside the vocabulary, both flag the device error word, and
+    check_kernel_errors() raises once (then the words are clear)."""
+    from llm_training_amd.ops.native import check_kernel_errors
+    check_kernel_errors(raise_error=False)
+    torch.manual_seed(0)
+    S, H, D, P = 64, 4, 128, 128
+    cos, sin = compute_rope_tables(D, P, 10000.0, device=DEV)
+    qkv = torch.randn(S, H, D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.arange(S, device=DEV)
+    x = qkv.clone()
+    lib().rope_(x, pos, cos, sin, H, False)
+    assert check_kernel_errors() == []  # in-range positions: clean
+    bad = pos.clone()
+    bad[5] = P + 1000  # clamped to the last table row
+    y = qkv.clone()
+    lib().rope_(y, bad, cos, sin, H, False)
+    with pytest.raises(RuntimeError, match="RoPE"):
+        check_kernel_errors()
+    assert check_kernel_errors() == []  # cleared
+    want = qkv.clone()
+    lib().rope_(want, torch.full_like(pos, P - 1), cos, sin, H, False)
+    assert torch.equal(y[5], want[5]) and torch.equal(y[:5], x[:5])
+    V = 1000
+    logits = torch.randn(16, V, device=DEV).bfloat16()
+    labels = torch.randint(0, V, (16,), device=DEV)
+    labels[3] = -100
+    lib().cross_entropy_(logits.clone(), labels, 0, -100, None, None, None, False)
+    assert check_kernel_errors() == []
+    labels[7] = V + 3
+    _, _, loss = lib().cross_entropy_(logits.clone(), labels, 0, -100, None, None, None, False)
+    assert torch.isfinite(loss).all()
+    with pytest.raises(RuntimeError, match="label"):
+        check_kernel_errors()
+
+
 @pytest.mark.parametrize("V", [32064, 128256, 50257])
 def test_cross_entropy(V):
     torch.manual_seed(0)
