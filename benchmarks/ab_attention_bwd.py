@@ -1,0 +1,41 @@
+"""In-process A/B of flash-attention backward variants (LLMT_FA_BWD_VARIANT is read on every launch):
+alternating windows of each variant on the same operands, so box-to-box clock differences cancel.
+    python benchmarks/ab_attention_bwd.py [B S Hq Hkv D] [variants, comma-separated]"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llm_training_amd.ops import fused as F_  # noqa: E402
+
+B, S, Hq, Hkv, D = (int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (4, 8192, 32, 8, 128)))
+variants = (sys.argv[6] if len(sys.argv) > 6 else "1,3").split(",")
+q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+o = F_.flash_attention(q, k, v, causal=True)
+do = torch.randn_like(o)
+grads = {}
+times = {x: [] for x in variants}
+for rnd in range(5):
+    for var in variants:
+        os.environ["LLMT_FA_BWD_VARIANT"] = var
+        for _ in range(2):
+            g = torch.autograd.grad(o, (q, k, v), do, retain_graph=True)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(10):
+            g = torch.autograd.grad(o, (q, k, v), do, retain_graph=True)
+        b.record()
+        torch.cuda.synchronize()
+        times[var].append(a.elapsed_time(b) / 10)
+        grads[var] = g
+ref = grads[variants[0]]
+out = {"shape": [B, S, Hq, Hkv, D]}
+for var in variants:
+    out[f"v{var}_ms"] = round(sorted(times[var])[len(times[var]) // 2], 4)
+    out[f"v{var}_max_abs_diff_vs_v{variants[0]}"] = max(float((x - y).abs().max()) for x, y in zip(grads[var], ref))
+print(json.dumps(out), flush=True)

@@ -945,6 +945,10 @@ __device__ __forceinline__ void wait_vm() {
 }
 // every wave's LDS reads retired, then a barrier that does NOT drain the DMA ring (no vmcnt(0))
 __device__ __forceinline__ void ring_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// the same without the LDS drain, for loops in which every read of the slot the next DMA overwrites has
+// already been consumed (so retired) before the barrier in program order, and the only reads still in
+// flight are the prefetched rows of a slot the next DMA does not touch
+__device__ __forceinline__ void ring_barrier_nodrain() { asm volatile("s_barrier" ::: "memory"); }
 
 // grid: ceil(S/128) * Hkv * B blocks (1-D), 4 waves x 32 keys; query tiles of 32 rows over all q heads of
 // the kv group; NS-slot LDS-DMA ring.
@@ -1222,7 +1226,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
       sl_0 = sl_p1;
       sl_p1 = (sl_p1 + SLOT == NS * SLOT) ? 0 : sl_p1 + SLOT;
       wait_vm<NDMA * (NS - 4)>();
-      ring_barrier();
+      if constexpr (V == 3)
+        ring_barrier_nodrain();
+      else
+        ring_barrier();
     }
     wait_vm<0>();  // no LDS-DMA may outlive the workgroup
   }
@@ -2341,6 +2348,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
 
 using namespace llmt;
 
+// dK/dV kernel variant, read on every launch so one process can A/B them (LLMT_FA_BWD_VARIANT):
+//   1 = end-of-tile barrier after an LDS drain, 3 = barrier without the drain (rows prefetched for the next
+//   tile stay in flight across it), 0 = sched-group pinned schedule, 2 = role-split 8-wave pairs (D128)
+static int dkdv_variant() {
+  const char* e = getenv("LLMT_FA_BWD_VARIANT");
+  return e ? atoi(e) : 3;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
+}
+
 static void set_dropout(AttnArgs& a, float p, uint32_t seed) {
   if (p <= 0.f) {
     a.drop_thresh = 0;
@@ -2479,13 +2494,19 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
       fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      if (dkdv_variant() == 3)
+        fa_bwd_dkdv128_kernel<3, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      else
+        fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       return hipGetLastError();
     }
     if (D == 64) {
       fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<64><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      if (dkdv_variant() == 3)
+        fa_bwd_dkdv128_kernel<3, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      else
+        fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       return hipGetLastError();
     }
     fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
@@ -2498,11 +2519,10 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     else
       fa_bwd_dq128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a, ld);
-    static const int variant = [] {
-      const char* e = getenv("LLMT_FA_BWD_VARIANT");
-      return e ? atoi(e) : 1;
-    }();
-    if (variant == 1)
+    const int variant = dkdv_variant();
+    if (variant == 3)
+      fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 1)
       fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 2)
       fa_bwd_dkdv2_kernel<128><<<(S + 127) / 128 * Hkv * B, 512, 0, stream>>>(a, ld);
