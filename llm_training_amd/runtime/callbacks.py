@@ -31,10 +31,38 @@ class Callback:
 
 
 class LearningRateMonitor(Callback):
-    """The trainer logs ``lr`` every step already; this keeps YAML configs that list it valid."""
+    """Lightning's LearningRateMonitor keys on top of the trainer's own ``lr``: ``lr-<Optimizer>`` (e.g.
+    ``lr-AdamW``) and, with ``log_momentum``, ``lr-<Optimizer>-momentum`` (Adam beta1), logged every step
+    (``logging_interval: step`` or None) or once per epoch (``epoch``) through the trainer's buffered
+    metrics (host values: no device sync)."""
 
-    def __init__(self, logging_interval: str | None = "step", log_momentum: bool = False, **kw):
+    def __init__(self, logging_interval: str | None = "step", log_momentum: bool = False,
+                 log_weight_decay: bool = False, **kw):
+        if logging_interval not in (None, "step", "epoch"):
+            raise ValueError(f"LearningRateMonitor: logging_interval must be 'step', 'epoch' or None, "
+                             f"got {logging_interval!r}")
         self.logging_interval = logging_interval
+        self.log_momentum = log_momentum
+        self.log_weight_decay = log_weight_decay
+
+    def _values(self, trainer) -> dict[str, float]:
+        name = getattr(trainer, "optimizer_name", "AdamW")
+        eng = getattr(trainer, "engine", None)
+        out = {f"lr-{name}": float(trainer.last_lr)}  # the rate the optimizer step just used
+        if self.log_momentum and eng is not None:
+            out[f"lr-{name}-momentum"] = float(eng.betas[0])
+        if self.log_weight_decay and eng is not None:
+            out[f"lr-{name}-weight_decay"] = float(eng.weight_decay)
+        return out
+
+    def on_step_metrics(self, trainer, lm):
+        if self.logging_interval != "epoch":
+            trainer.add_step_metrics(self._values(trainer))
+
+    def on_train_epoch_end(self, trainer, lm):
+        if self.logging_interval == "epoch":
+            trainer.add_step_metrics(self._values(trainer))
+            trainer._flush_logs(force=True)
 
 
 class ModelCheckpoint(Callback):

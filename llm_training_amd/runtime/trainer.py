@@ -129,6 +129,7 @@ class Trainer:
         self.lm = None
         self.datamodule = None
         self.scheduler = None
+        self.last_lr = float("nan")
         self.config_dict: dict | None = None
         self._log_buffer: list[tuple[int, dict]] = []
         self.last_metrics: dict[str, float] = {}
@@ -202,6 +203,7 @@ class Trainer:
             logger.info("frozen %d parameters", len(frozen))
         ospec = lm.optimizer_spec()
         hp = resolve_optimizer(ospec["name"], ospec["kwargs"])
+        self.optimizer_name = str(ospec["name"]).rsplit(".", 1)[-1]
         self.base_lr = hp["lr"]
         rd = getattr(st, "grad_reduce_dtype", None)
         self.engine = DataParallelEngine(lm.model, self.pc, st.zero_stage, lr=hp["lr"], betas=hp["betas"],
@@ -353,6 +355,7 @@ class Trainer:
             eng.clip_and_scale(self.gradient_clip_val)
             lr = self.scheduler.get_lr()
             eng.step(lr)
+        self.last_lr = lr
         self.scheduler.step()
         self.state.global_step += 1
         for k, v in counters.items():
@@ -368,6 +371,8 @@ class Trainer:
         self.watchdog.disarm()
         if self.collectives is not None and self.state.global_step % collective_debug.check_every() == 0:
             self.collectives.verify()
+        for cb in self.callbacks:  # metric contributions for this step's log row (before it is flushed)
+            _call(cb, "on_step_metrics", self, lm)
         self._flush_logs()
         for cb in self.callbacks:
             _call(cb, "on_train_batch_end", self, lm, None, batches[-1], self.state.batch_idx)
@@ -382,6 +387,14 @@ class Trainer:
             self._fpt[S] = model_flops_per_token(getattr(self.lm.model, "config", None), S)
         self.meter.fpt = self._fpt[S]
         self.meter.update(sum(t.numel() for t in ids))
+
+    def add_step_metrics(self, values: dict[str, float]):
+        """Extra scalar metrics (host floats) for the most recent optimizer step's log row."""
+        vals = {k: torch.tensor(float(v)) for k, v in values.items()}
+        if self._log_buffer and self._log_buffer[-1][0] == self.state.global_step:
+            self._log_buffer[-1][1].update(vals)
+        else:  # the step's row was already written (e.g. an epoch-end value): a row of its own
+            self._log_buffer.append((self.state.global_step, vals))
 
     def _flush_logs(self, force: bool = False):
         if not self._log_buffer:

@@ -70,6 +70,9 @@ trainer:
   max_steps: 4
   log_every_n_steps: 1
   gradient_clip_val: 1.0
+  callbacks:
+    - class_path: lightning.pytorch.callbacks.LearningRateMonitor
+      init_args: {{logging_interval: step, log_momentum: true}}
 model:
   class_path: llm_training.lms.CLM
   init_args.config:
@@ -87,6 +90,12 @@ data:
     assert main(["fit", "--config", str(cfg)]) == 0
     assert os.path.exists(tmp_path / "logs" / "t" / "metrics.csv")
     assert os.path.exists(tmp_path / "logs" / "t" / "config.yaml")
+    # LearningRateMonitor: Lightning's lr-<Optimizer> / -momentum columns, equal to the step's lr
+    import csv
+    rows = list(csv.DictReader(open(tmp_path / "logs" / "t" / "metrics.csv")))
+    assert rows and "lr-AdamW" in rows[-1] and "lr-AdamW-momentum" in rows[-1]
+    assert float(rows[-1]["lr-AdamW"]) == pytest.approx(float(rows[-1]["lr"]))
+    assert float(rows[-1]["lr-AdamW-momentum"]) == pytest.approx(0.9)
 
 
 def test_fsdp2_mp_policy_and_int_reshard_map_to_the_engine():
