@@ -1134,9 +1134,24 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
         lq[4 * c] = l4.x; lq[4 * c + 1] = l4.y; lq[4 * c + 2] = l4.z; lq[4 * c + 3] = l4.w;
         nd[4 * c] = d4.x; nd[4 * c + 1] = d4.y; nd[4 * c + 2] = d4.z; nd[4 * c + 3] = d4.w;
       }
+      // packed fp32 math (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: two lanes' worth per instruction)
+      // wherever two neighbouring elements take the same operation: the loop issues one instruction per
+      // cycle from its single wave per SIMD, so halving the VALU count of the softmax shortens it
+      typedef float f2 __attribute__((ext_vector_type(2)));
       float p[16];
+      const f2 sl2v = {sl2, sl2};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) p[i] = fexp2(fmaf(s[i], sl2, lq[i]));
+      for (int i = 0; i < 16; i += 2) {
+        if constexpr (V == 1) {  // scalar form (A/B reference)
+          p[i] = fexp2(fmaf(s[i], sl2, lq[i]));
+          p[i + 1] = fexp2(fmaf(s[i + 1], sl2, lq[i + 1]));
+        } else {
+          const f2 sv = {s[i], s[i + 1]}, lv = {lq[i], lq[i + 1]};
+          const f2 x = __builtin_elementwise_fma(sv, sl2v, lv);
+          p[i] = fexp2(x[0]);
+          p[i + 1] = fexp2(x[1]);
+        }
+      }
       if (m.need) {
         const int* Sg = reinterpret_cast<const int*>(Ls + 64);
 #pragma unroll
@@ -1157,10 +1172,20 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 8; j += 2) {
           const int i = 8 * s2 + j;
+          const f2 pv = {p[i], p[i + 1]}, dv = {d[i], d[i + 1]}, nv = {nd[i], nd[i + 1]};
+          f2 ds;
+          if constexpr (V == 1) {
+            ds[0] = p[i] * (d[i] + nd[i]);
+            ds[1] = p[i + 1] * (d[i + 1] + nd[i + 1]);
+          } else {
+            ds = pv * (dv + nv);
+          }
           pb[s2][j] = (__bf16)p[i];
-          db[s2][j] = (__bf16)(p[i] * (d[i] + nd[i]));
+          pb[s2][j + 1] = (__bf16)p[i + 1];
+          db[s2][j] = (__bf16)ds[0];
+          db[s2][j + 1] = (__bf16)ds[1];
         }
     };
 
