@@ -1992,7 +1992,7 @@ __device__ __forceinline__ float vadd(float a, float b) {
   return r;
 }
 
-template <int D>
+template <int D, int RS = 0>
 __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;  // k-steps of a D-deep product, 32-wide output tiles
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
@@ -2154,8 +2154,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
         for (int i = 0; i < 16; i += 2) {
           st[tt][i] = fexp2(fmaf(st[tt][i], sl2, nm));
           st[tt][i + 1] = fexp2(fmaf(st[tt][i + 1], sl2, nm));
-          rs0 = vadd(rs0, st[tt][i]);
-          rs1 = vadd(rs1, st[tt][i + 1]);
+          if constexpr (RS == 0) {
+            rs0 = vadd(rs0, st[tt][i]);
+            rs1 = vadd(rs1, st[tt][i + 1]);
+          } else {  // plain adds: the compiler places the trans-use wait states (and may pack the pair)
+            rs0 += st[tt][i];
+            rs1 += st[tt][i + 1];
+          }
         }
       l += rs0 + rs1;
 #pragma unroll
@@ -2430,31 +2435,32 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   a.scale = scale; a.causal = causal; a.window = window;
   set_dropout(a, drop_p, drop_seed);
   dim3 grid((S + 127) / 128, Hq, B);
-  static const int variant = [] {
-    const char* e = getenv("LLMT_FA_FWD_VARIANT");
-    // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907, fwd128 1.043
-    return e ? atoi(e) : 2;
-  }();
+  // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907, fwd128 1.043;
+  // 3 = fwd3 with compiler-placed row-sum adds (A/B); read per launch
+  const char* fve = getenv("LLMT_FA_FWD_VARIANT");
+  const int variant = fve ? atoi(fve) : 3;  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
   switch (D) {
     case 64:  // the v3 structure on 128-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a);
       else
-        fa_fwd3_kernel<64><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<64, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       break;
     case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a);
       else
-        fa_fwd3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<96, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       break;
     case 128: {
       if (a.drop_thresh)  // dropout lives in the generic kernels
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
       else if (variant == 1)
         fa_fwd128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else if (variant == 2)
+      else if (variant == 2)  // row sums through the inline-asm add (each behind its own wait state)
         fa_fwd3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else if (variant == 3)
+        fa_fwd3_kernel<128, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
     } break;
