@@ -818,12 +818,16 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 //                                  96..127: -lse*log2(e)}]
 constexpr int kLdTile = 128;
 
+// 16 lanes per row: each reads one 16-byte chunk of the row of O and of dO, so a wave instruction covers
+// four contiguous 256-byte rows (one row per lane read 64 scattered 16-byte pieces: 2.7 TB/s); the
+// partial dot products meet through three xor shuffles inside the 16-lane group.
 template <int D>
 __global__ __launch_bounds__(256) void fa_bwd_prep128_kernel(AttnArgs a, float* ld) {
   const int nT = (a.S + 31) / 32;
   const int64_t nrows = (int64_t)a.B * a.Hq * nT * 32;
   const float inv_scale = 1.f / a.scale;
-  for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < nrows; row += (int64_t)gridDim.x * 256) {
+  const int c = threadIdx.x & 15;
+  for (int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; row < nrows; row += (int64_t)gridDim.x * 16) {
     const int i = (int)(row & 31);
     const int64_t tt = row >> 5;
     const int t = (int)(tt % nT);
@@ -831,31 +835,39 @@ __global__ __launch_bounds__(256) void fa_bwd_prep128_kernel(AttnArgs a, float* 
     const int h = (int)(bh % a.Hq);
     const int b = (int)(bh / a.Hq);
     const int s = t * 32 + i;
-    float dl = 0.f, ls = -INFINITY, l2 = -INFINITY;
-    int sg = -1;
-    if (s < a.S) {
+    float dl = 0.f;
+    if (s < a.S && c < D / 8) {
       const bf16x8* op = reinterpret_cast<const bf16x8*>(a.o + (int64_t)b * a.o_sb + (int64_t)s * a.o_ss + (int64_t)h * a.o_sh);
       const bf16x8* dp = reinterpret_cast<const bf16x8*>(a.dout + (int64_t)b * a.d_sb + (int64_t)s * a.d_ss + (int64_t)h * a.d_sh);
+      float x[8], y[8];
+      unpack8(op[c], x);
+      unpack8(dp[c], y);
 #pragma unroll
-      for (int c = 0; c < D / 8; ++c) {
-        float x[8], y[8];
-        unpack8(op[c], x);
-        unpack8(dp[c], y);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dl += x[j] * y[j];
-      }
-      const int64_t lr = ((int64_t)b * a.Hq + h) * a.S + s;
-      ((float*)a.delta)[lr] = dl;
-      const float l = a.lse[lr];
-      ls = (l == -INFINITY) ? -INFINITY : -l * inv_scale;
-      l2 = (l == -INFINITY) ? -INFINITY : -l * kLog2e;
-      sg = a.seg ? a.seg[(int64_t)b * a.S + s] : 0;
+      for (int j = 0; j < 8; ++j) dl += x[j] * y[j];
     }
-    float* blk = ld + (bh * nT + t) * kLdTile;
-    blk[i] = ls;
-    blk[32 + i] = -dl;
-    reinterpret_cast<int*>(blk)[64 + i] = sg;
-    blk[96 + i] = l2;
+    dl += __shfl_xor(dl, 8, 16);
+    dl += __shfl_xor(dl, 4, 16);
+    dl += __shfl_xor(dl, 2, 16);
+    dl += __shfl_xor(dl, 1, 16);
+    if (c == 0) {
+      float ls = -INFINITY, l2 = -INFINITY;
+      int sg = -1;
+      if (s < a.S) {
+        const int64_t lr = ((int64_t)b * a.Hq + h) * a.S + s;
+        ((float*)a.delta)[lr] = dl;
+        const float l = a.lse[lr];
+        ls = (l == -INFINITY) ? -INFINITY : -l * inv_scale;
+        l2 = (l == -INFINITY) ? -INFINITY : -l * kLog2e;
+        sg = a.seg ? a.seg[(int64_t)b * a.S + s] : 0;
+      } else {
+        dl = 0.f;
+      }
+      float* blk = ld + (bh * nT + t) * kLdTile;
+      blk[i] = ls;
+      blk[32 + i] = -dl;
+      reinterpret_cast<int*>(blk)[64 + i] = sg;
+      blk[96 + i] = l2;
+    }
   }
 }
 
@@ -2523,7 +2535,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     float* ld = delta + nrows;
     const int64_t nT = (S + 31) / 32;
     if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
-      fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
+      fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       if (dkdv_variant() == 3)
         fa_bwd_dkdv128_kernel<3, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
@@ -2532,7 +2544,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       return hipGetLastError();
     }
     if (D == 64) {
-      fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
+      fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<64><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       if (dkdv_variant() == 3)
         fa_bwd_dkdv128_kernel<3, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
@@ -2540,7 +2552,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       return hipGetLastError();
     }
-    fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32, 256), 256, 0, stream>>>(a, ld);
+    fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
     static const int dq_variant = [] {
       // B4 S8192 Hq32 Hkv8 backward: 9.16 ms with dq3 vs 9.66 ms with the dq128 ring kernel
       const char* e = getenv("LLMT_FA_DQ_VARIANT");
