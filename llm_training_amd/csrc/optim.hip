@@ -84,6 +84,35 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const T* __restrict__ x, int
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// bf16 form with 16-byte loads, two per thread in flight per iteration (the 8-byte, one-load form read a
+// 218 M-element gradient at 3.7 TB/s with its 1024 partial blocks); the partials stay one per block
+__global__ __launch_bounds__(256) void sumsq8_kernel(const bf16* __restrict__ x, int64_t n8, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s0 = 0.f, s1 = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < n8; i += 2 * stride) {
+    const bf16x8 a = reinterpret_cast<const bf16x8*>(x)[i];
+    const bf16x8 b = reinterpret_cast<const bf16x8*>(x)[i + stride];
+    float fa[8], fb[8];
+    unpack8(a, fa);
+    unpack8(b, fb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s0 += fa[k] * fa[k];
+      s1 += fb[k] * fb[k];
+    }
+  }
+  if (i < n8) {
+    float fa[8];
+    unpack8(reinterpret_cast<const bf16x8*>(x)[i], fa);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s0 += fa[k] * fa[k];
+  }
+  const float s = block_sum<4>(s0 + s1, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
 __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
   __shared__ float red[4];
   float s = 0.f;
@@ -123,6 +152,11 @@ extern "C" hipError_t llmt_sumsq(const void* x, int is_fp32, int64_t n, float* o
   const int64_t n4 = n / 4;
   if (n4 == 0) return hipSuccess;
   const int grid = stream_grid(n4, 256) > 1024 ? 1024 : stream_grid(n4, 256);
+  if (!is_fp32 && n % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    sumsq8_kernel<<<grid, 256, 0, stream>>>((const bf16*)x, n / 8, ws);
+    sum_partials_kernel<<<1, 256, 0, stream>>>(ws, grid, out);
+    return hipGetLastError();
+  }
   if (is_fp32)
     sumsq_kernel<float><<<grid, 256, 0, stream>>>((const float*)x, n4, ws);
   else

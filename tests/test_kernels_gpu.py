@@ -193,6 +193,14 @@ def test_adamw_matches_torch():
     out = torch.zeros(1, device=DEV)
     lib().sumsq_(g, out)
     assert abs(out.item() - g.float().pow(2).sum().item()) / out.item() < 1e-4
+    # the 16-byte bf16 path (n % 8 == 0, aligned) incl. a grid-stride tail, the 8-byte path (odd offset)
+    for m_ in (8 * 1024 * 300 + 8, 8 * 1024 * 256 * 3 + 8 * 17):
+        gg = torch.randn(m_ + 4, device=DEV).bfloat16()
+        for view in (gg[:m_], gg[4:4 + m_]):
+            o = torch.zeros(1, device=DEV)
+            lib().sumsq_(view, o)
+            ref_ = view.float().pow(2).sum().item()
+            assert abs(o.item() - ref_) / ref_ < 1e-4
 
 
 def _attn_case(B, S, Hq, Hkv, D, causal=True, seg=None, window=-1, layout="bshd"):
