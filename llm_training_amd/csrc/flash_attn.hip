@@ -1290,691 +1290,6 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
   }
 }
 
-// ============================================================================ backward dK/dV, role-split pairs
-// grid: ceil(S/128) * Hkv * B blocks (1-D), 8 waves = 4 pairs x 32 keys, two waves per SIMD (<= 256
-// registers each; the 4-wave kernel above holds K, V, dK and dV in one wave: 404 registers, one wave per
-// SIMD, and its MFMAs idle whenever that wave waits). The two waves of a pair own the same 32 keys and
-// split each 32-query tile by role:
-//   P-wave   S = Q.K^T - lse/scale (8 MFMAs), P = exp2(S * scale * log2e) -> LDS (fp32),
-//            dV^T += dO^T . P (8 MFMAs)
-//   dS-wave  dP = dO.V^T - delta (8 MFMAs); one tile behind, dS = P . (dP - delta) with the partner's P
-//            of that tile (published by the tile barrier), dK^T += Q^T . dS (8 MFMAs)
-// so each wave keeps one of K / V and one of the dK / dV accumulators. The same 6-slot LDS-DMA ring as
-// above (each wave fetches 4 rows of Q and of dO per tile); the P exchange is double-buffered by tile
-// parity, written and read lane-linearly (16-byte columns, conflict-free).
-// Measured (opt-in, LLMT_FA_BWD_VARIANT=2): B4 S8192 Hq32 Hkv8 backward 10.81 ms vs 9.89 ms with the
-// 4-wave kernel — the per-tile barrier keeps both waves of a SIMD in the same phase (LDS reads together,
-// MFMAs together), so the second wave adds little overlap; kept for the record, not dispatched.
-template <int D>
-__global__ __launch_bounds__(512, 1) void fa_bwd_dkdv2_kernel(AttnArgs a, const float* ld) {
-  constexpr int NKK = D / 16, NDT = D / 32;
-  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
-  constexpr int NDMA = 3;              // DMA instructions per wave per tile: Q 1, dO 1, row constants 1
-  constexpr int PPAIR = 4 * 64 * 16;   // one pair's P of one tile: 4 x (64 lanes x 16 B)
-  constexpr int PBUF = 4 * PPAIR;      // four pairs
-  using QI = Img<128>;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT + 2 * PBUF];
-
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pair = wid >> 1, role = wid & 1;  // role 0: P / dV, role 1: dS / dK
-  const int S = a.S, grp = a.Hq / a.Hkv;
-  int L = (int)blockIdx.x;
-  const int hk = L % a.Hkv;
-  L /= a.Hkv;
-  const int b = L % a.B;
-  const int kb = L / a.B;
-  const int ks = kb * 128, kw = ks + pair * 32, kr = kw + r;
-  const int nT = (S + 31) / 32;
-  const int sk = (a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;
-  const float sl2 = a.scale * kLog2e;
-  const bf16* kvp = role == 0 ? a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh
-                              : a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh;
-  const int64_t kv_ss = role == 0 ? a.k_ss : a.v_ss;
-
-  bfv8 kf[NKK];  // K rows (role 0) or V rows (role 1) of this pair's keys: the B operand of S / dP
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) kf[kk] = gload8(kvp + (int64_t)min(kr, S - 1) * kv_ss + kk * 16 + hh * 8, kr < S);
-  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
-  int skv = sk;
-  asm volatile("" : "+v"(skv));
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]));
-  f32v16 acc[NDT];  // dV^T (role 0) or dK^T (role 1)
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
-
-  const RunInfo kr_run = block_run(a, b, min(ks, S - 1), min(ks + 127, S - 1));
-  const int q_beg = a.causal ? ks : max(0, kr_run.rs) / 32 * 32;
-  int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
-  if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
-  const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
-  const int T = nq * grp;
-
-  if (T > 0) {
-    int dq_off, dd_off;
-    {
-      const int row = 4 * wid + (lane >> 4);
-      const int ch = (lane & 15) ^ QI::swz(row);
-      dq_off = (row * (int)a.q_ss + ch * 8) * 2;
-      dd_off = (row * (int)a.d_ss + ch * 8) * 2;
-    }
-    const int ld_off = ((wid & 1) * 64 + lane) * 4;
-    asm volatile("" : "+v"(dq_off), "+v"(dd_off));
-    auto sl = [&](int t) -> const char* { return smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT); };
-    int iss_g = 0, iss_q = 0, iss_n = 0;
-    auto issue = [&](int t) {
-      const char* slot = sl(t);
-      const int q0 = q_beg + iss_q * BM;
-      const int h = hk * grp + iss_g;
-      const int64_t rows_left = S - q0;
-      const Rsrc qrs = make_rsrc4(a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_ss,
-                                  ((rows_left - 1) * a.q_ss + D) * 2);
-      const Rsrc drs = make_rsrc4(a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh + (int64_t)q0 * a.d_ss,
-                                  ((rows_left - 1) * a.d_ss + D) * 2);
-      const Rsrc lrs = make_rsrc4(ld + (((int64_t)b * a.Hq + h) * nT + (q0 >> 5)) * kLdTile, kLdTile * 4);
-      dma16(sgpr_rsrc(qrs), slot + 4 * wid * 256, dq_off);
-      dma16(sgpr_rsrc(drs), slot + IMG + 4 * wid * 256, dd_off);
-      dma4(sgpr_rsrc(lrs), slot + 2 * IMG + (wid & 1) * 256, ld_off);
-      if (++iss_n < T) {
-        if (++iss_q == nq) {
-          iss_q = 0;
-          ++iss_g;
-        }
-      }
-    };
-    int ini_g = 0, ini_q = 0, ini_n = 0;
-    auto tile_q0 = [&]() {
-      const int q0 = q_beg + ini_q * BM;
-      if (++ini_n < T) {
-        if (++ini_q == nq) {
-          ini_q = 0;
-          ++ini_g;
-        }
-      }
-      return q0;
-    };
-    int ro[NKK], to[NDT][2];
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) ro[kk] = QI::roff(r, 2 * kk + hh);
-    {
-      const int g = lane >> 4, i16 = lane & 15;
-      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        to[dt][0] = QI::toff(BM, row, dt * 32 + col);
-        to[dt][1] = QI::toff(BM, row + 8, dt * 32 + col);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(ro[kk]));
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
-    // this lane's 64 bytes of a pair's P image: four 16-byte columns, lane-linear within each
-    char* const pmine = smem + NS * SLOT + pair * PPAIR + lane * 16;
-
-#pragma unroll
-    for (int t = 0; t < NS - 2; ++t) issue(t);
-    wait_vm<NDMA * (NS - 3)>();  // tile 0 landed
-    ring_barrier();
-
-    f32v16 dprev;  // role 1: dP - delta of the previous tile
-    // role 1, one tile behind: dS of tile u from the partner's P and dprev, then dK^T += Q^T . dS
-    auto dk_tile = [&](int u) {
-      const char* pp = pmine + (u & 1) * PBUF;
-      f32v16 pv;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float4 f = *reinterpret_cast<const float4*>(pp + c * 1024);
-        pv[4 * c] = f.x; pv[4 * c + 1] = f.y; pv[4 * c + 2] = f.z; pv[4 * c + 3] = f.w;
-      }
-      bfv8 db[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) db[s2][j] = (__bf16)(pv[8 * s2 + j] * dprev[8 * s2 + j]);
-      const char* slot = sl(u);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const s16v4 lo = lds_tr(slot + to[dt][0] + 4096 * s2), hi = lds_tr(slot + to[dt][1] + 4096 * s2);
-          acc[dt] = mfma32(__builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)),
-                           db[s2], acc[dt]);
-        }
-    };
-
-    for (int t = 0; t < T; ++t) {
-      issue(t + NS - 2);
-      const char* slot = sl(t);
-      const float* Ls = reinterpret_cast<const float*>(slot + 2 * IMG);
-      const int q0 = tile_q0();
-      if (role == 0) {
-        // S - lse/scale (masked rows -inf) -> P
-        f32v16 sc;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float4 l4 = *reinterpret_cast<const float4*>(Ls + 8 * c + 4 * hh);
-          sc[4 * c] = l4.x; sc[4 * c + 1] = l4.y; sc[4 * c + 2] = l4.z; sc[4 * c + 3] = l4.w;
-        }
-        const bool m_seg = seg_mask(a, kr_run, q0, q0 + 31);
-        if (m_seg || (a.causal && kw + 31 > q0) || (a.window >= 0 && q0 + 31 - a.window > kw)) {
-          const int* Sg = reinterpret_cast<const int*>(Ls + 64);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            int4 s4 = make_int4(skv, skv, skv, skv);
-            if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int qi = q0 + 8 * c + 4 * hh + j;
-              bool ok = true;
-              if (a.causal) ok = ok && (kr <= qi);
-              if (a.window >= 0) ok = ok && (qi - kr <= a.window);
-              if (m_seg) ok = ok && ((&s4.x)[j] == skv);
-              sc[4 * c + j] = ok ? sc[4 * c + j] : -INFINITY;
-            }
-          }
-        }
-        bfv8 qr[NKK];
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) qr[kk] = lds_b128(slot + ro[kk]);
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) sc = mfma32(qr[kk], kf[kk], sc);
-        bfv8 pb[2];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[i] = fexp2(sc[i] * sl2);
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pb[s2][j] = (__bf16)sc[8 * s2 + j];
-        char* pp = pmine + (t & 1) * PBUF;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          *reinterpret_cast<float4*>(pp + c * 1024) = make_float4(sc[4 * c], sc[4 * c + 1], sc[4 * c + 2], sc[4 * c + 3]);
-        // dV^T += dO^T . P
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const s16v4 lo = lds_tr(slot + IMG + to[dt][0] + 4096 * s2);
-            const s16v4 hi = lds_tr(slot + IMG + to[dt][1] + 4096 * s2);
-            acc[dt] = mfma32(__builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)),
-                             pb[s2], acc[dt]);
-          }
-      } else {
-        if (t > 0) dk_tile(t - 1);
-        f32v16 dn;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
-          dn[4 * c] = d4.x; dn[4 * c + 1] = d4.y; dn[4 * c + 2] = d4.z; dn[4 * c + 3] = d4.w;
-        }
-        bfv8 dr[NKK];
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) dr[kk] = lds_b128(slot + IMG + ro[kk]);
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) dn = mfma32(dr[kk], kf[kk], dn);
-        dprev = dn;
-      }
-      wait_vm<NDMA * (NS - 3)>();
-      ring_barrier();
-    }
-    if (role == 1) dk_tile(T - 1);
-    wait_vm<0>();  // no LDS-DMA may outlive the workgroup
-  }
-
-  if (kr < S) {
-    bf16* op = role == 0 ? a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh
-                         : a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh;
-    const float f = role == 0 ? 1.f : a.scale;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint2 w;
-        w.x = pack_bf16x2(acc[dt][4 * c] * f, acc[dt][4 * c + 1] * f);
-        w.y = pack_bf16x2(acc[dt][4 * c + 2] * f, acc[dt][4 * c + 3] * f);
-        *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
-      }
-  }
-}
-
-// grid: ceil(S/128) * Hq * B blocks (1-D: the query heads of one kv head on one XCD at Hkv = 8,
-// heaviest query blocks first), 4 waves x 32 queries. Key tiles of 64 rows (K dual image, V row
-// image, segment ids) arrive in a 4-slot LDS-DMA ring; each tile is processed as two 32-key half
-// steps: half h runs the S^T/dP^T MFMAs of h beside the dS VALU + K^T reads of h-1, then the dQ MFMAs
-// of h-1 beside the row reads of h+1 (registers, one half ahead). One barrier per tile.
-__global__ __launch_bounds__(256, 1) void fa_bwd_dq128_kernel(AttnArgs a, const float* ld) {
-  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256, NS = 4;
-  constexpr int NDMA = 9;  // per wave per tile: K 4, V 4, segment ids 1
-  using KI = Img<128>;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int S = a.S, grp = a.Hq / a.Hkv;
-  const int nqb = (S + 127) / 128;
-  int L = (int)blockIdx.x;
-  const int hk = L % a.Hkv;
-  L /= a.Hkv;
-  const int h = hk * grp + L % grp;
-  L /= grp;
-  const int b = L % a.B;
-  const int mb = nqb - 1 - L / a.B;  // heaviest (last) query blocks first
-  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
-  const int nT = (S + 31) / 32;
-  const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
-  const bf16* dop = a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh;
-  const float sl2 = a.scale * kLog2e;
-  // this lane's query: -lse/scale, -delta, segment id (from the packed per-tile constants)
-  const float* blk = ld + (((int64_t)b * a.Hq + h) * nT + (min(qrow, S - 1) >> 5)) * kLdTile;
-  float lsn = qrow < S ? blk[qrow & 31] : -INFINITY;
-  float ndl = qrow < S ? blk[32 + (qrow & 31)] : 0.f;
-  int sq = qrow < S ? reinterpret_cast<const int*>(blk)[64 + (qrow & 31)] : -2;
-
-  bfv8 qf[8], df[8];
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
-    df[kk] = gload8(dop + (int64_t)min(qrow, S - 1) * a.d_ss + kk * 16 + hh * 8, qrow < S);
-  }
-  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
-  asm volatile("" : "+v"(lsn), "+v"(ndl), "+v"(sq));
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(df[kk]));
-  f32v16 dqt[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dqt[dt][i] = 0.f;
-
-  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
-  int kv_end = a.causal ? min(S, qs + 128) : S;
-  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
-  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
-
-  if (T > 0) {
-    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
-    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
-    const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
-    auto issue = [&](int t) {
-      const char* slot = smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT);
-      const int n0 = kv_beg + min(t, T - 1) * BN;
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int row0 = 16 * wid + 4 * n, row = row0 + (lane >> 4);
-        const int ch = (lane & 15) ^ KI::swz(row);
-        dma16(krs, slot + row0 * 256, ((n0 + row) * a.k_ss + ch * 8) * 2);
-        dma16(vrs, slot + IMG + row0 * 256, ((n0 + row) * a.v_ss + ch * 8) * 2);
-      }
-      dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);  // all waves write the same 256 B
-    };
-    // half step hs = 2 t + u covers keys n0(t) + 32 u ..
-    // slot base as ONE scalar (see the dK/dV kernel) and loop-constant lane offsets
-    auto hslot = [&](int hs) -> const char* {
-      return smem + __builtin_amdgcn_readfirstlane(((hs >> 1) % NS) * SLOT);
-    };
-    int ro[8], to[4][2];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
-    {
-      const int g = lane >> 4, i16 = lane & 15;
-      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        to[dt][0] = KI::toff(BN, row, dt * 32 + col);
-        to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(ro[kk]));
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
-    auto hkey0 = [&](int hs) { return kv_beg + min(hs >> 1, T - 1) * BN + 32 * (hs & 1); };
-    auto rows = [&](int hs, bfv8* kr_, bfv8* vr_) {
-      // rows 32*u.. of the half: +8192 B when u = 1 (swizzle depends on row & 15 only)
-      const char* slot = hslot(hs) + 8192 * (hs & 1);
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const char* p = slot + ro[kk];
-        kr_[kk] = lds_b128(p);
-        vr_[kk] = lds_b128(p + IMG);
-      }
-    };
-    // initial S^T / dP^T accumulators: loop-constant -lse/scale and -delta vectors used directly as the
-    // first MFMA's C operand; a half that needs a mask builds a -inf-patched copy instead
-    f32v16 sic, dic;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      sic[i] = lsn;
-      dic[i] = ndl;
-    }
-    auto need_mask = [&](int hs) {
-      const int k0 = hkey0(hs);
-      return seg_mask(a, qr, k0, k0 + 31) || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
-             (a.window >= 0 && k0 < qw + 31 - a.window);
-    };
-    auto masked_init = [&](int hs) {
-      const int k0 = hkey0(hs);
-      const bool m_seg = seg_mask(a, qr, k0, k0 + 31);
-      f32v16 si;
-      const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        int4 s4 = make_int4(sq, sq, sq, sq);
-        if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kx = k0 + 8 * c + 4 * hh + j;
-          bool ok = kx < S;
-          if (a.causal) ok = ok && (kx <= qrow);
-          if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
-          if (m_seg) ok = ok && ((&s4.x)[j] == sq);
-          si[4 * c + j] = ok ? lsn : -INFINITY;
-        }
-      }
-      return si;
-    };
-    // S^T and dP^T of half hs from the rows in kr_/vr_
-    auto sdp = [&](int hs, const bfv8* kr_, const bfv8* vr_, f32v16& sn, f32v16& dn) {
-      if (need_mask(hs))
-        sn = mfma32(kr_[0], qf[0], masked_init(hs));
-      else
-        sn = mfma32(kr_[0], qf[0], sic);
-      dn = mfma32(vr_[0], df[0], dic);
-#pragma unroll
-      for (int kk = 1; kk < 8; ++kk) {
-        sn = mfma32(kr_[kk], qf[kk], sn);
-        dn = mfma32(vr_[kk], df[kk], dn);
-      }
-    };
-
-    bfv8 kr_[8], vr_[8];
-    f32v16 sp, dp;
-    // one half step: S^T/dP^T of hs (rows already in kr_/vr_) || dS of hs-1; dQ of hs-1 || rows of hs+1
-    auto half = [&](int hs) {
-      f32v16 sn, dn;
-      const char* pslot = hslot(hs - 1);
-      const int pu = (hs - 1) & 1;
-      bfv8 trk[2][4];
-      {
-        const char* base = pslot + 8192 * pu;  // rows 32*pu..
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const char* p0 = base + to[dt][0];
-          const char* p1 = base + to[dt][1];
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const s16v4 lo = lds_tr(p0 + 4096 * s2), hi = lds_tr(p1 + 4096 * s2);
-            trk[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          }
-        }
-      }
-      sdp(hs, kr_, vr_, sn, dn);
-      bfv8 dsb[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dsb[s2][j] = (__bf16)(fexp2(sp[8 * s2 + j] * sl2) * dp[8 * s2 + j]);
-      rows(hs + 1, kr_, vr_);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) dqt[dt] = mfma32(trk[s2][dt], dsb[s2], dqt[dt]);
-      sp = sn;
-      dp = dn;
-    };
-
-#pragma unroll
-    for (int t = 0; t < NS; ++t) issue(t);
-    wait_vm<2 * NDMA>();  // tiles 0 and 1 landed
-    ring_barrier();
-    rows(0, kr_, vr_);
-    sdp(0, kr_, vr_, sp, dp);
-    rows(1, kr_, vr_);
-    for (int t = 0; t < T; ++t) {
-      half(2 * t + 1);
-      half(2 * t + 2);
-      wait_vm<NDMA>();  // tile t+2 landed (t+3 may stay in flight)
-      ring_barrier();
-      issue(t + NS);    // into tile t's slot, free after the barrier
-    }
-    wait_vm<0>();
-  }
-
-  if (qrow < S) {
-    bf16* dqp = a.out + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * a.dq_sh;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint2 w;
-        w.x = pack_bf16x2(dqt[dt][4 * c] * a.scale, dqt[dt][4 * c + 1] * a.scale);
-        w.y = pack_bf16x2(dqt[dt][4 * c + 2] * a.scale, dqt[dt][4 * c + 3] * a.scale);
-        *reinterpret_cast<uint2*>(dqp + dt * 32 + 8 * c + 4 * hh) = w;
-      }
-  }
-}
-
-// ============================================================================ forward, D = 128 pipeline
-// grid: ceil(S/128) * Hq * B blocks (1-D, kv-head-major, heaviest query blocks first), 4 waves x 32
-// queries (query on the lane: S^T = K.Q^T). K/V tiles of 64 keys arrive by LDS-DMA in a 4-slot ring
-// (two tiles in flight); each tile runs as two 32-key half steps: the S^T MFMA chain of half h beside
-// the online-softmax VALU, V^T reads and O^T += V^T.P^T MFMAs of half h-1. One barrier per tile.
-__global__ __launch_bounds__(256, 1) void fa_fwd128_kernel(AttnArgs a) {
-  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256, NS = 4;
-  constexpr int NDMA = 9;  // per wave per tile: K 4, V 4, segment ids 1
-  using KI = Img<128>;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int S = a.S, grp = a.Hq / a.Hkv;
-  const int nqb = (S + 127) / 128;
-  int L = (int)blockIdx.x;
-  const int hk = L % a.Hkv;
-  L /= a.Hkv;
-  const int h = hk * grp + L % grp;
-  L /= grp;
-  const int b = L % a.B;
-  const int mb = nqb - 1 - L / a.B;
-  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
-  const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
-  const float sl2 = a.scale * kLog2e;
-  int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
-
-  bfv8 qf[8];
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
-  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
-  asm volatile("" : "+v"(sq));
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(qf[kk]));
-  f32v16 ot[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
-  float m = -INFINITY, l = 0.f;
-
-  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
-  int kv_end = a.causal ? min(S, qs + 128) : S;
-  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
-  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
-
-  if (T > 0) {
-    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, (int64_t)S * a.k_ss * 2);
-    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, (int64_t)S * a.v_ss * 2);
-    const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
-    auto issue = [&](int t) {
-      const char* slot = smem + __builtin_amdgcn_readfirstlane((t % NS) * SLOT);
-      const int n0 = kv_beg + min(t, T - 1) * BN;
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int row0 = 16 * wid + 4 * n, row = row0 + (lane >> 4);
-        const int ch = (lane & 15) ^ KI::swz(row);
-        dma16(krs, slot + row0 * 256, ((n0 + row) * a.k_ss + ch * 8) * 2);
-        dma16(vrs, slot + IMG + row0 * 256, ((n0 + row) * a.v_ss + ch * 8) * 2);
-      }
-      dma4(srs, slot + 2 * IMG, (n0 + lane) * 4);
-    };
-    auto hslot = [&](int hs) -> const char* {
-      return smem + __builtin_amdgcn_readfirstlane(((hs >> 1) % NS) * SLOT);
-    };
-    int ro[8], to[4][2];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
-    {
-      const int g = lane >> 4, i16 = lane & 15;
-      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        to[dt][0] = KI::toff(BN, row, dt * 32 + col);
-        to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) asm volatile("" : "+v"(ro[kk]));
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
-    auto hkey0 = [&](int hs) { return kv_beg + min(hs >> 1, T - 1) * BN + 32 * (hs & 1); };
-    auto rows = [&](int hs, bfv8* kr_) {
-      const char* slot = hslot(hs) + 8192 * (hs & 1);
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) kr_[kk] = lds_b128(slot + ro[kk]);
-    };
-    // initial S^T accumulator of half hs: 0, or -inf where the key is not visible
-    auto init = [&](int hs, f32v16& si) {
-      const int k0 = hkey0(hs);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) si[i] = 0.f;
-      const bool m_seg = seg_mask(a, qr, k0, k0 + 31);
-      const bool need = m_seg || (k0 + 32 > S) || (a.causal && k0 + 31 > qw) ||
-                        (a.window >= 0 && k0 < qw + 31 - a.window) || qw + 31 >= S;
-      if (need) {
-        const int* Sg = reinterpret_cast<const int*>(hslot(hs) + 2 * IMG) + 32 * (hs & 1);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          int4 s4 = make_int4(sq, sq, sq, sq);
-          if (m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int kx = k0 + 8 * c + 4 * hh + j;
-            bool ok = kx < S && qrow < S;
-            if (a.causal) ok = ok && (kx <= qrow);
-            if (a.window >= 0) ok = ok && (qrow - kx <= a.window);
-            if (m_seg) ok = ok && ((&s4.x)[j] == sq);
-            si[4 * c + j] = ok ? 0.f : -INFINITY;
-          }
-        }
-      }
-    };
-
-    bfv8 kr_[8];
-    f32v16 sp;
-    auto half = [&](int hs) {
-      f32v16 sn;
-      init(hs, sn);
-      const char* pslot = hslot(hs - 1);
-      const int pu = (hs - 1) & 1;
-      bfv8 trv[2][4];
-      {
-        const char* base = pslot + IMG + 8192 * pu;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const char* p0 = base + to[dt][0];
-          const char* p1 = base + to[dt][1];
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const s16v4 lo = lds_tr(p0 + 4096 * s2), hi = lds_tr(p1 + 4096 * s2);
-            trv[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          }
-        }
-      }
-      // online softmax of half hs-1 (deferred rescale: keep the running max unless a row grew > kThr)
-      float smax = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        sp[i] *= sl2;
-        smax = fmaxf(smax, sp[i]);
-      }
-      smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
-      if (__any(smax > m + kThr)) {
-        const float mnew = fmaxf(m, smax);
-        const float alpha = (mnew == -INFINITY) ? 1.f : fexp2(m - mnew);
-        m = mnew;
-        l *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
-      }
-      const float muse = (m == -INFINITY) ? 0.f : m;
-      // one basic block from here: S^T chain of half hs || exp of half hs-1, then P.V of hs-1
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) sn = mfma32(kr_[kk], qf[kk], sn);
-      bfv8 pb[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float p = fexp2(sp[8 * s2 + j] - muse);
-          l += p;
-          pb[s2][j] = (__bf16)p;
-        }
-      rows(hs + 1, kr_);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) ot[dt] = mfma32(trv[s2][dt], pb[s2], ot[dt]);
-      sp = sn;
-    };
-
-#pragma unroll
-    for (int t = 0; t < NS; ++t) issue(t);
-    wait_vm<2 * NDMA>();  // tiles 0 and 1 landed
-    ring_barrier();
-    rows(0, kr_);
-    init(0, sp);
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) sp = mfma32(kr_[kk], qf[kk], sp);
-    rows(1, kr_);
-    for (int t = 0; t < T; ++t) {
-      half(2 * t + 1);
-      half(2 * t + 2);
-      wait_vm<NDMA>();
-      ring_barrier();
-      issue(t + NS);
-    }
-    wait_vm<0>();
-  }
-
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qrow < S) {
-    bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint2 w;
-        w.x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
-        w.y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
-        *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
-      }
-    if (hh == 0) {
-      const float muse = (m == -INFINITY) ? 0.f : m;
-      a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (muse + __log2f(lt)) * kLn2 : -INFINITY;
-    }
-  }
-}
-
 // ============================================================================ forward, D = 128, v3
 // grid: ceil(S/128) * Hq * B blocks (1-D, kv-head-major, heaviest query blocks first), 4 waves x 32
 // queries, two workgroups per CU. Differences from fa_fwd_kernel<128>, each aimed at the exposed LDS
@@ -2391,8 +1706,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
 using namespace llmt;
 
 // dK/dV kernel variant, read on every launch so one process can A/B them (LLMT_FA_BWD_VARIANT):
-//   1 = end-of-tile barrier after an LDS drain, 3 = barrier without the drain (rows prefetched for the next
-//   tile stay in flight across it), 0 = sched-group pinned schedule, 2 = role-split 8-wave pairs (D128)
+//   1 = end-of-tile barrier after an LDS drain and scalar softmax (A/B reference), 3 = barrier without
+//   the drain (rows prefetched for the next tile stay in flight across it) and packed softmax,
+//   0 = sched-group pinned schedule
 static int dkdv_variant() {
   const char* e = getenv("LLMT_FA_BWD_VARIANT");
   return e ? atoi(e) : 3;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
@@ -2447,8 +1763,9 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   a.scale = scale; a.causal = causal; a.window = window;
   set_dropout(a, drop_p, drop_seed);
   dim3 grid((S + 127) / 128, Hq, B);
-  // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907, fwd128 1.043;
-  // 3 = fwd3 with compiler-placed row-sum adds (A/B); read per launch
+  // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907 (variant 0), the
+  // removed one-wave-per-SIMD ring forward 1.043; 3 = fwd3 with compiler-placed row-sum adds, 2 = with the
+  // inline-asm adds (A/B reference); read per launch
   const char* fve = getenv("LLMT_FA_FWD_VARIANT");
   const int variant = fve ? atoi(fve) : 3;  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
   switch (D) {
@@ -2467,8 +1784,6 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
     case 128: {
       if (a.drop_thresh)  // dropout lives in the generic kernels
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
-      else if (variant == 1)
-        fa_fwd128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (variant == 2)  // row sums through the inline-asm add (each behind its own wait state)
         fa_fwd3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (variant == 3)
@@ -2553,22 +1868,14 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       return hipGetLastError();
     }
     fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
-    static const int dq_variant = [] {
-      // B4 S8192 Hq32 Hkv8 backward: 9.16 ms with dq3 vs 9.66 ms with the dq128 ring kernel
-      const char* e = getenv("LLMT_FA_DQ_VARIANT");
-      return e ? atoi(e) : 3;
-    }();
-    if (dq_variant == 3)
-      fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-    else
-      fa_bwd_dq128_kernel<<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a, ld);
+    // dQ: B4 S8192 Hq32 Hkv8 backward 9.16 ms with dq3 vs 9.66 ms with the earlier one-wave-per-SIMD ring
+    // kernel (removed, like the 8-wave role-split dK/dV kernel: 10.81 vs 9.89 ms, and the ring forward)
+    fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     const int variant = dkdv_variant();
     if (variant == 3)
       fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 1)
       fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 2)
-      fa_bwd_dkdv2_kernel<128><<<(S + 127) / 128 * Hkv * B, 512, 0, stream>>>(a, ld);
     else
       fa_bwd_dkdv128_kernel<0><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     return hipGetLastError();
