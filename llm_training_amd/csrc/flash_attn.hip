@@ -1227,17 +1227,6 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
       sdp(qr, dr, sn, dn);
       bfv8 pb[2], db[2];
       softmax(pslot, mprev, sacc, dacc, pb, db);
-      if constexpr (V == 0) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
-        }
-        // pin the S/dP chains of tile t inside region A (IR passes otherwise sink them into region B)
-        asm volatile("" : "+v"(sn), "+v"(dn));
-        __builtin_amdgcn_sched_barrier(0);
-      }
       // ---- region B: dV/dK of tile t-1  ||  row reads of tile t+1
       rows(smem + sl_p1, qr, dr);
 #pragma unroll
@@ -1247,14 +1236,6 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
           dvt[dt] = mfma32(trd[s2][dt], pb[s2], dvt[dt]);
           dkt[dt] = mfma32(trq[s2][dt], db[s2], dkt[dt]);
         }
-      if constexpr (V == 0) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // DS read
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
       sacc = sn;
       dacc = dn;
       mprev = mcur;
@@ -1707,8 +1688,8 @@ using namespace llmt;
 
 // dK/dV kernel variant, read on every launch so one process can A/B them (LLMT_FA_BWD_VARIANT):
 //   1 = end-of-tile barrier after an LDS drain and scalar softmax (A/B reference), 3 = barrier without
-//   the drain (rows prefetched for the next tile stay in flight across it) and packed softmax,
-//   0 = sched-group pinned schedule
+//   the drain (rows prefetched for the next tile stay in flight across it) and packed softmax. (A
+//   sched-group pinned schedule of the same loop measured 9.17 vs 8.12 ms at B4 S8192 and was removed.)
 static int dkdv_variant() {
   const char* e = getenv("LLMT_FA_BWD_VARIANT");
   return e ? atoi(e) : 3;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
@@ -1874,10 +1855,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     const int variant = dkdv_variant();
     if (variant == 3)
       fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 1)
-      fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else
-      fa_bwd_dkdv128_kernel<0><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     return hipGetLastError();
   }
   if (gqa && !work) return hipErrorInvalidValue;
