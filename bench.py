@@ -139,6 +139,8 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--attn", default="flash", choices=["flash", "sdpa", "eager"])
     ap.add_argument("--ckpt", action="store_true", help="full activation checkpointing")
+    ap.add_argument("--ckpt-keep-attn", action="store_true",
+                    help="with --ckpt: keep the flash-attention outputs (recompute_granularity full_keep_attention)")
     ap.add_argument("--offload-optimizer", action="store_true", help="fp32 master/Adam state in host memory")
     ap.add_argument("--loss-chunk", type=int, default=8192, help="rows per lm_head GEMM of the fused CE")
     ap.add_argument("--force-sharded", action="store_true",
@@ -179,6 +181,8 @@ def main():
         cfg["num_hidden_layers"] = args.layers
     common = dict(attn_implementation=args.attn, enable_gradient_checkpointing=args.ckpt,
                   loss_chunk_size=args.loss_chunk)
+    if args.ckpt and args.ckpt_keep_attn:
+        common["recompute_granularity"] = "full_keep_attention"
     if phi3:
         from llm_training_amd.models.phi3 import Phi3 as Model
         from llm_training_amd.models.phi3 import Phi3Config as MCfg
@@ -292,7 +296,9 @@ def main():
         par = f"dp{pc.dp_size}" + (f"-tp{pc.tp_size}" if pc.tp_size > 1 else "")
         cfg_out = {"model": model_name if not args.layers else f"{model_name}-{args.layers}L(INVALID-debug)",
                    "global_batch": pc.dp_size * B, "seq_len": S, "parallelism": par, "zero_stage": stage,
-                   "attn": args.attn, "activation_checkpointing": args.ckpt,
+                   "attn": args.attn,
+                   "activation_checkpointing": ("full_keep_attention" if args.ckpt and args.ckpt_keep_attn
+                                                else args.ckpt),
                    "optimizer": ("host AdamW (offload) fp32 master" if args.offload_optimizer
                                  else "fused AdamW fp32 master"),
                    "grad_clip": 1.0, "gemm_tuning": gemm_mode}

@@ -32,6 +32,7 @@ from ..parallel import tensor_parallel as tpl
 from ..parallel.context import ParallelContext
 from .base import BaseModel, BaseModelConfig, CausalLMOutput, load_hf_config_dict, to_dtype
 from .modules import Linear, RMSNorm, VocabParallelEmbedding, normal_
+from .utils import keep_attention_context
 
 logger = logging.getLogger("llm_training")
 
@@ -59,7 +60,10 @@ class LlamaConfig(BaseModelConfig):
     tp_comm_overlap: bool = True
     mlp_bias: bool = False
     enable_gradient_checkpointing: bool = False
-    recompute_granularity: Literal["full", "selective"] = "full"
+    # "full_keep_attention": full layer recompute except the flash-attention forward, whose output and LSE
+    # are kept (torch selective-checkpoint policy on llmt::flash_attn_fwd): + S*B*H*2 bytes per layer, one
+    # attention forward less per step (the long-context cost: attention dominates at 128K)
+    recompute_granularity: Literal["full", "selective", "full_keep_attention"] = "full"
     # loss-head chunking of the fused linear + cross-entropy (rows per lm_head GEMM)
     loss_chunk_size: int = 8192
 
@@ -269,14 +273,17 @@ class Llama(BaseModel):
             x = embed_hook(x)
         rt = self._runtime(input_ids, position_ids, segment_ids, device, S, B)
         residual = None
+        gran = self.config.recompute_granularity
         for layer in self.layers:
-            if (self.gradient_checkpointing and self.config.recompute_granularity == "full" and self.training
+            if (self.gradient_checkpointing and gran in ("full", "full_keep_attention") and self.training
                     and torch.is_grad_enabled()):
+                kw = {"use_reentrant": False}
+                if gran == "full_keep_attention":
+                    kw["context_fn"] = keep_attention_context
                 if residual is None:
-                    x, residual = ckpt.checkpoint(lambda a, lay=layer: lay(a, None, rt), x, use_reentrant=False)
+                    x, residual = ckpt.checkpoint(lambda a, lay=layer: lay(a, None, rt), x, **kw)
                 else:
-                    x, residual = ckpt.checkpoint(lambda a, r, lay=layer: lay(a, r, rt), x, residual,
-                                                  use_reentrant=False)
+                    x, residual = ckpt.checkpoint(lambda a, r, lay=layer: lay(a, r, rt), x, residual, **kw)
             else:
                 x, residual = layer(x, residual, rt)
         h, _ = self.norm(x, residual)

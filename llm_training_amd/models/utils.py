@@ -38,3 +38,18 @@ def init_on_device(device: torch.device | str, include_buffers: bool = False):
 
 def init_empty_weights(include_buffers: bool = False):
     return init_on_device(torch.device("meta"), include_buffers=include_buffers)
+
+
+def _keep_attention_policy(ctx, op, *args, **kwargs):
+    from torch.utils.checkpoint import CheckpointPolicy
+    if str(op).startswith("llmt.flash_attn_fwd"):  # the OpOverload llmt::flash_attn_fwd.default
+        return CheckpointPolicy.MUST_SAVE
+    return CheckpointPolicy.PREFER_RECOMPUTE
+
+
+def keep_attention_context():
+    """Selective-checkpoint contexts for ``recompute_granularity: full_keep_attention``: a checkpointed
+    decoder layer saves the flash-attention forward's outputs (O and the LSE) and recomputes everything
+    else in backward."""
+    from torch.utils.checkpoint import create_selective_checkpoint_contexts
+    return create_selective_checkpoint_contexts(_keep_attention_policy)

@@ -247,3 +247,50 @@ def test_hf_causal_lm_uses_hip_attention_packed():
     assert len(calls) == 2  # one flash call per layer
     err = ((hg.float().cpu() - hc).norm() / hc.norm()).item()
     assert err < 3e-2, err
+
+
+@pytest.mark.gpu
+def test_checkpoint_keep_attention_skips_the_attention_recompute():
+    """recompute_granularity full_keep_attention: the flash-attention forward runs once per layer (its O /
+    LSE are kept by the selective-checkpoint policy) instead of twice under full recompute, and the
+    gradients equal the full-recompute ones bitwise (deterministic kernels)."""
+    import os
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    class Count(TorchDispatchMode):
+        def __init__(self):
+            super().__init__()
+            self.n = 0
+
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            if str(func).startswith("llmt.flash_attn_fwd"):
+                self.n += 1
+            return func(*args, **(kwargs or {}))
+
+    os.environ["LLMT_DETERMINISTIC"] = "1"
+    try:
+        dev = torch.device("cuda", 0)
+        ids = torch.randint(0, 1024, (2, 512), device=dev)
+        res = {}
+        for gran in ("full", "full_keep_attention"):
+            cfg = LlamaConfig(vocab_size=1024, hidden_size=256, intermediate_size=512, num_hidden_layers=3,
+                              num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=1024,
+                              enable_gradient_checkpointing=True, recompute_granularity=gran)
+            m = Llama(cfg, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
+            m.init_weights(5)
+            m.train()
+            with Count() as c:
+                loss = m(ids).logits.float().square().mean()
+                loss.backward()
+            res[gran] = (c.n, {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    finally:
+        os.environ.pop("LLMT_DETERMINISTIC", None)
+    assert res["full"][0] == 6 and res["full_keep_attention"][0] == 3, (res["full"][0], res["full_keep_attention"][0])
+    g0, g1 = res["full"][1], res["full_keep_attention"][1]
+    assert g0.keys() == g1.keys()
+    # bitwise except the embedding gradient, whose scatter-add order is not fixed outside deterministic
+    # mode's sort-based kernel (chosen when the model is built from the process environment)
+    bad = [k for k in g0 if not torch.equal(g0[k], g1[k]) and "embed" not in k]
+    assert not bad, bad
+    e = [k for k in g0 if "embed" in k][0]
+    assert ((g0[e].float() - g1[e].float()).norm() / g0[e].float().norm()).item() < 1e-2

@@ -186,7 +186,7 @@ def test_orpo_loss_matches_formula():
     assert abs(loss.item() - (or_loss + ce).item()) < 1e-4
 
 
-@pytest.mark.parametrize("granularity", ["full", "selective"])
+@pytest.mark.parametrize("granularity", ["full", "selective", "full_keep_attention"])
 def test_activation_checkpointing_matches(granularity):
     from llm_training_amd.models.llama import Llama
     from llm_training_amd.parallel.context import ParallelContext
