@@ -799,15 +799,15 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward, D = 128 pipeline
-// The D = 128 backward (every Llama-family model) runs a software-pipelined pair of kernels built
-// for one wave per SIMD (512 registers per lane):
-//  * Q / dO (dK/dV pass) tiles arrive by LDS-DMA (`buffer_load ... lds`, zero-filled past the end) into
-//    a ring of NS slots, several tiles ahead, behind counted `s_waitcnt vmcnt` and a raw barrier — the
-//    loads no longer stall every iteration (the v2 kernels waited on a one-tile-ahead register stage).
-//  * per-row constants are folded into the MFMA accumulators' initial values: S' = Q.K^T - lse/scale,
-//    dP' = dO.V^T - delta, so P = exp2(S' * scale * log2e) and dS = P * dP' need no subtraction; rows
-//    that must not contribute (past S, masked) start at -inf, so only diagonal / window / packed tiles
-//    pay for a mask and it is applied once, to the initial values.
+// The D = 64 / 96 / 128 backward (every Llama-family and Phi-3 model) is: a prep kernel (delta and the
+// packed per-row constants below), the query-parallel dQ kernel (fa_bwd_dq3_kernel, two workgroups per
+// CU) and this key-parallel dK/dV kernel, built for one wave per SIMD (512 registers per lane):
+//  * Q / dO tiles arrive by LDS-DMA (`buffer_load ... lds`, zero-filled past the end) into a ring of NS
+//    slots, several tiles ahead, behind counted `s_waitcnt vmcnt` and a raw barrier.
+//  * one wave per SIMD issues one instruction per issue slot, so the loop is instruction-bound, not
+//    MFMA-bound (profiles/r2_dkdv_issue_bound.md): descriptors are built once per head, S / dP start
+//    from the MFMA's inline zero and the row constants enter the softmax (P = exp2(fma(S, scale*log2e,
+//    -lse*log2e)), dS = P (dP - delta), packed fp32), masks only on diagonal / window / packed tiles.
 //  * each iteration overlaps the S/dP MFMAs of tile t with the softmax VALU and transposed LDS reads of
 //    tile t-1, and the dV/dK MFMAs of tile t-1 with the row reads of tile t+1.
 //  * the dK/dV workgroup loops over every query head of its kv-head group, so GQA needs no fp32
