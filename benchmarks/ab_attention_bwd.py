@@ -12,6 +12,7 @@ from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D = (int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (4, 8192, 32, 8, 128)))
 variants = (sys.argv[6] if len(sys.argv) > 6 else "1,3").split(",")
+ENV = sys.argv[7] if len(sys.argv) > 7 else "LLMT_FA_BWD_VARIANT"  # or LLMT_FA_DQ_VARIANT
 q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
@@ -21,7 +22,7 @@ grads = {}
 times = {x: [] for x in variants}
 for rnd in range(5):
     for var in variants:
-        os.environ["LLMT_FA_BWD_VARIANT"] = var
+        os.environ[ENV] = var
         for _ in range(2):
             g = torch.autograd.grad(o, (q, k, v), do, retain_graph=True)
         torch.cuda.synchronize()
@@ -34,7 +35,7 @@ for rnd in range(5):
         times[var].append(a.elapsed_time(b) / 10)
         grads[var] = g
 ref = grads[variants[0]]
-out = {"shape": [B, S, Hq, Hkv, D]}
+out = {"shape": [B, S, Hq, Hkv, D], "env": ENV}
 for var in variants:
     out[f"v{var}_ms"] = round(sorted(times[var])[len(times[var]) // 2], 4)
     out[f"v{var}_max_abs_diff_vs_v{variants[0]}"] = max(float((x - y).abs().max()) for x, y in zip(grads[var], ref))

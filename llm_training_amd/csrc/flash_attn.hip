@@ -1511,7 +1511,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 // V row reads -> dP^T = V.dO^T, dS = P (dP - delta) with P = exp2(S * scale * log2e - lse * log2e)
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
 // dQ = scale * sum; the row constants come straight from lse / delta (delta written by the prep kernel).
-template <int D>
+template <int D, bool IL = true>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
@@ -1615,10 +1615,20 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
           st[i] = 0.f;
           dpt[i] = 0.f;
         }
+        if constexpr (IL) {
+          // V row kk reloads fr[kk] right behind the S^T MFMA that consumed it: the V reads fly under the
+          // rest of the S^T chain instead of starting after it
 #pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) st = mfma32(fr[kk], qf[kk], st);
+          for (int kk = 0; kk < NKK; ++kk) {
+            st = mfma32(fr[kk], qf[kk], st);
+            fr[kk] = lds_b128(slot + IMG + 8192 * tt + ro[kk]);
+          }
+        } else {
 #pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) fr[kk] = lds_b128(slot + IMG + 8192 * tt + ro[kk]);
+          for (int kk = 0; kk < NKK; ++kk) st = mfma32(fr[kk], qf[kk], st);
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) fr[kk] = lds_b128(slot + IMG + 8192 * tt + ro[kk]);
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) dpt = mfma32(fr[kk], df[kk], dpt);
@@ -1851,7 +1861,15 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
     // dQ: B4 S8192 Hq32 Hkv8 backward 9.16 ms with dq3 vs 9.66 ms with the earlier one-wave-per-SIMD ring
     // kernel (removed, like the 8-wave role-split dK/dV kernel: 10.81 vs 9.89 ms, and the ring forward)
-    fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+    {
+      // LLMT_FA_DQ_VARIANT=0: V reads after the whole S^T chain (A/B reference, read per launch); the
+      // default interleaves them: B4 S8192 backward 8.00 -> 7.93 ms in one process, same gradients
+      const char* dqe = getenv("LLMT_FA_DQ_VARIANT");
+      if (dqe && atoi(dqe) == 0)
+        fa_bwd_dq3_kernel<128, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else
+        fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+    }
     const int variant = dkdv_variant();
     if (variant == 3)
       fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
