@@ -22,6 +22,8 @@ hipError_t llmt_rmsnorm_bwd(const void* dy, const void* x, const void* w, const 
                             hipStream_t stream);
 hipError_t llmt_swiglu_fwd(const void* gu, void* c, int64_t T, int I, hipStream_t stream);
 hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu, int64_t T, int I, hipStream_t stream);
+hipError_t llmt_swiglu_bwd_tr(const void* gu, const void* dc, void* dgu, void* dguT, int64_t T, int I,
+                              hipStream_t stream);
 hipError_t llmt_transpose2d(const void* in, void* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo,
                             hipStream_t stream);
 hipError_t llmt_splitk_reduce(const float* slabs, int nsplit, int64_t n, void* out, int out_is_fp32, int accumulate,
@@ -174,6 +176,21 @@ at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dc) {
   check(llmt_swiglu_bwd(gu.data_ptr(), dc.data_ptr(), dgu.data_ptr(), gu.numel() / I2, (int)(I2 / 2), cur_stream()),
         "swiglu_bwd");
   return dgu;
+}
+
+// SwiGLU backward that also returns dgu^T [2I, T] (T, I multiples of 64)
+std::tuple<at::Tensor, at::Tensor> swiglu_bwd_tr(const at::Tensor& gu, const at::Tensor& dc) {
+  check_bf16_cuda(gu, "gate_up");
+  check_bf16_cuda(dc, "dc");
+  TORCH_CHECK(gu.is_contiguous() && dc.is_contiguous(), "swiglu_bwd_tr: contiguous inputs");
+  const int64_t I2 = gu.size(-1), T = gu.numel() / I2;
+  TORCH_CHECK(dc.numel() == T * (I2 / 2), "swiglu_bwd_tr: dc must be [T, I]");
+  auto dgu = at::empty_like(gu);
+  auto dguT = at::empty({I2, T}, gu.options());
+  check(llmt_swiglu_bwd_tr(gu.data_ptr(), dc.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), T, (int)(I2 / 2),
+                           cur_stream()),
+        "swiglu_bwd_tr");
+  return {dgu, dguT};
 }
 
 // ---------------------------------------------------------------- RoPE (in place)
@@ -464,6 +481,7 @@ TORCH_LIBRARY(llmt, m) {
   m.def("swiglu_bwd(Tensor gu, Tensor dc) -> Tensor");
   m.def("transpose_(Tensor x, Tensor(a!) out) -> ()");
   m.def("splitk_reduce_(Tensor slabs, Tensor(a!) out, bool accumulate) -> ()");
+  m.def("swiglu_bwd_tr(Tensor gu, Tensor dc) -> (Tensor, Tensor)");
   m.def("rope_(Tensor(a!) qkv, Tensor pos, Tensor cos, Tensor sin, int nheads, bool inverse) -> ()");
   m.def(
       "cross_entropy_(Tensor(a!) logits, Tensor labels, int vocab_start, int ignore_index, Tensor? lse_in, "
@@ -492,6 +510,7 @@ TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("transpose_", &transpose_);
   m.impl("splitk_reduce_", &splitk_reduce_);
+  m.impl("swiglu_bwd_tr", &swiglu_bwd_tr);
   m.impl("rope_", &rope_);
   m.impl("cross_entropy_", &cross_entropy_);
   m.impl("adamw_", &adamw_);

@@ -231,3 +231,85 @@ extern "C" hipError_t llmt_splitk_reduce(const float* slabs, int nsplit, int64_t
                                                                                 (llmt::bf16*)out, accumulate);
   return hipGetLastError();
 }
+
+// SwiGLU backward that also writes dgu^T [2I, T]: the token-contiguous copy the gate_up weight gradient
+// needs for hipBLASLt's TN kernel (4.81 vs 5.58 ms for the TT form at T = 32768, I = 14336), produced while
+// the tile is in registers instead of by a separate transpose pass that re-reads dgu (0.82 ms). One block
+// per 64 tokens x 64 intermediate columns: gate / up / dc rows in, dgu rows out, both halves transposed
+// through LDS (rows padded to 66 elements) and written as 128-byte token runs. T and I multiples of 64.
+namespace llmt {
+__global__ __launch_bounds__(256) void swiglu_bwd_tr_kernel(const bf16* __restrict__ gu, const bf16* __restrict__ dc,
+                                                            bf16* __restrict__ dgu, bf16* __restrict__ dguT,
+                                                            int64_t T, int I) {
+  // LDS tiles of 32-bit words: word [col][p] = (token 2p, token 2p+1) of one output column, so the
+  // transposed rows come out as 16-byte reads (4 words = 8 tokens); rows padded to 36 words
+  constexpr int PW = 36;
+  __shared__ uint32_t tg[64 * PW];
+  __shared__ uint32_t tu[64 * PW];
+  const int j0 = blockIdx.x * 64;
+  const int64_t t0 = (int64_t)blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  const int cc = tid & 7, p = tid >> 3;  // 8 lanes cover a 128-byte row run; 32 token pairs
+  const int c = cc * 8;
+  uint32_t wg[8], wu[8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t t = t0 + 2 * p + h;
+    const bf16* grow = gu + t * 2 * I;
+    bf16* drow = dgu + t * 2 * I;
+    float a[8], b[8], g[8], da[8], db[8];
+    unpack8(*reinterpret_cast<const bf16x8*>(grow + j0 + c), a);
+    unpack8(*reinterpret_cast<const bf16x8*>(grow + I + j0 + c), b);
+    unpack8(*reinterpret_cast<const bf16x8*>(dc + t * I + j0 + c), g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // the swiglu_bwd_kernel math, element for element
+      const float sg = sigmoidf_(a[i]);
+      const float silu = a[i] * sg;
+      da[i] = g[i] * b[i] * sg * (1.f + a[i] * (1.f - sg));
+      db[i] = g[i] * silu;
+    }
+    const bf16x8 pa = pack8(da), pb = pack8(db);
+    *reinterpret_cast<bf16x8*>(drow + j0 + c) = pa;
+    *reinterpret_cast<bf16x8*>(drow + I + j0 + c) = pb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t lo_g = pa.w[i] & 0xffffu, hi_g = pa.w[i] >> 16;
+      const uint32_t lo_u = pb.w[i] & 0xffffu, hi_u = pb.w[i] >> 16;
+      if (h == 0) {
+        wg[2 * i] = lo_g; wg[2 * i + 1] = hi_g;
+        wu[2 * i] = lo_u; wu[2 * i + 1] = hi_u;
+      } else {
+        wg[2 * i] |= lo_g << 16; wg[2 * i + 1] |= hi_g << 16;
+        wu[2 * i] |= lo_u << 16; wu[2 * i + 1] |= hi_u << 16;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    tg[(c + i) * PW + p] = wg[i];
+    tu[(c + i) * PW + p] = wu[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + 256 * k;
+    const int j = idx >> 3, ch = idx & 7;  // output row j, tokens 8ch .. 8ch+7
+    const uint4 vg = *reinterpret_cast<const uint4*>(tg + j * PW + 4 * ch);
+    const uint4 vu = *reinterpret_cast<const uint4*>(tu + j * PW + 4 * ch);
+    *reinterpret_cast<uint4*>(dguT + (int64_t)(j0 + j) * T + t0 + ch * 8) = vg;
+    *reinterpret_cast<uint4*>(dguT + (int64_t)(I + j0 + j) * T + t0 + ch * 8) = vu;
+  }
+}
+}  // namespace llmt
+
+extern "C" hipError_t llmt_swiglu_bwd_tr(const void* gu, const void* dc, void* dgu, void* dguT, int64_t T, int I,
+                                         hipStream_t stream) {
+  if (T % 64 || I % 64 || T == 0) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(gu) | reinterpret_cast<uintptr_t>(dc) | reinterpret_cast<uintptr_t>(dgu) |
+       reinterpret_cast<uintptr_t>(dguT)) & 15)
+    return hipErrorInvalidValue;
+  if (T / 64 > 65535) return hipErrorInvalidValue;
+  llmt::swiglu_bwd_tr_kernel<<<dim3((unsigned)(I / 64), (unsigned)(T / 64)), 256, 0, stream>>>(
+      (const llmt::bf16*)gu, (const llmt::bf16*)dc, (llmt::bf16*)dgu, (llmt::bf16*)dguT, T, I);
+  return hipGetLastError();
+}

@@ -213,6 +213,9 @@ def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
 
 def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate: bool) -> bool:
     """out [N, K] (+)= dy[M, N]^T @ x[M, K] on the selected GEMM path; False if only torch can do it."""
+    dy_t = _DY_T.pop(dy.data_ptr(), None) if _DY_T else None
+    if dy_t is not None and (tuple(dy_t.shape) != (dy.shape[1], dy.shape[0]) or not dy.is_contiguous()):
+        dy_t = None
     if not (out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32)):
         return False
     path = _path("wgrad", dy.shape[0], x.shape[1], dy, x)
@@ -220,6 +223,10 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
     K = x.shape[1]
     if path == "lt" and TRANSPOSE_LAYOUTS[0] and M >= _TR_WGRAD_MIN_M and _tr_ok(dy, x):
         sk, o2 = ALLOW_STREAMK[0], out.view(N, K)
+        if dy_t is not None:
+            # dy^T came with dy (the SwiGLU backward wrote both): TN, both operands token-contiguous
+            lib().gemm_lt(transpose(x), dy_t, o2, True, False, K, N, M, M, M, K, accumulate, sk)
+            return True
 
         def nt():  # dW^T (K x N) = x^T (K x M) . dy (M x N), straight from the token-major operands
             lib().gemm_lt(x, dy, o2, False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, sk)
@@ -330,6 +337,7 @@ class _LinearFn(Function):
             dx = mm_nn(dy2 if dy2.stride(-1) == 1 else dy2.contiguous(), w).view(*dy.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _wgrad_mm(w, dy2.t(), x.reshape(-1, x.shape[-1]))
+        _DY_T.clear()  # consumed above, or not needed (frozen weight)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy2.sum(0)
         return dx, dw, db
@@ -442,6 +450,20 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tenso
 # ----------------------------------------------------------------------------- SwiGLU
 
 
+# Token-contiguous transposes of input gradients, produced by the kernel that wrote the gradient (the
+# SwiGLU backward) for the weight gradient of the layer that consumes it next (gate_up): data_ptr -> dy^T.
+# At most one entry lives at a time; the consuming linear backward pops it.
+_DY_T: dict[int, torch.Tensor] = {}
+# opt-in (LLMT_SWIGLU_DY_T=1): the TN weight gradient it enables (4.8 vs 5.6 ms for gate_up) gains about
+# what the extra transposed write costs on Llama-3-8B (same-box steps, on / off / on: 21,666 / 21,632 /
+# 21,759 tok/s; with the first 16-bit LDS transpose 21,895 / 21,888 / 21,873)
+FUSED_DY_T = [os.environ.get("LLMT_SWIGLU_DY_T", "0") == "1"]
+
+
+def drop_dy_t():
+    _DY_T.clear()
+
+
 class _SwiGLUFn(Function):
     @staticmethod
     def forward(ctx, gu):
@@ -452,7 +474,17 @@ class _SwiGLUFn(Function):
     @staticmethod
     def backward(ctx, dc):
         (gu,) = ctx.saved_tensors
-        return lib().swiglu_bwd(gu, dc.contiguous())
+        dc = dc.contiguous()
+        _DY_T.clear()
+        I2 = gu.shape[-1]
+        T = gu.numel() // I2
+        if (FUSED_DY_T[0] and TRANSPOSE_LAYOUTS[0] and T % 64 == 0 and (I2 // 2) % 64 == 0
+                and T >= _TR_WGRAD_MIN_M and GEMM_MODES.get("wgrad") == "lt"):
+            # dgu plus dgu^T in one pass: the gate_up weight gradient then runs hipBLASLt's TN kernel
+            dgu, dgu_t = lib().swiglu_bwd_tr(gu, dc)
+            _DY_T[dgu.data_ptr()] = dgu_t
+            return dgu
+        return lib().swiglu_bwd(gu, dc)
 
 
 def swiglu(gate_up: torch.Tensor) -> torch.Tensor:

@@ -169,7 +169,7 @@ class _AGLinear(Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from ..ops.fused import _wgrad_mm, mm_nn
+        from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn
         (full,) = ctx.saved_tensors
         w, group = ctx.w, ctx.group
         n = _ws(group)
@@ -186,6 +186,7 @@ class _AGLinear(Function):
             db = dy2.sum(0)
         if work is not None:
             work.wait()
+        drop_dy_t()  # a SwiGLU-produced dy^T is only used by the plain linear path
         return dx, dw, db, None
 
 
@@ -206,7 +207,7 @@ class _LinearRS(Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from ..ops.fused import _wgrad_mm, mm_nn
+        from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn
         (x,) = ctx.saved_tensors
         w, group = ctx.w, ctx.group
         n, r = _ws(group), dist.get_rank(group)
@@ -231,6 +232,7 @@ class _LinearRS(Function):
             dw = _wgrad_mm(w, f2.t(), _rows(x))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _rows(dy).sum(0)
+        drop_dy_t()  # a SwiGLU-produced dy^T is only used by the plain linear path
         return dx, dw, db, None
 
 

@@ -84,6 +84,40 @@ def test_rope_inplace_roundtrip(D):
     assert _rel(x, qkv) < 2e-2
 
 
+def test_swiglu_bwd_with_transposed_gradient(monkeypatch):
+    """swiglu_bwd_tr: dgu equal to swiglu_bwd bitwise and dgu^T its exact transpose; through the ops, the
+    gate_up weight gradient takes it (TN) and matches the path without it."""
+    import llm_training_amd.ops.fused as fused
+    torch.manual_seed(0)
+    T, I = 4096, 512
+    gu = torch.randn(T, 2 * I, device=DEV).bfloat16()
+    dc = torch.randn(T, I, device=DEV).bfloat16()
+    dgu, dgu_t = lib().swiglu_bwd_tr(gu, dc)
+    assert torch.equal(dgu, lib().swiglu_bwd(gu, dc))
+    assert torch.equal(dgu_t, dgu.t().contiguous())
+    monkeypatch.setattr(fused, "GEMM_MODES", {"fwd": "lt", "dgrad": "lt", "wgrad": "lt"})
+    x = torch.randn(T, 256, device=DEV).bfloat16()
+    w_gu = (0.05 * torch.randn(2 * I, 256, device=DEV)).bfloat16()
+    w_dn = (0.05 * torch.randn(256, I, device=DEV)).bfloat16()
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(fused, "FUSED_DY_T", [on])
+        monkeypatch.setattr(fused, "_LAYOUT_CACHE", {})
+        a = x.clone().requires_grad_(True)
+        g1, g2 = w_gu.clone().requires_grad_(True), w_dn.clone().requires_grad_(True)
+        y = fused.linear(fused.swiglu(fused.linear(a, g1)), g2)
+        y.float().square().mean().backward()
+        assert not fused._DY_T  # consumed
+        grads.append((a.grad, g1.grad, g2.grad))
+    for u, v in zip(*grads):
+        assert _rel(u, v) < 1e-2
+    want = ((dgu.float().t() @ x.float()))
+    got = torch.empty(2 * I, 256, device=DEV, dtype=torch.float32)
+    fused._DY_T[dgu.data_ptr()] = dgu_t
+    assert fused.wgrad_into(got, dgu, x, False)
+    assert _rel(got, want) < 1e-4
+
+
 def test_kernel_index_checks():
     """Data-dependent indices out of range: the RoPE kernel clamps a position past its cos/sin table and
     the CE kernel skips a label outside the vocabulary, both flag the device error word, and
