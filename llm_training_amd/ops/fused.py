@@ -239,9 +239,9 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
 
         variants = {"nt": nt, "tt": tt, "nn": nn}
         if N * K <= _SPLITK_MAX_OUT and M % 256 == 0:
-            # split-K in two along the token (contraction) dimension as a strided batch into fp32 slabs +
-            # one reduction pass: twice the output tiles for outputs that fill the 256 CUs in 1.5 / 3.5
-            # waves of 256x256 tiles (qkv, down)
+            # split-K along the token (contraction) dimension into 2 or 4 slices, run as one strided-batch
+            # GEMM into fp32 slabs + one reduction pass: 2-4x the output tiles for outputs that fill the
+            # 256 CUs in 1.5 / 3.5 waves of 256x256 tiles (qkv, down)
             def _split(a, b, ta, tb, lda, ldb, n_split):
                 def run():
                     slabs = torch.empty(n_split, N, K, device=out.device, dtype=torch.float32)
