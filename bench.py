@@ -151,6 +151,12 @@ def main():
     if args.workload == "gpt2-cpu":
         bench_gpt2_cpu(args)
         return
+    # `python bench.py --gpus N` without torchrun: start N rank processes here (no HIP call in this
+    # parent) and exit with the job's code; under torchrun / srun WORLD_SIZE must equal --gpus
+    from llm_training_amd.launch import maybe_launch
+    rc = maybe_launch(args.gpus, [sys.executable, os.path.abspath(__file__), *sys.argv[1:]])
+    if rc is not None:
+        sys.exit(rc)
 
     from llm_training_amd.ops.native import lib
     from llm_training_amd.parallel.context import ParallelContext, init_distributed
@@ -170,8 +176,8 @@ def main():
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                 device_id=device)
     gemm_mode = setup_gemm_tuning(args.gemm_tuning)
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     lib()  # fail loudly if the HIP extension is missing
     pc = ParallelContext.create("auto", args.tp, device)
 

@@ -5,6 +5,11 @@ re-designed for CDNA4: hand-written HIP kernels for the hot ops, a flat-buffer Z
 tensor/sequence parallelism over RCCL/xGMI, one process per GPU.
 """
 import logging
+import os
+
+# RCCL on MI355X hosts needs dmabuf IPC (legacy IPC handles are rejected by the host driver); set
+# before anything initialises HIP, for torchrun / srun launches too (see llm_training_amd/launch.py)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 __version__ = "0.1.0"
 

@@ -94,6 +94,15 @@ def cmd_fit(argv):
     if not configs:
         raise SystemExit("llm-training fit: --config is required")
     cfg = load_config(configs, overrides)
+    # trainer.devices ranks on this node, one process each (Lightning's subprocess launcher); the
+    # parent only supervises and returns the job's exit code
+    from ..launch import launch_for_trainer
+    rc = launch_for_trainer(dict(cfg.get("trainer") or {}),
+                            [sys.executable, "-m", "llm_training_amd.cli.main", "fit", *argv])
+    if rc is not None:
+        if rc:
+            raise SystemExit(rc)
+        return 0
     ckpt = cfg.pop("ckpt_path", None)
     trainer, lm, dm = build_from_config(cfg)
     trainer.fit(lm, dm, ckpt_path=ckpt)
@@ -145,4 +154,5 @@ def main(argv: list[str] | None = None):
 
 
 if __name__ == "__main__":
-    main()
+    r = main()
+    sys.exit(r if isinstance(r, int) else 0)

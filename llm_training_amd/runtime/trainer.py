@@ -48,7 +48,7 @@ PRECISIONS = {"bf16-true": (torch.bfloat16, None), "bf16": (torch.bfloat16, None
               "16-mixed": None, 16: None, "16": None, "transformer-engine": None}
 # Lightning Trainer arguments that exist upstream but have no effect here: accepted (with a warning)
 # so reference configs load; anything else is a typo and raises, as jsonargparse would
-IGNORED_TRAINER_ARGS = {"devices", "accelerator", "num_sanity_val_steps", "benchmark", "fast_dev_run",
+IGNORED_TRAINER_ARGS = {"num_sanity_val_steps", "benchmark", "fast_dev_run",
                         "overfit_batches", "profiler", "detect_anomaly", "barebones", "plugins",
                         "sync_batchnorm", "reload_dataloaders_every_n_epochs", "enable_model_summary",
                         "inference_mode", "use_distributed_sampler", "min_epochs", "min_steps", "max_time",
@@ -84,6 +84,9 @@ class Trainer:
                  default_root_dir: str = "logs", num_sanity_val_steps: int = 0, seed: int | None = None,
                  deterministic: bool = False, benchmark: Any = None, gemm_tuning: str | None = None, **unused):
         self.strategy: Strategy = resolve_strategy(strategy)
+        # devices / num_nodes decide how many ranks llm_training_amd.launch starts; inside a rank the
+        # accelerator picks the device type (cpu -> gloo ranks)
+        self.devices, self.accelerator = devices, accelerator
         self.gemm_tuning = gemm_tuning  # runtime/gemm_tuning.py modes; applied in setup()
         self.deterministic = bool(deterministic)
         self.precision = precision
@@ -176,7 +179,8 @@ class Trainer:
     # ------------------------------------------------------------------ setup
     def setup(self, lm, datamodule, ckpt_path: str | None = None):
         st = self.strategy
-        rank, local, world, device = init_distributed(st.process_group_backend, st.timeout_minutes)
+        rank, local, world, device = init_distributed(st.process_group_backend, st.timeout_minutes,
+                                                      device_type="cpu" if self.accelerator == "cpu" else None)
         self.device = device
         if self.gemm_tuning is not None:
             from .gemm_tuning import setup_gemm_tuning
