@@ -145,8 +145,11 @@ class BaseDataModule:
         kw = {}
         if self.config.num_workers > 0 and self.config.prefetch_factor:
             kw["prefetch_factor"] = self.config.prefetch_factor
+        # a loader-owned generator for the worker base seed: creating the iterator (again after a resume)
+        # must not draw from the global generator that dropout / NEFTune consume
+        gen = torch.Generator().manual_seed(seed * 1_000_003 + epoch * 7919 + dp_rank)
         return DataLoader(ds, batch_sampler=sampler, collate_fn=self.collator, num_workers=self.config.num_workers,
-                          pin_memory=self.config.pin_memory, persistent_workers=False, **kw)
+                          pin_memory=self.config.pin_memory, persistent_workers=False, generator=gen, **kw)
 
     def val_dataloader(self, dp_rank=0, dp_size=1) -> DataLoader | None:
         ds = self.datasets.get("validation")
@@ -154,7 +157,8 @@ class BaseDataModule:
             return None
         sampler = ResumableDistributedSampler(len(ds), self.config.batch_size, dp_rank, dp_size, False, 0,
                                               drop_last=False)
-        return DataLoader(ds, batch_sampler=sampler, collate_fn=self.collator, num_workers=self.config.num_workers)
+        return DataLoader(ds, batch_sampler=sampler, collate_fn=self.collator, num_workers=self.config.num_workers,
+                          generator=torch.Generator().manual_seed(dp_rank))
 
     def print_dataset_info(self):
         for k, d in self.datasets.items():

@@ -38,6 +38,8 @@ class CLM(BaseLM):
             mt = m.t()
             if pc.tp:
                 n = x.shape[0]
+                if mt.shape[0] < n * pc.tp_size:  # sequence right-padded to a TP multiple: no noise on pads
+                    mt = torch.nn.functional.pad(mt, (0, 0, 0, n * pc.tp_size - mt.shape[0]))
                 mt = mt[pc.tp_rank * n:(pc.tp_rank + 1) * n]
             noise = torch.empty_like(x).uniform_(-1, 1) * mt.unsqueeze(-1) * mag.view(1, -1, 1)
             return x + noise.detach()

@@ -79,7 +79,8 @@ class DPO(_PairMixin, BaseLM):
         super().configure_model(pc, device, dtype, seed, resuming)
         spec = self.config.ref_model
         if spec is None and not resuming:
-            self.ref_model = copy.deepcopy(self.model)
+            # the parallel context (process groups) is shared, not copied
+            self.ref_model = copy.deepcopy(self.model, memo={id(self.model.pc): self.model.pc})
         elif spec is None:
             # resuming: the policy holds trained weights (and the checkpoint does not store the frozen
             # reference), so rebuild the reference from the pre-trained / initial weights instead
@@ -113,10 +114,21 @@ class DPO(_PairMixin, BaseLM):
              "Chosen Log P": pc_lp.detach().mean(), "Rejected Log P": pr_lp.detach().mean(), "Loss": loss.detach()}
         return loss, m
 
+    def on_engine_ready(self, engine):
+        """With ZeRO-3 the frozen reference model is dp-sharded like the policy (reference dpo.py:59-71):
+        gather-only units, 1/dp of its bytes per rank (parallel/frozen.py)."""
+        self.ref_shards = None
+        if engine.stage >= 3 and engine.sharded:
+            from ..parallel.frozen import FrozenShards
+            self.ref_shards = FrozenShards(self.ref_model, engine.group, engine.pc.dp_rank if engine.dp > 1 else 0,
+                                           engine.dp, engine.comm_stream)
+
     def _step(self, batch):
         pc_lp, pr_lp = self.logps(self.model, batch)
         with torch.no_grad():
             rc_lp, rr_lp = self.logps(self.ref_model, batch)
+        if getattr(self, "ref_shards", None) is not None:
+            self.ref_shards.release_all()
         return self.compute_loss(pc_lp, pr_lp, rc_lp, rr_lp)
 
     def training_step(self, batch, batch_idx=0):

@@ -183,6 +183,26 @@ class LlamaDecoderLayer(nn.Module):
         return self.mlp_block(h, g), residual
 
 
+def _pad_seq(pad: int, input_ids, position_ids, segment_ids, inputs_embeds):
+    """Right-pad a batch by ``pad`` tokens along the sequence (see Llama.hidden_states)."""
+    import torch.nn.functional as Fn
+    if input_ids is not None:
+        B, S = input_ids.shape
+        input_ids = Fn.pad(input_ids, (0, pad), value=0)
+    else:
+        B, S = inputs_embeds.shape[:2]
+        inputs_embeds = Fn.pad(inputs_embeds, (0, 0, 0, pad))
+    dev = (input_ids if input_ids is not None else inputs_embeds).device
+    if position_ids is None:
+        position_ids = torch.arange(S, device=dev).unsqueeze(0).expand(B, S)
+    position_ids = Fn.pad(position_ids.to(dev).long().expand(B, S), (0, pad), value=0)
+    if segment_ids is not None:
+        seg = segment_ids.to(dev)
+        fresh = seg.max() + 1  # the padding forms a segment of its own (device op, no host sync)
+        segment_ids = torch.cat([seg, fresh.expand(B, pad).to(seg.dtype)], 1)
+    return input_ids, position_ids, segment_ids, inputs_embeds
+
+
 class Llama(BaseModel):
     config_class = LlamaConfig
     hf_model_type = "llama"
@@ -258,7 +278,21 @@ class Llama(BaseModel):
 
     def hidden_states(self, input_ids=None, position_ids=None, segment_ids=None, inputs_embeds=None,
                       gather_sequence: bool = True, embed_hook=None):
-        """Post-norm hidden states, sequence-major [S, B, H] (full sequence unless gather_sequence=False)."""
+        """Post-norm hidden states, sequence-major [S, B, H] (full sequence unless gather_sequence=False).
+
+        Under TP + SP the sequence is sharded over the TP ranks: a length that does not divide by the TP
+        size is right-padded to the next multiple (pad tokens: id 0 / zero embeddings, position 0, their
+        own segment) and the padding is stripped again from the gathered output. Padding at the END
+        never changes a real token's output (causal attention), so any S works, as with DTensor
+        Shard(1) in the reference (llama_model.py:197-244)."""
+        S_real = None
+        if self.pc.tp:
+            L = (input_ids if input_ids is not None else inputs_embeds).shape[1]
+            pad = (-L) % self.pc.tp_size
+            if pad:
+                input_ids, position_ids, segment_ids, inputs_embeds = _pad_seq(
+                    pad, input_ids, position_ids, segment_ids, inputs_embeds)
+                S_real = L
         if input_ids is not None:
             B, S = input_ids.shape
             device = input_ids.device
@@ -289,6 +323,8 @@ class Llama(BaseModel):
         h, _ = self.norm(x, residual)
         if gather_sequence and self.pc.tp:
             h = tpl.gather_seq(h, self.pc.tp_group)
+            if S_real is not None:
+                h = h[:S_real]
         return h
 
     def forward(self, input_ids=None, attention_mask=None, position_ids=None, inputs_embeds=None,

@@ -691,12 +691,40 @@ def _apply_weight_grad(w: torch.Tensor, dw: torch.Tensor, g: torch.Tensor):
     if mg is None:
         return (dw * gs).to(w.dtype)
     mg2 = mg.view(dw.shape)
+    # mixed dtypes (fp32 dw into a bf16 buffer or back) are computed in fp32 and rounded once, with
+    # no [V, H]-sized temporary
     if getattr(w, "grad_added", False):
-        mg2.addcmul_(dw.to(mg.dtype), gs.to(mg.dtype))
+        mg2.addcmul_(dw, gs)
     else:
-        torch.mul(dw, gs, out=mg2) if mg.dtype == dw.dtype else mg2.copy_(dw * gs)
+        torch.mul(dw, gs, out=mg2)
     w.grad_added = True
     return None
+
+
+def dw_accumulator(w: torch.Tensor, n_rows: int, chunk: int) -> torch.Tensor:
+    """Weight-gradient accumulator of a row-chunked loss head: fp32 whenever several chunks add into it
+    or the weight's gradient buffer is fp32 (bf16-mixed), so the sum over chunks is not rounded to bf16
+    per chunk; a single chunk's GEMM already accumulates in fp32 and rounds once."""
+    mg = getattr(w, "main_grad", None)
+    fp32 = n_rows > chunk or (mg is not None and mg.dtype == torch.float32)
+    return torch.empty(w.shape, device=w.device, dtype=torch.float32 if fp32 else w.dtype)
+
+
+def dw_add_chunk(dw: torch.Tensor, lg: torch.Tensor, h: torch.Tensor, first: bool):
+    """dw (+)= lg^T @ h on the native GEMM path (fp32 or bf16 output), else in torch."""
+    if wgrad_into(dw, lg, h, not first):
+        return
+    if dw.dtype == lg.dtype:
+        if first:
+            torch.mm(lg.t(), h, out=dw)
+        else:
+            dw.addmm_(lg.t(), h)
+    else:
+        part = torch.mm(lg.t(), h, out_dtype=dw.dtype) if lg.is_cuda else lg.t().to(dw.dtype) @ h.to(dw.dtype)
+        if first:
+            dw.copy_(part)
+        else:
+            dw.add_(part)
 
 
 class _FusedLinearCEFn(Function):
@@ -719,7 +747,7 @@ class _FusedLinearCEFn(Function):
         loss_rows = torch.empty(N, device=h.device, dtype=torch.float32)
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dh = torch.empty_like(h) if need_h else None
-        dw = torch.empty(w.shape, device=w.device, dtype=w.dtype) if need_w else None
+        dw = dw_accumulator(w, N, chunk) if need_w else None
         wt = weight_t(w, N) if need_h and N > chunk else None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
@@ -728,11 +756,8 @@ class _FusedLinearCEFn(Function):
             loss_rows[s0:s1] = lr
             if need_h:
                 mm_nn(lg, w, out=dh[s0:s1], wt=wt)
-            if need_w and not wgrad_into(dw, lg, h[s0:s1], s0 > 0):
-                if s0 == 0:
-                    torch.mm(lg.t(), h[s0:s1], out=dw)
-                else:
-                    dw.addmm_(lg.t(), h[s0:s1])
+            if need_w:
+                dw_add_chunk(dw, lg, h[s0:s1], s0 == 0)
             del lg
         ctx.save_for_backward(*(t for t in (dh, dw) if t is not None))
         ctx.has = (need_h, need_w)
@@ -817,18 +842,20 @@ class _LinearLogpsFn(Function):
         N = h.shape[0]
         dh = torch.empty_like(h)
         coef = (-g).float().contiguous()
-        dw_acc = None
+        need_w = ctx.needs_input_grad[1]
+        dw = dw_accumulator(w, N, chunk) if need_w else None
         wt = weight_t(w, N) if N > chunk else None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, coef[s0:s1], None, True)
             mm_nn(lg, w, out=dh[s0:s1], wt=wt)
-            if ctx.needs_input_grad[1]:
-                r = _wgrad_mm(w, lg.t(), h[s0:s1])
-                if r is not None:
-                    dw_acc = r if dw_acc is None else dw_acc + r
-        return dh, dw_acc, None, None, None
+            if need_w:
+                dw_add_chunk(dw, lg, h[s0:s1], s0 == 0)
+        dwr = None
+        if need_w:
+            dwr = _apply_weight_grad(w, dw, torch.ones((), device=dw.device, dtype=torch.float32))
+        return dh, dwr, None, None, None
 
 
 def linear_token_logps(h, w, labels, ignore_index: int = -100, chunk_size: int = 8192):

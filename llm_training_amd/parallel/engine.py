@@ -132,6 +132,8 @@ class _Unit:
     param_ring: bool = False        # stage 3: gathered params live in a slot of the parameter ring
     shapes: list = field(default_factory=list)  # parameter shapes (ring units re-bind their views)
     pslot: object = None            # the parameter ring slot currently held
+    opt: object = None              # generic torch optimizer over this unit's master shard
+    opt_pieces: list = field(default_factory=list)  # (param index, start, end in the shard, master view)
 
     @property
     def shard_numel(self):
@@ -146,8 +148,13 @@ class DataParallelEngine:
                  offload_optimizer: bool = False, force_sharded: bool | None = None,
                  shard_gradients: bool | None = None, offload_params: bool = False, offload_device: str = "cpu",
                  nvme_path: str | None = None, quantized_weights: bool = False, quantized_gradients: bool = False,
-                 hpz_partition_size: int = 1):
+                 hpz_partition_size: int = 1, optimizer_factory=None):
         self.model = model
+        # any torch.optim class instead of the fused AdamW: one optimizer per unit over the unit's flat fp32
+        # master shard (DeepSpeed ZeRO semantics: the wrapped optimizer sees flat partitions)
+        self.optimizer_factory = optimizer_factory
+        if optimizer_factory is not None and (offload_optimizer or offload_device == "nvme"):
+            raise ValueError("optimizer offload runs the host AdamW; a generic torch optimizer needs it off")
         self.offload = bool(offload_optimizer) or offload_device == "nvme"
         self.offload_device = offload_device
         self.nvme_path = nvme_path
@@ -330,7 +337,12 @@ class DataParallelEngine:
             # upload the master itself
             if self.param_dtype == torch.bfloat16:
                 u.p_host = torch.empty(u.master.numel(), dtype=torch.bfloat16, pin_memory=pin)
-        if self.offload and self.offload_device == "nvme":
+        if self.optimizer_factory is not None:
+            # generic optimizer: one param per parameter piece of this rank's shard (the whole parameter,
+            # in its shape, when the shard holds all of it), no Adam moments here
+            u.opt_pieces = self._opt_pieces(u)
+            u.opt = self.optimizer_factory([pv for _, _, _, pv in u.opt_pieces])
+        elif self.offload and self.offload_device == "nvme":
             u.exp_avg = self._nvme_tensor(i, "exp_avg", torch.zeros(u.master.numel()))
             u.exp_avg_sq = self._nvme_tensor(i, "exp_avg_sq", torch.zeros(u.master.numel()))
         else:
@@ -802,7 +814,20 @@ class DataParallelEngine:
         for u in self.units:
             g = self._grad_shard(u)
             pout = self._param_out(u)
-            if self.native:
+            if u.opt is not None:
+                # generic optimizer: the scaled fp32 gradient pieces as .grad of the master pieces, one
+                # step, then the training-dtype copy (the unit's fp32 gradient exists for this call only)
+                g32 = g.to(torch.float32).mul_(self._gscale)
+                for _, a, b, pv in u.opt_pieces:
+                    pv.grad = g32[a:b].view(pv.shape)
+                for grp in u.opt.param_groups:
+                    grp["lr"] = lr
+                u.opt.step()
+                for _, _, _, pv in u.opt_pieces:
+                    pv.grad = None
+                del g32
+                pout.copy_(u.master)
+            elif self.native:
                 lib().adamw_(u.master, u.exp_avg, u.exp_avg_sq, g, pout, lr, b1, b2, self.eps,
                              self.weight_decay, self.step_count, self._gscale)
             else:
@@ -910,11 +935,128 @@ class DataParallelEngine:
             u.opt_event = None
 
     # ------------------------------------------------------------------ state (checkpointing)
+    # ------------------------------------------------------------------ generic optimizers
+    # Tensor-wise optimizers (their update uses norms / factored statistics of the WHOLE parameter) are
+    # exact only where every rank's shard holds whole parameters (ZeRO stage 0, or dp 1); element-wise
+    # ones (SGD, the Adam family, RMSprop, Adagrad, ...) are exact at every stage.
+    TENSORWISE = ("Adafactor", "Muon", "LBFGS", "Lamb", "LAMB", "Lars", "LARS", "Shampoo")
+
+    def _opt_pieces(self, u: _Unit) -> list:
+        a, b = self.shard_range(u)
+        pieces = []
+        whole = True
+        for i, (o, shp) in enumerate(zip(u.offsets, u.shapes)):
+            s, e = max(o, a), min(o + shp.numel(), b)
+            if e <= s:
+                continue
+            view = u.master[s - a:e - a]
+            if s == o and e == o + shp.numel():
+                view = view.view(shp)
+            else:
+                whole = False
+            pieces.append((i, s - a, e - a, view))
+        if not whole:
+            probe = self.optimizer_factory([torch.zeros(1)])
+            if type(probe).__name__ in self.TENSORWISE:
+                raise ValueError(f"{type(probe).__name__} normalises by whole-parameter statistics: with ZeRO "
+                                 f"stage {self.stage} at dp {self.dp} a rank holds parameter pieces; use ZeRO "
+                                 "stage 0 (ddp) or an element-wise optimizer")
+        return pieces
+
+    def _elementwise(self, u: _Unit) -> list[tuple[int, str, torch.Tensor]]:
+        """(piece index, state key, tensor) of the element-wise state (same shape as its piece)."""
+        out = []
+        if u.opt is None:
+            return out
+        for j, (_, _, _, pv) in enumerate(u.opt_pieces):
+            for k, v in u.opt.state.get(pv, {}).items():
+                if torch.is_tensor(v) and v.shape == pv.shape:
+                    out.append((j, k, v))
+        return out
+
+    def state_kinds(self) -> list[str]:
+        """Element-wise optimizer state kinds of every unit, checkpointed as flat slices like the master:
+        the fused AdamW's moments, or the element-wise state tensors of a generic optimizer."""
+        if self.optimizer_factory is None:
+            return ["master", "exp_avg", "exp_avg_sq"]
+        kinds = ["master"]
+        for u in self.units:
+            for _, k, _ in self._elementwise(u):
+                if "opt:" + k not in kinds:
+                    kinds.append("opt:" + k)
+        return kinds
+
+    def state_params(self, u: _Unit, kind: str) -> set[int] | None:
+        """Indices of the unit's parameters that carry state ``kind`` (None: all of them)."""
+        if not kind.startswith("opt:"):
+            return None
+        return {u.opt_pieces[j][0] for j, k, _ in self._elementwise(u) if k == kind[4:]}
+
+    def unit_state(self, u: _Unit, kind: str) -> torch.Tensor | None:
+        """The flat (shard-sized) state tensor ``kind`` of unit ``u`` (a copy for generic optimizers;
+        None if it does not exist yet)."""
+        if not kind.startswith("opt:"):
+            return getattr(u, kind)
+        flat = None
+        for j, k, v in self._elementwise(u):
+            if k != kind[4:]:
+                continue
+            if flat is None:
+                flat = torch.zeros_like(u.master)
+            _, a, b, _ = u.opt_pieces[j]
+            flat[a:b].copy_(v.reshape(-1))
+        return flat
+
+    def optimizer_extra_state(self) -> dict[str, torch.Tensor]:
+        """Non-element-wise generic-optimizer state of this rank (step counters, factored statistics),
+        keyed ``u<unit>.p<param index>.<key>``: restored only into the same layout."""
+        out = {}
+        for u in self.units:
+            if u.opt is None:
+                continue
+            for i, _, _, pv in u.opt_pieces:
+                for k, v in u.opt.state.get(pv, {}).items():
+                    if torch.is_tensor(v) and v.shape == pv.shape:
+                        continue
+                    out[f"u{u.idx}.p{i}.{k}"] = (v if torch.is_tensor(v) else torch.tensor(v)).detach().to(
+                        "cpu", copy=True)
+        return out
+
+    @torch.no_grad()
+    def load_unit_states(self, tensors: list[dict[str, torch.Tensor]], extra: dict[str, torch.Tensor] | None = None,
+                         present: list[dict[str, set]] | None = None):
+        """Install a generic optimizer's state before its first step (torch optimizers create state lazily):
+        ``tensors[unit]["opt:<key>"]`` = flat shard-sized element-wise state, ``present[unit][kind]`` = the
+        parameter indices that had it, ``extra`` = per-piece rest."""
+        extra = extra or {}
+        for ui, u in enumerate(self.units):
+            if u.opt is None:
+                continue
+            state = {}
+            for j, (i, a, b, pv) in enumerate(u.opt_pieces):
+                st = {k[4:]: v[a:b].view(pv.shape).clone() for k, v in tensors[ui].items()
+                      if k.startswith("opt:") and (present is None or i in present[ui].get(k, ()))}
+                pre = f"u{u.idx}.p{i}."
+                for k, v in extra.items():
+                    if k.startswith(pre):
+                        st[k[len(pre):]] = v.clone()
+                if st:
+                    if any(k.startswith("opt:") for k in tensors[ui]) and not any(
+                            k.startswith(pre) for k in extra) and "step" not in st:
+                        st["step"] = torch.tensor(float(self.step_count))
+                    state[j] = st
+            if state:
+                sd = u.opt.state_dict()
+                sd["state"] = state
+                u.opt.load_state_dict(sd)
+
     def optimizer_state(self) -> dict:
         self.wait_params()
+        kinds = self.state_kinds()
         return {
             "step": self.step_count,
-            "units": [{"master": u.master, "exp_avg": u.exp_avg, "exp_avg_sq": u.exp_avg_sq} for u in self.units],
+            "units": [{k: self.unit_state(u, k) for k in kinds} for u in self.units],
+            "extra": self.optimizer_extra_state(),
             "stage": self.stage, "dp": self.dp, "dp_rank": self.pc.dp_rank,
             "numels": [u.numel for u in self.units],
         }
@@ -925,8 +1067,12 @@ class DataParallelEngine:
         self.step_count = int(st["step"])
         for u, s in zip(self.units, st["units"]):
             u.master.copy_(s["master"])
-            u.exp_avg.copy_(s["exp_avg"])
-            u.exp_avg_sq.copy_(s["exp_avg_sq"])
+            if u.opt is None:
+                u.exp_avg.copy_(s["exp_avg"])
+                u.exp_avg_sq.copy_(s["exp_avg_sq"])
+        if self.optimizer_factory is not None:
+            self.load_unit_states([{k: v.clone() for k, v in s.items() if k.startswith("opt:") and v is not None}
+                                   for s in st["units"]], st.get("extra"))
         self.sync_params_from_master()
 
     @torch.no_grad()

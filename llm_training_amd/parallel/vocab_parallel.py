@@ -20,7 +20,7 @@ import torch
 import torch.distributed as dist
 from torch.autograd import Function
 
-from ..ops.fused import _apply_weight_grad, _wgrad_mm, mm_nn, mm_nt, weight_t, wgrad_into
+from ..ops.fused import _apply_weight_grad, dw_accumulator, dw_add_chunk, mm_nn, mm_nt, weight_t
 from ..ops.native import lib, use_native
 
 
@@ -89,7 +89,7 @@ class _VPFusedCE(Function):
         loss = ((lse - tgt) * valid).sum() * inv_n[0]
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dh = torch.empty_like(h) if need_h else None
-        dw_full = torch.empty(w_full.shape, device=w.device, dtype=w.dtype) if need_w else None
+        dw_full = dw_accumulator(w_full, N, chunk) if need_w else None
         dw = dw_full[:n_valid] if need_w else None
         if need_w and n_valid < w_full.shape[0]:
             dw_full[n_valid:].zero_()
@@ -100,11 +100,8 @@ class _VPFusedCE(Function):
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), None, inv_n, native)
             if need_h:
                 mm_nn(lg, w, out=dh[s0:s1], wt=wt)
-            if need_w and not wgrad_into(dw, lg, h[s0:s1], s0 > 0):
-                if s0 == 0:
-                    torch.mm(lg.t(), h[s0:s1], out=dw)
-                else:
-                    dw.addmm_(lg.t(), h[s0:s1])
+            if need_w:
+                dw_add_chunk(dw, lg, h[s0:s1], s0 == 0)
             del lg
         ctx.save_for_backward(*(t for t in (dh, dw_full) if t is not None))
         ctx.has = (need_h, need_w)
@@ -155,14 +152,16 @@ class _VPLogps(Function):
         N = h.shape[0]
         dh = torch.empty_like(h)
         coef = (-g).float().contiguous()
-        dw = torch.zeros(w_full.shape, device=w.device, dtype=torch.float32)
+        dw = dw_accumulator(w_full, N, chunk)
+        if n_valid < w_full.shape[0]:
+            dw[n_valid:].zero_()
+        wt = weight_t(w, N) if native and N > chunk else None
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), coef[s0:s1], None, native)
-            mm_nn(lg, w, out=dh[s0:s1])
-            dw[:n_valid].addmm_(lg.t().float(), h[s0:s1].float()) if not lg.is_cuda else \
-                dw[:n_valid].add_(torch.mm(lg.t(), h[s0:s1], out_dtype=torch.float32))
+            mm_nn(lg, w, out=dh[s0:s1], wt=wt)
+            dw_add_chunk(dw[:n_valid], lg, h[s0:s1], s0 == 0)
         one = torch.ones((), device=dw.device, dtype=torch.float32)
         return dh, _apply_weight_grad(w_full, dw, one), None, None, None, None, None, None
 

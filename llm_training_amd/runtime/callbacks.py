@@ -50,7 +50,9 @@ class LearningRateMonitor(Callback):
         eng = getattr(trainer, "engine", None)
         out = {f"lr-{name}": float(trainer.last_lr)}  # the rate the optimizer step just used
         if self.log_momentum and eng is not None:
-            out[f"lr-{name}-momentum"] = float(eng.betas[0])
+            grp = eng.units[0].opt.param_groups[0] if eng.units and eng.units[0].opt is not None else {}
+            mom = grp.get("momentum", grp["betas"][0] if "betas" in grp else eng.betas[0])
+            out[f"lr-{name}-momentum"] = float(mom)
         if self.log_weight_decay and eng is not None:
             out[f"lr-{name}-weight_decay"] = float(eng.weight_decay)
         return out
@@ -66,9 +68,20 @@ class LearningRateMonitor(Callback):
 
 
 class ModelCheckpoint(Callback):
+    """Lightning ModelCheckpoint surface (reference model_checkpoint.py:13-18): every_n_train_steps /
+    epoch-end cadence, ``save_top_k`` (the newest k, or the best k by ``monitor`` / ``mode``),
+    ``save_last`` (``last.ckpt`` symlink), ``async_save`` (shard files written on a background thread).
+
+    Old checkpoints are deleted and ``last.ckpt`` is moved only once the NEW checkpoint is complete on
+    every rank: with async writes that happens at the start of the next save (or at fit end), after
+    the pending writes are joined, a barrier, and ``is_complete`` — a crash mid-write always leaves the
+    previous complete checkpoint in place."""
+
     def __init__(self, dirpath: str | None = None, filename: str | None = None, every_n_train_steps: int | None = None,
                  save_on_train_epoch_end: bool | None = None, save_top_k: int = 1, save_last: bool | None = None,
                  monitor: str | None = None, mode: str = "min", async_save: bool = False, **kw):
+        if mode not in ("min", "max"):
+            raise ValueError(f"ModelCheckpoint mode must be 'min' or 'max', got {mode!r}")
         self.dirpath = dirpath
         self.async_save = async_save  # write the shard files on a background thread
         self.filename = filename or "epoch={epoch}-step={step}"
@@ -78,26 +91,61 @@ class ModelCheckpoint(Callback):
         self.save_last = save_last
         self.monitor = monitor
         self.mode = mode
-        self.saved: list[str] = []
+        self.saved: list[str] = []              # complete checkpoints kept, oldest first
+        self.scores: dict[str, float] = {}      # monitored value of each kept checkpoint
+        self._pending: str | None = None        # saved, not yet known complete on every rank
 
     def _dir(self, trainer) -> str:
         # reference: <log_dir>/checkpoints when logging to a run directory (model_checkpoint.py:13-18)
         return self.dirpath or os.path.join(trainer.log_dir, "checkpoints")
+
+    def _score(self, trainer) -> float | None:
+        if self.monitor is None:
+            return None
+        trainer._flush_logs(force=True)  # the step's metrics, DP-averaged (one host sync per save)
+        v = trainer.last_metrics.get(self.monitor)
+        if v is None or v != v:
+            logger.warning("ModelCheckpoint: monitored metric %r not available at step %d; the checkpoint is "
+                           "kept but not ranked", self.monitor, trainer.global_step)
+            return None
+        return float(v)
 
     def _save(self, trainer):
         if self.save_top_k == 0:
             return
         name = self.filename.format(epoch=trainer.state.epoch, step=trainer.global_step) + ".ckpt"
         path = os.path.join(self._dir(trainer), name)
-        if path in self.saved:
+        if path in self.saved or path == self._pending:
             return
+        self.finalize(trainer)  # the previous save is complete everywhere before anything is removed
+        score = self._score(trainer)
         trainer.save_checkpoint(path, async_write=self.async_save)
+        if score is not None:
+            self.scores[path] = score
+        self._pending = path
+        if not self.async_save:
+            self.finalize(trainer)
+
+    def finalize(self, trainer):
+        """Promote the pending checkpoint once it is complete on every rank: rotate old ones, move
+        ``last.ckpt``."""
+        path = self._pending
+        if path is None:
+            return
+        from ..ckpt.checkpoint import is_complete, wait_for_pending_saves
+        wait_for_pending_saves()
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()
+        self._pending = None
+        if not is_complete(path):
+            logger.error("checkpoint %s is incomplete; keeping the previous checkpoints", path)
+            return
         self.saved.append(path)
-        if self.save_top_k > 0 and self.monitor is None:
-            while len(self.saved) > self.save_top_k:
-                old = self.saved.pop(0)
-                if trainer.is_global_zero and os.path.exists(old):
-                    shutil.rmtree(old, ignore_errors=True)
+        for old in self._to_remove():
+            self.saved.remove(old)
+            self.scores.pop(old, None)
+            if trainer.is_global_zero:
+                _remove_checkpoint(old)
         if self.save_last and trainer.is_global_zero:
             link = os.path.join(self._dir(trainer), "last.ckpt")
             try:
@@ -107,6 +155,19 @@ class ModelCheckpoint(Callback):
             except OSError:
                 pass
 
+    def _to_remove(self) -> list[str]:
+        k = self.save_top_k
+        if k < 0 or len(self.saved) <= k:
+            return []
+        if self.monitor is None:
+            return self.saved[:len(self.saved) - k]
+        # best k by the monitored value; unranked checkpoints go first, ties keep the newer one
+        sign = 1.0 if self.mode == "min" else -1.0
+        order = sorted(range(len(self.saved)), key=lambda i: (
+            self.saved[i] not in self.scores, sign * self.scores.get(self.saved[i], 0.0), -i))
+        keep = {self.saved[i] for i in order[:k]}
+        return [p for p in self.saved if p not in keep]
+
     def on_train_batch_end(self, trainer, lm, outputs, batch, batch_idx):
         n = self.every_n_train_steps
         if n and trainer.global_step > 0 and trainer.global_step % n == 0:
@@ -115,6 +176,16 @@ class ModelCheckpoint(Callback):
     def on_train_epoch_end(self, trainer, lm):
         if self.save_on_train_epoch_end or (self.save_on_train_epoch_end is None and not self.every_n_train_steps):
             self._save(trainer)
+
+    def on_fit_end(self, trainer, lm):
+        self.finalize(trainer)
+
+
+def _remove_checkpoint(path: str):
+    if os.path.isdir(path) and not os.path.islink(path):
+        shutil.rmtree(path, ignore_errors=True)
+    elif os.path.exists(path):
+        os.remove(path)
 
 
 class SaveConfigCallback(Callback):
@@ -188,18 +259,28 @@ class OutputRedirection(Callback):
         rank = trainer.pc.rank if trainer.pc else 0
         fname = os.path.join(d, name[0] + (f".rank{rank}" if rank else "") + ".log")
         os.makedirs(d, exist_ok=True)
+        self._orig = (sys.stdout, sys.stderr)
         self._f = open(fname, "a", buffering=1)
         if self.redirect_stdout:
             sys.stdout = _Tee(self._orig[0], self._f)
         if self.redirect_stderr:
             sys.stderr = _Tee(self._orig[1], self._f)
+        self._handlers = []
         for h in logging.getLogger("llm_training").handlers:
             if isinstance(h, logging.StreamHandler) and not isinstance(h, logging.FileHandler):
+                self._handlers.append((h, h.stream))
                 h.setStream(sys.stderr)
 
     def on_fit_end(self, trainer, lm):
+        self.teardown(trainer, lm)
+
+    def teardown(self, trainer=None, lm=None):
+        """Undo the redirection (also after a failed fit): streams, logging handlers, the log file."""
         if self._f:
             sys.stdout, sys.stderr = self._orig
+            for h, old in getattr(self, "_handlers", []):
+                h.setStream(old)
+            self._handlers = []
             self._f.close()
             self._f = None
 

@@ -211,8 +211,11 @@ def is_complete_checkpoint(path: str | os.PathLike) -> bool:
 def checkpoint_step(path: str | os.PathLike) -> int:
     p = Path(path)
     try:
+        if p.is_file():
+            from ..ckpt.checkpoint import read_meta
+            return int(read_meta(str(p))["trainer"]["global_step"])
         return int(json.loads((p / "meta.json").read_text())["trainer"]["global_step"])
-    except (KeyError, ValueError, OSError):
+    except Exception:  # noqa: BLE001 - fall back to the step in the name
         m = _STEP_RE.search(p.name)
         return int(m.group(1)) if m else -1
 
@@ -223,6 +226,8 @@ def find_last_checkpoint(root: str | os.PathLike) -> str | None:
     if not root.exists():
         return None
     cands = [m.parent for m in root.rglob("meta.json") if is_complete_checkpoint(m.parent)]
+    # consolidated single-file checkpoints (save_distributed_checkpoint: false)
+    cands += [f for f in root.rglob("*.ckpt") if f.is_file() and not f.is_symlink() and is_complete_checkpoint(f)]
     if not cands:
         return None
     best = max(cands, key=lambda p: (checkpoint_step(p), p.stat().st_mtime))

@@ -192,7 +192,10 @@ class Trainer:
             # kernel already reduces in a fixed order (no float atomics in the backward)
             torch.use_deterministic_algorithms(True, warn_only=True)
             os.environ["LLMT_DETERMINISTIC"] = "1"
-        torch.manual_seed(seed + self.pc.dp_rank)
+        # one generator stream per (dp, tp) rank: under TP + SP every random op (dropout masks, NEFTune
+        # noise, attention-dropout seeds) acts on a sequence / head shard of its own, so the TP ranks of a
+        # DP group must not share masks (tp 1 keeps seed + dp_rank)
+        torch.manual_seed(seed + self.pc.dp_rank + 1_000_003 * self.pc.tp_rank)
         if ckpt_path == "last":
             ckpt_path = self.resolve_last_checkpoint()
         self.lm, self.datamodule = lm, datamodule
@@ -210,12 +213,18 @@ class Trainer:
         self.optimizer_name = str(ospec["name"]).rsplit(".", 1)[-1]
         self.base_lr = hp["lr"]
         rd = getattr(st, "grad_reduce_dtype", None)
+        factory = None
+        if hp["kind"] == "generic":
+            cls, okw = hp["cls"], hp["kwargs"]
+            factory = lambda params: cls(params, **okw)  # noqa: E731
+            logger.info("optimizer %s runs generically over the flat fp32 master shards", hp["name"])
         self.engine = DataParallelEngine(lm.model, self.pc, st.zero_stage, lr=hp["lr"], betas=hp["betas"],
-                                         eps=hp["eps"], weight_decay=hp["weight_decay"],
+                                         eps=hp["eps"], weight_decay=hp["weight_decay"], optimizer_factory=factory,
                                          grad_dtype=self.grad_dtype,
                                          reduce_dtype=getattr(torch, rd) if rd else self.grad_dtype,
                                          reshard_after_forward=st.reshard_after_forward,
                                          overlap_comm=st.overlap_comm, **st.engine_kwargs())
+        _call(lm, "on_engine_ready", self.engine)  # e.g. DPO shards its frozen reference model (ZeRO-3)
         self.scheduler = lm.build_lr_scheduler(self.base_lr, self.estimated_stepping_batches())
         if ckpt_path:
             from ..ckpt.checkpoint import load_checkpoint
@@ -283,6 +292,8 @@ class Trainer:
         finally:
             if self.watchdog is not None:
                 self.watchdog.close()
+            for cb in self.callbacks:
+                _call(cb, "teardown", self, lm)
 
     def _fit(self, lm, datamodule=None, ckpt_path: str | None = None):
         self.setup(lm, datamodule, ckpt_path)
@@ -470,6 +481,7 @@ class Trainer:
         out = dict(zip(keys, vec.cpu().tolist()))
         if "Loss/Val" in out and "Perplexity/Val" in out:
             out["Perplexity/Val"] = math.exp(out["Loss/Val"])
+        self.last_metrics.update(out)  # visible to ModelCheckpoint(monitor="Loss/Val")
         if self.is_global_zero:
             for lg in self.loggers:
                 _call(lg, "log_metrics", out, self.state.global_step)

@@ -105,9 +105,23 @@ def read_deepspeed_checkpoint(p: Path) -> dict[str, torch.Tensor]:
                 part = -(-n // world)  # each rank holds ceil(n / world) elements of every parameter
                 sd[name] = torch.cat([f[off:off + part] for f in flats])[:n].view(shape).clone()
                 off += part
-    # frozen parameters: whole tensors in the module state dict (stage 1/2) or fragments (stage 3)
-    for name, frag in (ms.get("frozen_param_fragments") or {}).items():
-        sd.setdefault(name, frag)
+    # frozen parameters: whole tensors in the module state dict (stage 1/2); at stage 3 every rank's
+    # zero_pp_rank_<r>_mp_rank_00_model_states.pt holds its fragment (ceil(n / world) elements, padded),
+    # merged in rank order as DeepSpeed's zero_to_fp32 does (_zero3_merge_frozen_params)
+    frozen_shapes = ms.get("frozen_param_shapes") or {}
+    if stage >= 3 and frozen_shapes:
+        rank_files = sorted(d.glob("zero_pp_rank_*_mp_rank_00_model_states.pt"),
+                            key=lambda f: int(f.name.split("zero_pp_rank_")[1].split("_")[0]))
+        frags = [(_torch_load(f).get("frozen_param_fragments") or {}) for f in rank_files] or \
+            [ms.get("frozen_param_fragments") or {}]
+        for name, shape in frozen_shapes.items():
+            n = int(torch.Size(shape).numel())
+            pieces = [fr[name].reshape(-1) for fr in frags if name in fr]
+            if pieces:
+                sd[name] = torch.cat(pieces)[:n].view(shape).clone()
+    else:
+        for name, frag in (ms.get("frozen_param_fragments") or {}).items():
+            sd.setdefault(name, frag)
     for name, t in module.items():
         if name not in sd and isinstance(t, torch.Tensor) and t.numel() > 0:
             sd[name] = t
@@ -164,7 +178,8 @@ def convert(checkpoint_path, output_dir=None, config_path=None, eos_token_id=Non
     out = Path(output_dir) if output_dir else cp.parent / "hf" / cp.stem
     cfg = None
     foreign = False
-    if (cp / "meta.json").exists():
+    from ..ckpt.checkpoint import is_complete as _ours
+    if (cp / "meta.json").exists() or (cp.is_file() and _ours(cp)):  # ours: shard dir or consolidated file
         meta, parts = load_model_state_for_export(str(cp))
         model_cls = import_object(meta["model_class"])
         mcfg = model_cls.config_class.model_validate({**meta["model_config"], "hf_path": None})

@@ -287,8 +287,11 @@ def test_checkpoint_reshards_across_layouts(tmp_path):
         assert torch.allclose(loaded[0]["sd"][k], v), k
     assert loaded[1]["step"] == 2
     # one shard file per rank, no full gather anywhere
-    assert {f for f in saved[0]["files"] if f.endswith(".safetensors")} == {
+    assert {f for f in saved[0]["files"] if f.startswith("shard") and f.endswith(".safetensors")} == {
         f"shard-tp{t}-dp{d}.safetensors" for t in range(2) for d in range(2)}
+    # plus every rank's generator states
+    assert {f for f in saved[0]["files"] if f.startswith("rng")} == {
+        f"rng-tp{t}-dp{d}.safetensors" for t in range(2) for d in range(2)}
 
 
 def test_checkpoint_dp4_zero3_to_dp2_zero2_and_offload(tmp_path):
@@ -369,4 +372,125 @@ def test_eight_rank_data_parallel_rehearsal(stage):
             assert torch.allclose(out[r]["params"][k], v, atol=2e-4, rtol=1e-4), (stage, r, k)
     avg = [sum(out[r]["losses"][i] for r in range(8)) / 8 for i in range(2)]
     for a, b in zip(avg, ref_losses):
+        assert abs(a - b) < 1e-5
+
+
+def _make_opt(name, params):
+    if name == "sgd":
+        return torch.optim.SGD(params, lr=1e-2, momentum=0.9, nesterov=True, weight_decay=0.01)
+    if name == "adafactor":
+        return torch.optim.Adafactor(params, lr=1e-2)
+    return torch.optim.AdamW(params, lr=1e-2, amsgrad=True, weight_decay=0.0)
+
+
+def _opt_factory(name):
+    import functools
+    return functools.partial(_make_opt, name)  # picklable for the gloo workers
+
+
+@pytest.mark.parametrize("opt,stage", [("sgd", 2), ("amsgrad", 2), ("adafactor", 0), ("sgd", 3)])
+def test_generic_optimizers_match_single_process(opt, stage):
+    """Any torch optimizer over the engine's fp32 master pieces (reference MasterWeightsOptimizer,
+    optim/master_weight_wrapper.py:17-80): dp2 == one process. Element-wise optimizers at any ZeRO stage;
+    a tensor-wise one (Adafactor: whole-parameter RMS, factored second moments) where ranks hold whole
+    parameters (stage 0), with per-parameter shapes exactly as the reference applies it."""
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    cfg_kw = {}
+    gb = _batches(128, STEPS, B=4)
+    m = Llama(tiny_llama_cfg(**cfg_kw), ParallelContext.single(), dtype=torch.float32)
+    m.init_weights(1)
+    full0 = {k: v.clone() for k, v in m.state_dict().items()}
+    eng, ref_losses = _train(m, ParallelContext.single(), 0, gb, optimizer_factory=_opt_factory(opt))
+    ref = _full_params(m, eng)
+    if opt == "adafactor":  # factored statistics of the 2-D weights: per-parameter shapes reached the optimizer
+        assert any("row_var" in st for st in eng.units[1].opt.state.values())
+    out = run_gloo(_dp_worker, 2, (stage, cfg_kw, full0, gb, False, 1, False,
+                                   {"optimizer_factory": _opt_factory(opt)}))
+    for r in (0, 1):
+        for k, v in ref.items():
+            assert torch.allclose(out[r]["params"][k], v, atol=2e-5, rtol=1e-4), (opt, r, k)
+    assert any(not torch.allclose(ref[k], full0[k]) for k in ref)  # it trained
+
+
+def _adafactor_sharded_worker(rank, world):
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+    pc = ParallelContext.create("auto", 1, "cpu")
+    m = Llama(tiny_llama_cfg(), pc, dtype=torch.float32)
+    try:
+        DataParallelEngine(m, pc, 2, optimizer_factory=_opt_factory("adafactor"))
+    except ValueError as e:
+        return str(e)
+    return ""
+
+
+def test_tensorwise_optimizer_refuses_zero_shards():
+    out = run_gloo(_adafactor_sharded_worker, 2, ())
+    assert all("whole-parameter" in out[r] for r in (0, 1))
+
+
+def _pref_batches(n, B=2, S=12, V=128, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        b = {}
+        for side in ("chosen", "rejected"):
+            ids = torch.randint(1, V, (B, S), generator=g)
+            lab = ids.clone()
+            lab[:, :4] = -100
+            b.update({f"{side}_input_ids": ids, f"{side}_labels": lab,
+                      f"{side}_attention_mask": torch.ones(B, S, dtype=torch.long)})
+        out.append(b)
+    return out
+
+
+def _dpo_worker(rank, world, stage, batches, seed):
+    from llm_training_amd.lms.preference import DPO
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+    pc = ParallelContext.create("auto", 1, "cpu") if world > 1 else ParallelContext.single()
+    lm = DPO({"model": {"model_class": "llm_training.models.Llama",
+                        "model_config": dict(vocab_size=128, hidden_size=64, intermediate_size=128,
+                                             num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2)},
+              "beta": 0.1})
+    lm.configure_model(pc, torch.device("cpu"), torch.float32, seed=seed)
+    full_ref = sum(p.numel() * p.element_size() for p in lm.ref_model.parameters())
+    eng = DataParallelEngine(lm.model, pc, stage, lr=1e-2, weight_decay=0.0)
+    lm.on_engine_ready(eng)
+    lm.train()
+    B = batches[0]["chosen_input_ids"].shape[0] // pc.dp_size
+    losses = []
+    for b in batches:
+        local = {k: v[pc.dp_rank * B:(pc.dp_rank + 1) * B] for k, v in b.items()}
+        eng.begin_step(1)
+        eng.zero_grad()
+        eng.begin_micro(0)
+        loss, m, _ = lm.training_step(local)
+        loss.backward()
+        eng.finish_backward()
+        eng.clip_and_scale(1.0)
+        eng.step(1e-2)
+        losses.append(float(loss))
+    with eng.full_params_context():
+        params = {k: v.detach().clone() for k, v in lm.model.state_dict().items()}
+    shards = lm.ref_shards.resident_bytes() if lm.ref_shards is not None else full_ref
+    held = sum(p.numel() * p.element_size() for p in lm.ref_model.parameters())  # bound between forwards
+    return {"losses": losses, "params": params, "ref_bytes": shards, "full_ref": full_ref, "held": held}
+
+
+def test_dpo_reference_model_zero3_sharded_matches_single_process():
+    """DPO at dp2 x ZeRO-3: the frozen reference model is gather-only dp-sharded (1/dp bytes per rank,
+    nothing gathered between steps) and training equals the single-process run."""
+    batches = _pref_batches(3, B=4)
+    ref = run_gloo(_dpo_worker, 1, (0, batches, 7))[0]
+    out = run_gloo(_dpo_worker, 2, (3, batches, 7))
+    for r in (0, 1):
+        assert out[r]["ref_bytes"] <= out[r]["full_ref"] / 2 * 1.05
+        assert out[r]["held"] == 0
+        for k, v in ref["params"].items():
+            assert torch.allclose(out[r]["params"][k], v, atol=2e-5, rtol=1e-4), k
+    avg = [(a + b) / 2 for a, b in zip(out[0]["losses"], out[1]["losses"])]
+    for a, b in zip(avg, ref["losses"]):
         assert abs(a - b) < 1e-5

@@ -189,6 +189,41 @@ def test_fused_linear_cross_entropy():
     assert _rel(w.grad, wr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("head", ["flce", "logps"])
+def test_loss_head_weight_grad_accumulates_in_fp32(head):
+    """lm_head dW summed over 4 row chunks: with an fp32 gradient buffer (bf16-mixed) it equals the
+    single-chunk GEMM (fp32 accumulate, one rounding) to fp32 precision; with bf16 gradients it is
+    rounded once, not once per chunk."""
+    torch.manual_seed(0)
+    N, H, V = 2048, 256, 8192
+
+    def run(chunk, fp32_buf):
+        h = torch.randn(N, H, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).bfloat16()
+        w = (0.05 * torch.randn(V, H, device=DEV, generator=torch.Generator(DEV).manual_seed(2))).bfloat16()
+        lab = torch.randint(0, V, (N,), device=DEV, generator=torch.Generator(DEV).manual_seed(3))
+        w.requires_grad_(True)
+        if fp32_buf:
+            w.main_grad = torch.zeros(V, H, device=DEV, dtype=torch.float32)
+            w.grad_added = False
+        if head == "flce":
+            F_.fused_linear_cross_entropy(h, w, lab, chunk_size=chunk).backward()
+        else:
+            lp = F_.linear_token_logps(h, w, lab, chunk_size=chunk)
+            (lp * torch.linspace(-1, 1, N, device=DEV)).sum().backward()
+        return (w.main_grad if fp32_buf else w.grad).float(), h, w, lab
+
+    g4, *_ = run(N // 4, True)
+    g1, *_ = run(N, True)
+    assert _rel(g4, g1) < 1e-5
+    gb, h, w, lab = run(N // 4, False)
+    hr, wr = h.float(), w.detach().float().requires_grad_(True)
+    if head == "flce":
+        torch.nn.functional.cross_entropy(hr @ wr.t(), lab).backward()
+    else:
+        (ref.token_logps(hr @ wr.t(), lab) * torch.linspace(-1, 1, N, device=DEV)).sum().backward()
+    assert _rel(gb, wr.grad) < 8e-3  # bf16 dlogits operand + one final rounding
+
+
 def test_linear_token_logps():
     torch.manual_seed(0)
     N, H, V = 300, 128, 5000

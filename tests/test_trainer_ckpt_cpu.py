@@ -194,3 +194,37 @@ def test_convert_to_hf_from_reference_checkpoints(tmp_path, fmt):
     assert set(got) == set(hf)
     for k, v in hf.items():
         assert torch.equal(got[k], v.float()), k
+
+
+def test_convert_deepspeed_zero3_merges_frozen_fragments(tmp_path):
+    """ZeRO-3 keeps frozen parameters as per-rank fragments in every rank's model-states file; the
+    converter concatenates them in rank order (DeepSpeed zero_to_fp32 _zero3_merge_frozen_params)."""
+    from collections import OrderedDict
+
+    import yaml
+    from safetensors.torch import load_file
+
+    from llm_training_amd.tools.convert_to_hf import convert
+    hf, lm_keys, cfg = _reference_style_state()
+    (tmp_path / "cfg.yaml").write_text(yaml.safe_dump(cfg))
+    frozen = "model.embed_tokens.weight"
+    world = 3
+    trainable = OrderedDict((k, v) for k, v in lm_keys.items() if k != frozen)
+    ck = tmp_path / "ck"
+    _write_deepspeed(ck, trainable, 3, world)
+    tag = ck / "checkpoint"
+    fz = lm_keys[frozen].float().reshape(-1)
+    fz = torch.cat([fz, fz.new_zeros((-fz.numel()) % world)])
+    name = "_forward_module." + frozen
+    base = torch.load(tag / "mp_rank_00_model_states.pt", weights_only=False)
+    for r, frag in enumerate(fz.chunk(world)):
+        st = dict(base, frozen_param_shapes=OrderedDict([(name, lm_keys[frozen].shape)]),
+                  frozen_param_fragments={name: frag.clone()})
+        torch.save(st, tag / f"zero_pp_rank_{r}_mp_rank_00_model_states.pt")
+    torch.save(dict(base, frozen_param_shapes=OrderedDict([(name, lm_keys[frozen].shape)]),
+                    frozen_param_fragments={name: fz.chunk(world)[0].clone()}),
+               tag / "mp_rank_00_model_states.pt")
+    out = convert(str(ck), str(tmp_path / "hf"), config_path=str(tmp_path / "cfg.yaml"), dtype="float32")
+    got = load_file(os.path.join(out, "model.safetensors"))
+    for k, v in hf.items():
+        assert torch.equal(got[k], v.float()), k
