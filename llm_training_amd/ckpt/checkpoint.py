@@ -173,7 +173,7 @@ def _meta(trainer) -> dict:
 def save_checkpoint(trainer, path: str, async_write: bool = False, consolidated: bool | None = None):
     pc = trainer.pc
     if consolidated is None:
-        consolidated = not getattr(trainer.strategy, "save_distributed_checkpoint", True)
+        consolidated = not getattr(getattr(trainer, "strategy", None), "save_distributed_checkpoint", True)
     wait_for_pending_saves()
     if consolidated:
         _save_consolidated(trainer, path)

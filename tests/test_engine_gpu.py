@@ -243,3 +243,45 @@ def test_training_step_has_no_host_sync(rccl_group, stage, forced, packed):
         torch.cuda.set_sync_debug_mode("default")
     torch.cuda.synchronize()
     assert torch.isfinite(loss).item()
+
+
+def test_generic_optimizer_on_the_sharded_gpu_path(rccl_group, monkeypatch):
+    """A generic torch optimizer (SGD with momentum) on the optimizer stream over the fp32 master pieces:
+    forced ZeRO-2 == plain stage 0, bitwise (deterministic kernels, one-rank reduce-scatter = copy)."""
+    monkeypatch.setenv("LLMT_DETERMINISTIC", "1")
+    import functools
+    dev = rccl_group
+    fac = functools.partial(torch.optim.SGD, lr=1e-2, momentum=0.9)
+    ref_l, ref_p, e0, _ = _run(dev, 0, forced=False, optimizer_factory=fac)
+    l, p, e2, _ = _run(dev, 2, forced=True, optimizer_factory=fac)
+    assert type(e2.units[1].opt).__name__ == "SGD" and e2.units[1].opt.state
+    assert l == ref_l, (l, ref_l)
+    assert all(torch.equal(p[k], ref_p[k]) for k in ref_p)
+    assert l[-1] < l[0]
+
+
+def test_dpo_reference_model_gather_only_on_gpu(rccl_group):
+    """The ZeRO-3 gather-only reference model on the GPU path (comm-stream all-gathers into the
+    ring, prefetch, release): its log-probs equal the unsharded reference's."""
+    from llm_training_amd.lms.preference import DPO
+    from llm_training_amd.parallel.frozen import FrozenShards
+    dev = rccl_group
+    lm = DPO({"model": {"model_class": "llm_training.models.Llama",
+                        "model_config": dict(vocab_size=4096, hidden_size=512, intermediate_size=1024,
+                                             num_hidden_layers=3, num_attention_heads=8, num_key_value_heads=2)}})
+    lm.configure_model(ParallelContext.single(dev), dev, torch.bfloat16, seed=3)
+    g = torch.Generator(device=dev).manual_seed(1)
+    b = {}
+    for side in ("chosen", "rejected"):
+        ids = torch.randint(0, 4096, (2, 256), device=dev, generator=g)
+        b.update({f"{side}_input_ids": ids, f"{side}_labels": ids,
+                  f"{side}_attention_mask": torch.ones_like(ids)})
+    with torch.no_grad():
+        want = lm.logps(lm.ref_model, b)
+    fs = FrozenShards(lm.ref_model, dist.group.WORLD, 0, 1, torch.cuda.Stream(device=dev))
+    for _ in range(2):
+        with torch.no_grad():
+            got = lm.logps(lm.ref_model, b)
+        fs.release_all()
+        assert all(torch.equal(x, y) for x, y in zip(got, want))
+    assert sum(p.numel() for p in lm.ref_model.parameters()) == 0  # nothing bound between forwards
