@@ -33,7 +33,7 @@ hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const float* cos
 hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, int V, const int64_t* labels,
                               int64_t vocab_start, int64_t ignore_index, const float* lse_in, float* lse_out,
                               float* tgt_out, float* loss_out, const float* coef_row, const float* coef_scalar,
-                              int write_grad, int64_t vocab_total, int* err, hipStream_t stream);
+                              int write_grad, int64_t vocab_total, int* err, float* rowsum_out, hipStream_t stream);
 hipError_t llmt_adamw(float* p, float* m, float* v, const void* g, int grad_is_fp32, void* pout, int64_t n,
                       float lr, float b1, float b2, float eps, float wd, int64_t step, const float* gscale,
                       hipStream_t stream);
@@ -265,7 +265,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_(at::Tensor logits,
                                                              const c10::optional<at::Tensor>& lse_in,
                                                              const c10::optional<at::Tensor>& coef_row,
                                                              const c10::optional<at::Tensor>& coef_scalar,
-                                                             bool write_grad, int64_t vocab_total) {
+                                                             bool write_grad, int64_t vocab_total,
+                                                             const c10::optional<at::Tensor>& rowsum) {
   check_bf16_cuda(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] with unit column stride");
   const int64_t N = logits.size(0), V = logits.size(1);
@@ -281,7 +282,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_(at::Tensor logits,
   check(llmt_cross_entropy(logits.data_ptr(), N, logits.stride(0), (int)V, labels.data_ptr<int64_t>(), vocab_start,
                            ignore_index, fptr(lse_in, N), lse.data_ptr<float>(), tgt.data_ptr<float>(),
                            loss.data_ptr<float>(), fptr(coef_row, N), fptr(coef_scalar, 1), write_grad ? 1 : 0,
-                           vocab_total >= 0 ? vocab_total : (vocab_start == 0 ? V : 0), err_words(), cur_stream()),
+                           vocab_total >= 0 ? vocab_total : (vocab_start == 0 ? V : 0), err_words(),
+                           (rowsum.has_value() && rowsum->defined() && !lse_in.has_value())
+                               ? const_cast<float*>(fptr(rowsum, N)) : nullptr,
+                           cur_stream()),
         "cross_entropy");
   return {lse, tgt, loss};
 }
@@ -485,7 +489,8 @@ TORCH_LIBRARY(llmt, m) {
   m.def("rope_(Tensor(a!) qkv, Tensor pos, Tensor cos, Tensor sin, int nheads, bool inverse) -> ()");
   m.def(
       "cross_entropy_(Tensor(a!) logits, Tensor labels, int vocab_start, int ignore_index, Tensor? lse_in, "
-      "Tensor? coef_row, Tensor? coef_scalar, bool write_grad, int vocab_total=-1) -> (Tensor, Tensor, Tensor)");
+      "Tensor? coef_row, Tensor? coef_scalar, bool write_grad, int vocab_total=-1, Tensor(b!)? rowsum=None) -> "
+      "(Tensor, Tensor, Tensor)");
   m.def("kernel_errors() -> Tensor", &kernel_errors);
   m.def(
       "adamw_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? pout, float lr, float b1, float b2, "

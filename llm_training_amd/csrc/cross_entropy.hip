@@ -25,7 +25,8 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
                                                  float* __restrict__ lse_out, float* __restrict__ tgt_out,
                                                  float* __restrict__ loss_out, const float* __restrict__ coef_row,
                                                  const float* __restrict__ coef_scalar, int write_grad,
-                                                 int64_t vocab_total, int* __restrict__ err) {
+                                                 int64_t vocab_total, int* __restrict__ err,
+                                                 float* __restrict__ rowsum_out) {
   __shared__ float red[4];
   const int64_t row = blockIdx.x;
   bf16* x = logits + row * ld;
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
   if (lse_in) {
     lse = lse_in[row];
   } else {
-    float m = -INFINITY, s = 0.f;
+    float m = -INFINITY, s = 0.f, rsum = 0.f;  // rsum: plain sum of the row's logits (ORPO metrics)
     if constexpr (VEC) {
       const bf16x8* xv = reinterpret_cast<const bf16x8*>(x);
       const int V8 = V >> 3;
@@ -56,7 +57,10 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
           m = lm;
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s += __expf(f[i] - m);
+        for (int i = 0; i < 8; ++i) {
+          s += __expf(f[i] - m);
+          rsum += f[i];
+        }
       }
       for (int j = (V8 << 3) + tid; j < V; j += 256) {
         const float f = bf2f(x[j]);
@@ -65,6 +69,7 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
           m = f;
         }
         s += __expf(f - m);
+        rsum += f;
       }
     } else {
       for (int j = tid; j < V; j += 256) {
@@ -74,12 +79,17 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
           m = f;
         }
         s += __expf(f - m);
+        rsum += f;
       }
     }
     const float gm = block_max<4>(m, red);
     s = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
     const float gs = block_sum<4>(s, red);
     lse = gm + __logf(gs);
+    if (rowsum_out) {  // uniform branch: every thread takes part in the block reduction
+      const float rs = block_sum<4>(rsum, red);
+      if (tid == 0) rowsum_out[row] = rs;
+    }
   }
   const float tgt = local_hit ? bf2f(x[lloc]) : 0.f;
   if (tid == 0) {
@@ -128,16 +138,16 @@ extern "C" hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, in
                                          int64_t vocab_start, int64_t ignore_index, const float* lse_in,
                                          float* lse_out, float* tgt_out, float* loss_out, const float* coef_row,
                                          const float* coef_scalar, int write_grad, int64_t vocab_total, int* err,
-                                         hipStream_t stream) {
+                                         float* rowsum_out, hipStream_t stream) {
   if (N == 0) return hipSuccess;
   const bool vec = (ld % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) & 15) == 0);
   if (vec)
     ce_kernel<true><<<(unsigned)N, 256, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index, lse_in,
                                                      lse_out, tgt_out, loss_out, coef_row, coef_scalar, write_grad,
-                                                     vocab_total, err);
+                                                     vocab_total, err, rowsum_out);
   else
     ce_kernel<false><<<(unsigned)N, 256, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index,
                                                       lse_in, lse_out, tgt_out, loss_out, coef_row, coef_scalar,
-                                                      write_grad, vocab_total, err);
+                                                      write_grad, vocab_total, err, rowsum_out);
   return hipGetLastError();
 }

@@ -174,12 +174,13 @@ class BaseLM:
                                                 ignore_index, chunk, vocab_size=model.embed_tokens.vocab_size)
         return fused_linear_cross_entropy(h, w, labels_sb, ignore_index, chunk)
 
-    def token_logps_from_hidden(self, model: BaseModel, h, labels_sb, ignore_index: int):
+    def token_logps_from_hidden(self, model: BaseModel, h, labels_sb, ignore_index: int, logit_sums: bool = False):
         from ..ops.fused import linear_token_logps
         w = model.lm_head_weight()
         chunk = getattr(model.config, "loss_chunk_size", 8192)
         if model.pc.tp:
             from ..parallel.vocab_parallel import vocab_parallel_token_logps
             return vocab_parallel_token_logps(h, w, labels_sb, model.embed_tokens.v0, model.pc.tp_group,
-                                              ignore_index, chunk, vocab_size=model.embed_tokens.vocab_size)
-        return linear_token_logps(h, w, labels_sb, ignore_index, chunk)
+                                              ignore_index, chunk, vocab_size=model.embed_tokens.vocab_size,
+                                              logit_sums=logit_sums)
+        return linear_token_logps(h, w, labels_sb, ignore_index, chunk, logit_sums=logit_sums)

@@ -49,15 +49,26 @@ def concat_pair(batch: dict, ignore_index: int, pad_id: int = 0, multiple: int =
 
 
 class _PairMixin:
-    def pair_token_logps(self, model, batch, pad_id=0):
-        multiple = model.pc.tp_size if model.pc.tp else 1
-        cat = concat_pair(batch, self.config.ignore_index, pad_id, multiple)
+    def pair_token_logps(self, model, batch, pad_id=0, logit_means: bool = False):
+        """Per-token log-probs of the chosen and rejected rows in one forward. ``logit_means``: also the
+        mean logit of the chosen / rejected forwards over their own [B, S, V] (reference ORPO metrics
+        "Chosen Logits" / "Rejected Logits", orpo.py:149-150), from the CE kernel's row sums."""
+        cat = concat_pair(batch, self.config.ignore_index, pad_id)
         labels = shift_labels(cat["labels"], self.config.ignore_index)
         cat["attention_mask_trivial"] = False
         h = self.hidden_and_head(model, cat["input_ids"], "attention_mask", cat)
-        lp = self.token_logps_from_hidden(model, h, labels.t().contiguous(), self.config.ignore_index).t()
+        res = self.token_logps_from_hidden(model, h, labels.t().contiguous(), self.config.ignore_index,
+                                           logit_sums=logit_means)
+        lp, rs = res if logit_means else (res, None)
+        lp = lp.t()
         mask = labels != self.config.ignore_index
         B = batch["chosen_input_ids"].shape[0]
+        if logit_means:
+            V = getattr(model.config, "vocab_size", None) or model.lm_head_weight().shape[0]
+            rs = rs.t()  # [2B, S]
+            sc, sr = batch["chosen_input_ids"].shape[1], batch["rejected_input_ids"].shape[1]
+            means = (rs[:B, :sc].sum() / (B * sc * V), rs[B:, :sr].sum() / (B * sr * V))
+            return lp, mask, B, h, labels, means
         return lp, mask, B, h, labels
 
 
@@ -152,7 +163,7 @@ class ORPO(_PairMixin, BaseLM):
     config_class = ORPOConfig
 
     def _step(self, batch):
-        lp, mask, B, h, labels = self.pair_token_logps(self.model, batch)
+        lp, mask, B, h, labels, (c_logits, r_logits) = self.pair_token_logps(self.model, batch, logit_means=True)
         n = mask.sum(-1).clamp(min=1)
         seq = lp.sum(-1) / n  # ORPO: length-normalised log-probs (reference orpo.py:93)
         c_lp, r_lp = seq[:B], seq[B:]
@@ -168,7 +179,8 @@ class ORPO(_PairMixin, BaseLM):
         m = {"OR Loss": or_loss.detach(), "CE Loss": ce_loss.detach(), "Chosen Rewards": cr.mean(),
              "Rejected Rewards": rr.mean(), "Reward Accuracy": (cr > rr).float().mean(),
              "Reward Margin": (cr - rr).mean(), "Chosen Log P": c_lp.detach().mean(),
-             "Rejected Log P": r_lp.detach().mean(), "Log Odds Ratio": ratio.detach().mean(),
+             "Rejected Log P": r_lp.detach().mean(), "Chosen Logits": c_logits, "Rejected Logits": r_logits,
+             "Log Odds Ratio": ratio.detach().mean(),
              "Log Odds Chosen": log_odds.detach().mean(), "Loss": loss.detach()}
         return loss, m
 

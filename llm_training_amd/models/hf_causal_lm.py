@@ -95,7 +95,9 @@ def _register_hf_attention():
 class HFCausalLMConfig(BaseModelConfig):
     hf_config: dict[str, Any] | None = None
     enable_gradient_checkpointing: bool = False
-    enable_liger_kernel: bool = False  # accepted for parity; the fused loss head is always used
+    # reference hf_causal_lm.py:42-43 (Liger instance patch, rope=False): RMSNorm and the SiLU-gated MLP
+    # of the transformers modules run on the HIP kernels (the loss head is always the fused one)
+    enable_liger_kernel: bool = False
     loss_chunk_size: int = 8192
 
 
@@ -131,6 +133,10 @@ class HFCausalLM(BaseModel):
             self.hf_model.to(device)
         if config.enable_gradient_checkpointing:
             self.hf_model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+        self.fused_modules: dict[str, int] = {}
+        if config.enable_liger_kernel:
+            self.fused_modules = apply_fused_kernels(self.hf_model)
+            logger.info("HFCausalLM: fused kernels patched into %s", self.fused_modules or "no module")
 
     @property
     def hf_config(self):
@@ -219,6 +225,71 @@ class HFCausalLM(BaseModel):
 
     def _tp_rule(self, key):
         return "rep", None
+
+
+# ---------------------------------------------------------------------------- fused-kernel instance patch
+# RMSNorm classes computing w * (x / rms(x)) in fp32 then cast (Llama / Mistral / Qwen2 / Qwen3 / Phi-3 /
+# Granite / OLMo-2 ...). Gemma-style (1 + w) norms are left alone.
+_NORM_SKIP = ("Gemma",)
+
+
+def _patch_norm(m: nn.Module) -> bool:
+    if getattr(m, "weight", None) is None or type(m).__name__.startswith(_NORM_SKIP):
+        return False
+    eps = getattr(m, "variance_epsilon", getattr(m, "eps", None))
+    if eps is None:
+        return False
+
+    def forward(hidden_states, _m=m, _eps=float(eps)):
+        from ..ops.fused import rms_norm
+        return rms_norm(hidden_states, _m.weight, _eps)
+
+    m.forward = forward
+    return True
+
+
+def _is_silu(act) -> bool:
+    return isinstance(act, nn.SiLU) or type(act).__name__ in ("SiLUActivation", "SiLU")
+
+
+def _patch_mlp(m: nn.Module) -> bool:
+    act = getattr(m, "act_fn", getattr(m, "activation_fn", None))
+    if act is None or not _is_silu(act):
+        return False
+    if all(hasattr(m, n) for n in ("gate_proj", "up_proj", "down_proj")):
+        # one GEMM for gate and up (the weights concatenated per call), the SwiGLU kernel on the fused
+        # [.., 2I] buffer, then down_proj (Liger's LigerSwiGLUMLP)
+        def forward(x, _m=m):
+            from ..ops.fused import swiglu
+            w = torch.cat([_m.gate_proj.weight, _m.up_proj.weight], 0)
+            b = None
+            if _m.gate_proj.bias is not None:
+                b = torch.cat([_m.gate_proj.bias, _m.up_proj.bias], 0)
+            return _m.down_proj(swiglu(torch.nn.functional.linear(x, w, b)))
+    elif hasattr(m, "gate_up_proj") and hasattr(m, "down_proj"):  # Phi-3: fused [gate | up] projection
+        def forward(x, _m=m):
+            from ..ops.fused import swiglu
+            return _m.down_proj(swiglu(_m.gate_up_proj(x)))
+    else:
+        return False
+    m.forward = forward
+    return True
+
+
+def apply_fused_kernels(model: nn.Module) -> dict[str, int]:
+    """Patch every RMSNorm and SiLU-gated MLP instance of a transformers model onto the HIP kernels;
+    returns {class name: count}. On the CPU the same functions run their torch reference ops."""
+    done: dict[str, int] = {}
+    for m in model.modules():
+        name = type(m).__name__
+        ok = False
+        if name.endswith("RMSNorm"):
+            ok = _patch_norm(m)
+        elif name.endswith("MLP"):
+            ok = _patch_mlp(m)
+        if ok:
+            done[name] = done.get(name, 0) + 1
+    return done
 
 
 class _ParamsUnit(nn.Module):

@@ -823,18 +823,21 @@ class _LinearLogpsFn(Function):
         L = lib()
         N = h.shape[0]
         out = torch.empty(N, device=h.device, dtype=torch.float32)
+        rowsum = torch.empty(N, device=h.device, dtype=torch.float32)  # sum of each row's logits (metrics)
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
-            _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, None, False)
+            _, _, lr = L.cross_entropy_(lg, labels[s0:s1], 0, ignore_index, None, None, None, False, -1,
+                                        rowsum[s0:s1])
             out[s0:s1] = -lr
         ctx.save_for_backward(h, labels)
         ctx.w = w
         ctx.cfg = (ignore_index, chunk)
-        return out
+        ctx.mark_non_differentiable(rowsum)
+        return out, rowsum
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, _g_rowsum=None):
         h, labels = ctx.saved_tensors
         w = ctx.w
         ignore_index, chunk = ctx.cfg
@@ -858,15 +861,21 @@ class _LinearLogpsFn(Function):
         return dh, dwr, None, None, None
 
 
-def linear_token_logps(h, w, labels, ignore_index: int = -100, chunk_size: int = 8192):
-    """log p(labels) per token for logits = h @ w.T; zeros where label == ignore_index. h: [N, H]."""
+def linear_token_logps(h, w, labels, ignore_index: int = -100, chunk_size: int = 8192,
+                       logit_sums: bool = False):
+    """log p(labels) per token for logits = h @ w.T; zeros where label == ignore_index. h: [N, H].
+    ``logit_sums``: also return each row's sum of logits (fp32, no gradient; the CE kernel's side output)
+    for the reference's ORPO "Chosen / Rejected Logits" metrics without materialising the logits."""
     h2 = h.reshape(-1, h.shape[-1])
     lab = labels.reshape(-1)
     if use_native(h2):
-        out = _LinearLogpsFn.apply(h2.contiguous(), w, lab.contiguous(), ignore_index, chunk_size)
+        out, rs = _LinearLogpsFn.apply(h2.contiguous(), w, lab.contiguous(), ignore_index, chunk_size)
     else:
-        out = ref.token_logps(linear(h2, w), lab, ignore_index)
-    return out.view(labels.shape)
+        logits = linear(h2, w)
+        out = ref.token_logps(logits, lab, ignore_index)
+        rs = logits.detach().float().sum(-1)
+    out = out.view(labels.shape)
+    return (out, rs.view(labels.shape)) if logit_sums else out
 
 
 def token_logps(logits, labels, ignore_index: int = -100):

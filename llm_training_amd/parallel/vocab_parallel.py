@@ -31,16 +31,18 @@ def _combine_lse(lse_local: torch.Tensor, group) -> torch.Tensor:
     return torch.logsumexp(allv.view(n, -1), dim=0)
 
 
-def _local_stats(lg, lab, v0, ignore_index, native):
-    """(lse_local, tgt_local) of logits lg [n, Vl] for global labels lab."""
+def _local_stats(lg, lab, v0, ignore_index, native, rowsum=None):
+    """(lse_local, tgt_local) of logits lg [n, Vl] for global labels lab (+ local row sums into rowsum)."""
     if native:
-        lse, tgt, _ = lib().cross_entropy_(lg, lab, v0, ignore_index, None, None, None, False, 0)
+        lse, tgt, _ = lib().cross_entropy_(lg, lab, v0, ignore_index, None, None, None, False, 0, rowsum)
         return lse, tgt
     lf = lg.float()
     lse = torch.logsumexp(lf, -1)
     loc = lab - v0
     hit = (lab != ignore_index) & (loc >= 0) & (loc < lg.shape[1])
     tgt = lf.gather(1, loc.clamp(0, lg.shape[1] - 1).unsqueeze(1)).squeeze(1) * hit
+    if rowsum is not None:
+        rowsum.copy_(lf.sum(-1))
     return lse, tgt
 
 
@@ -127,23 +129,27 @@ class _VPLogps(Function):
         N = h.shape[0]
         w = w_full[:n_valid]
         lses, tgts = [], []
+        rowsum = torch.zeros(N, device=h.device, dtype=torch.float32)
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
-            lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
+            lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native, rowsum[s0:s1])
             lses.append(lse)
             tgts.append(tgt)
         lse = _combine_lse(torch.cat(lses), group)
-        tgt = torch.cat(tgts)
-        dist.all_reduce(tgt, group=group)
+        # target logits and the per-row logit sums (ORPO metrics) in one all-reduce
+        both = torch.stack([torch.cat(tgts), rowsum])
+        dist.all_reduce(both, group=group)
+        tgt, rowsum = both[0], both[1].contiguous()
         valid = labels != ignore_index
         ctx.save_for_backward(h, labels, lse)
         ctx.w = w_full
         ctx.cfg = (v0, ignore_index, chunk, n_valid)
-        return (tgt - lse) * valid
+        ctx.mark_non_differentiable(rowsum)
+        return (tgt - lse) * valid, rowsum
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, _g_rowsum=None):
         h, labels, lse = ctx.saved_tensors
         w_full = ctx.w
         v0, ignore_index, chunk, n_valid = ctx.cfg
@@ -180,9 +186,9 @@ def vocab_parallel_cross_entropy(h, w_local, labels, vocab_start, group, ignore_
 
 
 def vocab_parallel_token_logps(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192,
-                               vocab_size: int | None = None):
+                               vocab_size: int | None = None, logit_sums: bool = False):
     shape = labels.shape
     h = h.reshape(-1, h.shape[-1]).contiguous()
-    out = _VPLogps.apply(h, w_local, labels.reshape(-1).contiguous(), int(vocab_start), ignore_index, group,
-                         chunk_size, _n_valid(w_local, vocab_start, vocab_size))
-    return out.view(shape)
+    out, rs = _VPLogps.apply(h, w_local, labels.reshape(-1).contiguous(), int(vocab_start), ignore_index, group,
+                             chunk_size, _n_valid(w_local, vocab_start, vocab_size))
+    return (out.view(shape), rs.view(shape)) if logit_sums else out.view(shape)

@@ -294,3 +294,30 @@ def test_checkpoint_keep_attention_skips_the_attention_recompute():
     assert not bad, bad
     e = [k for k in g0 if "embed" in k][0]
     assert ((g0[e].float() - g1[e].float()).norm() / g0[e].float().norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("model_type", ["llama", "phi3"])
+def test_hf_enable_liger_kernel_on_hip(model_type):
+    """enable_liger_kernel on the GPU: the patched transformers RMSNorm / MLP run the HIP RMSNorm and
+    SwiGLU kernels (bf16) and agree with the unpatched model to bf16 tolerance, forward and backward."""
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 8, "num_key_value_heads": 4,
+          "hidden_size": 512, "intermediate_size": 1024, "vocab_size": 1000, "max_position_embeddings": 512}
+    if model_type == "phi3":
+        hc.update(pad_token_id=0, bos_token_id=1, eos_token_id=2)
+    outs = []
+    for patch in (False, True):
+        m = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=patch), dtype=torch.bfloat16,
+                       device="cuda")
+        m.init_weights(0)
+        ids = torch.randint(0, 1000, (2, 256), device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+        h = m.hidden_states(ids)
+        (h.float() ** 2).mean().backward()
+        outs.append((h.detach().float(), {n: p.grad.float() for n, p in m.named_parameters() if p.grad is not None}))
+    (h0, g0), (h1, g1) = outs
+
+    def rel(a, b):
+        return ((a - b).norm() / (b.norm() + 1e-12)).item()
+    assert rel(h1, h0) < 2e-2
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 5e-2, k

@@ -184,6 +184,12 @@ def test_orpo_loss_matches_formula():
     or_loss = -(0.1 * torch.nn.functional.logsigmoid(lo)).mean()
     ce = -cs.sum() / cn.sum()
     assert abs(loss.item() - (or_loss + ce).item()) < 1e-4
+    # reference metrics "Chosen Logits" / "Rejected Logits" (orpo.py:149-150): mean of each forward's logits
+    with torch.no_grad():
+        cl = orpo.model(input_ids=batch["chosen_input_ids"]).logits.mean()
+        rl = orpo.model(input_ids=batch["rejected_input_ids"]).logits.mean()
+    assert abs(m["Chosen Logits/Train/Step"].item() - cl.item()) < 1e-5
+    assert abs(m["Rejected Logits/Train/Step"].item() - rl.item()) < 1e-5
 
 
 @pytest.mark.parametrize("granularity", ["full", "selective", "full_keep_attention"])
@@ -281,3 +287,30 @@ def test_attention_dropout_applies_in_training_only():
         torch.manual_seed(2)
         b = drop(input_ids=ids).logits
     assert not torch.allclose(a, b)
+
+
+@pytest.mark.parametrize("model_type", ["llama", "qwen2", "mistral", "phi3"])
+def test_hf_enable_liger_kernel_patches_and_matches(model_type):
+    """HFCausalLM(enable_liger_kernel=True) (reference hf_causal_lm.py:42-43): RMSNorm and the SiLU-gated
+    MLP modules run on the fused ops and the model's outputs / gradients equal the unpatched HF model."""
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 2,
+          "hidden_size": 64, "intermediate_size": 128, "vocab_size": 100, "max_position_embeddings": 64}
+    if model_type == "phi3":
+        hc.update(pad_token_id=0, bos_token_id=1, eos_token_id=2)
+    outs = []
+    for patch in (False, True):
+        m = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=patch, attn_implementation="eager"))
+        m.init_weights(0)
+        if patch:
+            names = set(m.fused_modules)
+            assert any(n.endswith("RMSNorm") for n in names) and any(n.endswith("MLP") for n in names), names
+        ids = torch.randint(0, 100, (2, 16), generator=torch.Generator().manual_seed(1))
+        h = m.hidden_states(ids)
+        h.float().pow(2).mean().backward()
+        outs.append((h.detach(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}))
+    (h0, g0), (h1, g1) = outs
+    assert torch.allclose(h0, h1, atol=1e-5, rtol=1e-4)
+    assert g0.keys() == g1.keys()
+    for k in g0:
+        assert torch.allclose(g0[k], g1[k], atol=1e-5, rtol=1e-4), k

@@ -68,7 +68,8 @@ def test_vocab_parallel_heads(group, head):
         torch.nn.functional.cross_entropy(hr @ wr.t(), lab, ignore_index=-100).backward()
         assert abs(out.item() - torch.nn.functional.cross_entropy(hr @ wr.t(), lab).item()) < 2e-2
     else:
-        out = vp._VPLogps.apply(h, w, lab, 0, -100, group, 256, V)
+        out, rs = vp._VPLogps.apply(h, w, lab, 0, -100, group, 256, V)
+        assert _rel(rs, (hr @ wr.t()).sum(-1)) < 1e-2  # logit row sums (ORPO metrics)
         gg = torch.randn_like(out)
         (out * gg).sum().backward()
         lr_ = ref.token_logps(hr @ wr.t(), lab)
