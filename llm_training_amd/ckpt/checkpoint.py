@@ -164,6 +164,7 @@ def _meta(trainer) -> dict:
         "tp_size": pc.tp_size, "dp_size": pc.dp_size, "zero_stage": eng.stage,
         "param_dtype": str(eng.param_dtype).replace("torch.", ""),
         "optimizer_kinds": eng.state_kinds(),
+        "loss_scaler": trainer.scaler.state_dict() if getattr(trainer, "scaler", None) is not None else None,
         "config": trainer.config_dict,
         "model_class": f"{type(trainer.lm.model).__module__}.{type(trainer.lm.model).__qualname__}",
         "model_config": trainer.lm.model.config.model_dump(mode="json"),
@@ -462,6 +463,8 @@ def load_checkpoint(trainer, path: str, load_optimizer: bool = True):
         trainer.state.load_state_dict(meta["trainer"])
         if trainer.scheduler is not None and meta.get("scheduler"):
             trainer.scheduler.load_state_dict(meta["scheduler"])
+        if getattr(trainer, "scaler", None) is not None and meta.get("loss_scaler"):
+            trainer.scaler.load_state_dict(meta["loss_scaler"])
         # generator states: exact continuation of NEFTune noise / dropout when the layout is unchanged
         st = {k: v for k, v in side.items() if k in ("cpu", "cuda")}
         if st:

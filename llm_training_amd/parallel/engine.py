@@ -201,6 +201,8 @@ class DataParallelEngine:
         self.cuda = dev.type == "cuda"
         # the optimizer / norm kernels take fp32 or bf16 gradients: native on any GPU
         self.native = self.cuda and use_native(torch.empty(0, device=dev, dtype=torch.bfloat16))
+        if any(p.dtype == torch.float16 for p in model.parameters()) or grad_dtype == torch.float16:
+            self.native = False  # fp16 precisions: the bf16/fp32 optimizer and norm kernels do not apply
         self.comm_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.overlap) else None
         if self.cuda and (self.dp > 1 or self.pc.tp_size > 1):
             # RCCL kernels share the CUs with the GEMMs of the compute stream: hipBLASLt's stream-K
@@ -749,11 +751,12 @@ class DataParallelEngine:
         pool = sum(s["buf"].numel() * s["buf"].element_size() for s in getattr(self, "_gpool", []))
         return {"persistent": persistent, "transient": transient, "pool": pool}
 
-    def clip_and_scale(self, max_norm: float | None):
-        """Global grad norm computed on device; returns the device scalar scale used by the optimizer."""
+    def clip_and_scale(self, max_norm: float | None, loss_scale: float = 1.0):
+        """Global grad norm computed on device; returns the device scalar scale used by the optimizer.
+        ``loss_scale``: the fp16 loss scale the gradients carry (divided out of the norm and the update)."""
         if self.opt_stream is not None:
             torch.cuda.current_stream().wait_stream(self.opt_stream)
-        denom = float(self.dp * self.accum)
+        denom = float(self.dp * self.accum) * float(loss_scale)
         need_norm = max_norm is not None and max_norm > 0
         sumsq = torch.zeros(1, device=self.device, dtype=torch.float32)
         rep = torch.zeros(1, device=self.device, dtype=torch.float32)

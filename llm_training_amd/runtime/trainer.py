@@ -40,12 +40,46 @@ logger = logging.getLogger("llm_training")
 #  * bf16-mixed: bf16 compute copies, fp32 gradients (accumulated and reduced in fp32) on fp32 masters —
 #                the numerics of autocast over fp32 parameters (fsdp2_precision.py:55-90,106-117)
 #  * 32-true   : fp32 everywhere; on the GPU the torch ops run (the HIP kernels are bf16 MFMA kernels)
-#  * 16-*      : rejected with an explanation (fp16 needs loss scaling and the kernels are bf16; bf16 runs
-#                at the same MFMA rate on MI355X with fp32's exponent range)
+#  * 16-true / 16-mixed: fp16 params (fp16 / fp32 gradients) with a dynamic loss scaler (reference
+#                FSDP2Precision GradScaler, fsdp2_precision.py:19-21,55-96,129-163, without its Q10 bug):
+#                the loss is scaled before backward, gradients are unscaled inside the clip scale, a step
+#                whose gradient norm is not finite is skipped and halves the scale, 2000 good steps
+#                double it. fp16 tensors run the torch ops (the HIP kernels are bf16 MFMA kernels: bf16
+#                runs at the same rate on MI355X with fp32's exponent range and needs no scaler).
 PRECISIONS = {"bf16-true": (torch.bfloat16, None), "bf16": (torch.bfloat16, None),
               "bf16-mixed": (torch.bfloat16, torch.float32), "32-true": (torch.float32, None),
-              "32": (torch.float32, None), 32: (torch.float32, None), "64-true": None, "16-true": None,
-              "16-mixed": None, 16: None, "16": None, "transformer-engine": None}
+              "32": (torch.float32, None), 32: (torch.float32, None), "64-true": None,
+              "16-true": (torch.float16, None), "16": (torch.float16, None), 16: (torch.float16, None),
+              "16-mixed": (torch.float16, torch.float32), "transformer-engine": None}
+FP16 = {"16-true", "16", 16, "16-mixed"}
+
+
+class LossScaler:
+    """Dynamic loss scale for fp16 (torch.amp.GradScaler semantics: init 2**16, x2 every 2000 finite
+    steps, x0.5 on an overflow, whose step is skipped)."""
+
+    def __init__(self, init_scale: float = 2.0 ** 16, growth_factor: float = 2.0, backoff_factor: float = 0.5,
+                 growth_interval: int = 2000):
+        self.scale, self.growth_factor, self.backoff_factor = float(init_scale), growth_factor, backoff_factor
+        self.growth_interval, self.good_steps, self.skipped = int(growth_interval), 0, 0
+
+    def update(self, finite: bool) -> bool:
+        if finite:
+            self.good_steps += 1
+            if self.good_steps >= self.growth_interval:
+                self.scale *= self.growth_factor
+                self.good_steps = 0
+        else:
+            self.scale *= self.backoff_factor
+            self.good_steps = 0
+            self.skipped += 1
+        return finite
+
+    def state_dict(self):
+        return {"scale": self.scale, "good_steps": self.good_steps, "skipped": self.skipped}
+
+    def load_state_dict(self, st):
+        self.scale, self.good_steps, self.skipped = float(st["scale"]), int(st["good_steps"]), int(st["skipped"])
 # Lightning Trainer arguments that exist upstream but have no effect here: accepted (with a warning)
 # so reference configs load; anything else is a typo and raises, as jsonargparse would
 IGNORED_TRAINER_ARGS = {"num_sanity_val_steps", "benchmark", "fast_dev_run",
@@ -124,9 +158,9 @@ class Trainer:
         if precision not in PRECISIONS:
             raise ValueError(f"unknown precision {precision!r}; use one of bf16-true, bf16-mixed, 32-true")
         if PRECISIONS[precision] is None:
-            raise ValueError(f"precision {precision!r} is not supported: the MI355X kernels are bf16 MFMA kernels "
-                             "(same rate as fp16, fp32 exponent range, no loss scaling needed) — use bf16-true or "
-                             "bf16-mixed, or 32-true for fp32")
+            raise ValueError(f"precision {precision!r} is not supported; use bf16-true, bf16-mixed, 16-true, "
+                             "16-mixed or 32-true")
+        self.scaler = LossScaler() if precision in FP16 else None
         self.pc: ParallelContext | None = None
         self.engine: DataParallelEngine | None = None
         self.lm = None
@@ -360,22 +394,35 @@ class Trainer:
             with trace_range("forward"):
                 loss, metrics, cnt = lm.training_step(b, self.state.batch_idx + i)
             with trace_range("backward"):
-                loss.backward()
+                (loss * self.scaler.scale if self.scaler is not None else loss).backward()
             for k, v in metrics.items():
                 metrics_acc[k] = metrics_acc.get(k, 0) + v.detach().float().to(self.device) / len(batches)
             for k, v in cnt.items():
                 counters[k] = counters.get(k, 0) + v
         with trace_range("optimizer"):
             eng.finish_backward()
-            eng.clip_and_scale(self.gradient_clip_val)
-            lr = self.scheduler.get_lr()
-            eng.step(lr)
+            if self.scaler is None:
+                eng.clip_and_scale(self.gradient_clip_val)
+                lr = self.scheduler.get_lr()
+                eng.step(lr)
+            else:  # fp16: unscale inside the clip scale; an overflowed step is skipped (one host sync)
+                eng.clip_and_scale(self.gradient_clip_val, loss_scale=self.scaler.scale)
+                finite = bool(torch.isfinite(eng.grad_norm).all().item())
+                lr = self.scheduler.get_lr()
+                if self.scaler.update(finite):
+                    eng.step(lr)
+                else:
+                    logger.warning("fp16 gradient overflow at step %d: step skipped, loss scale -> %g",
+                                   self.state.global_step + 1, self.scaler.scale)
         self.last_lr = lr
         self.scheduler.step()
         self.state.global_step += 1
         for k, v in counters.items():
             self.state.consumed[k] = self.state.consumed.get(k, 0) + v
         metrics_acc["lr"] = torch.tensor(lr)
+        if self.scaler is not None:  # reference: DeepSpeed fp16 skipped steps on the progress bar
+            metrics_acc["Loss Scale"] = torch.tensor(self.scaler.scale)
+            metrics_acc["Skipped Steps"] = torch.tensor(float(self.scaler.skipped))
         if getattr(lm.config, "log_grad_norm", True) and eng.grad_norm is not None:
             metrics_acc["Gradient Norm"] = eng.grad_norm.reshape(())
         self.state.batch_idx += len(batches)

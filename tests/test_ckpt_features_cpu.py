@@ -211,3 +211,24 @@ def test_generic_optimizer_resume_is_exact(tmp_path, opt, kw):
     a, b = _losses(log1 / "r"), _losses(log2 / "r")
     for s in (4, 5, 6):
         assert abs(a[s] - b[s]) < 1e-6, (s, a[s], b[s])
+
+
+@pytest.mark.parametrize("precision", ["16-mixed", "16-true"])
+def test_fp16_precisions_with_dynamic_loss_scaler(tmp_path, precision):
+    """fp16 params with the loss scaler (reference FSDP2Precision 16-true / 16-mixed): an absurd initial
+    scale overflows, those steps are skipped and the scale backs off until training proceeds; the
+    scaler state is checkpointed."""
+    log = tmp_path / "log"
+    t = Trainer(strategy="ddp", precision=precision, max_steps=8, seed=1, log_every_n_steps=1,
+                logger=JSONLLogger(str(log), "r"), default_root_dir=str(tmp_path))
+    t.scaler.scale = 2.0 ** 100  # overflows fp16 gradients at once
+    lm = _lm()
+    t.fit(lm, _dm())
+    assert next(lm.model.parameters()).dtype == torch.float16
+    assert t.scaler.skipped >= 1 and t.scaler.scale < 2.0 ** 100
+    rows = [json.loads(line) for line in open(log / "r" / "metrics.jsonl")]
+    assert rows[-1]["Skipped Steps"] == t.scaler.skipped
+    losses = [r["Loss/Train/Step"] for r in rows if "Loss/Train/Step" in r]
+    assert all(x == x for x in losses)
+    t.save_checkpoint(str(tmp_path / "ck"))
+    assert ckpt.read_meta(str(tmp_path / "ck"))["loss_scaler"]["scale"] == t.scaler.scale
