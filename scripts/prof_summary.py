@@ -27,7 +27,17 @@ def main():
     ap.add_argument("--tail-ms", type=float, default=0.0,
                     help="only dispatches that start in the last X ms of the trace (steady-state steps; "
                          "skips warm-up, GEMM solution timing and start-up kernels)")
+    ap.add_argument("--bench-log", default=None,
+                    help="bench.py output of the profiled run: its JSON line sets --steps and --tail-ms "
+                         "(the timed steps only)")
     args = ap.parse_args()
+    if args.bench_log:
+        import json
+        for line in open(args.bench_log):
+            if line.startswith('{"metric"'):
+                r = json.loads(line)
+                args.steps = int(r["steps"])
+                args.tail_ms = float(r["ms_per_step"]) * args.steps
     c = sqlite3.connect(args.db)
     span = c.execute("select min(start), max(end) from rocpd_kernel_dispatch").fetchone()
     t0 = span[1] - int(args.tail_ms * 1e6) if args.tail_ms else span[0]
