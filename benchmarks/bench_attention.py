@@ -30,19 +30,21 @@ def main():
     ap.add_argument("--Hkv", type=int, default=8)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--sdpa", action="store_true")
+    ap.add_argument("--noncausal", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
     B, S, Hq, Hkv, D = a.B, a.S, a.Hq, a.Hkv, a.D
     q = torch.randn(B, S, Hq, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, S, Hkv, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(B, S, Hkv, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    flops_f = 4 * B * Hq * S * S * D / 2
-    res = {"shape": [B, S, Hq, Hkv, D]}
-    o = F_.flash_attention(q, k, v)
+    causal = not a.noncausal
+    flops_f = 4 * B * Hq * S * S * D / (2 if causal else 1)
+    res = {"shape": [B, S, Hq, Hkv, D], "causal": causal}
+    o = F_.flash_attention(q, k, v, causal=causal)
     do = torch.randn_like(o)
-    tf = timeit(lambda: F_.flash_attention(q, k, v))
+    tf = timeit(lambda: F_.flash_attention(q, k, v, causal=causal))
     def fb():
-        o = F_.flash_attention(q, k, v)
+        o = F_.flash_attention(q, k, v, causal=causal)
         o.backward(do)
     tfb = timeit(fb)
     res["hip_fwd_ms"] = tf * 1e3

@@ -1,0 +1,70 @@
+"""Two rank processes on ONE MI355X over gloo (RCCL refuses two ranks on one GPU): ZeRO-2 and ZeRO-3 at
+dp 2 and TP+SP at tp 2 run the engine's and the TP layers' rank > 0 paths with the HIP kernels and real
+cross-rank data, and train like one process. (The 8-GPU RCCL run itself is the driver's scaling bench.)"""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _single(tmp_path):
+    from llm_training_amd.lms.clm import CLM
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+    from tests.multirank_gpu_common import CFG, batches
+    dev = torch.device("cuda", 0)
+    m = Llama(CFG, ParallelContext.single(dev), dtype=torch.bfloat16, device=dev)
+    m.init_weights(3)
+    full0 = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    torch.save(full0, tmp_path / "full0.pt")
+    eng = DataParallelEngine(m, ParallelContext.single(dev), 0, lr=1e-3, weight_decay=0.0)
+    lm = CLM({"model": None})
+    lm.model = m
+    lm.train()
+    losses = []
+    for ids in batches(dev):
+        eng.begin_step(1)
+        eng.zero_grad()
+        eng.begin_micro(0)
+        loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+        loss.backward()
+        eng.finish_backward()
+        eng.clip_and_scale(1.0)
+        eng.step(1e-3)
+        losses.append(loss.item())
+    eng.wait_params()
+    return losses, {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+
+
+@pytest.fixture(scope="module")
+def reference(tmp_path_factory):
+    d = tmp_path_factory.mktemp("mr")
+    losses, params = _single(d)
+    return d, losses, params
+
+
+@pytest.mark.parametrize("mode", ["dp2_z2", "dp2_z3", "tp2"])
+def test_two_ranks_on_one_gpu_match_single_process(reference, mode):
+    d, ref_losses, ref_params = reference
+    out = d / f"{mode}.pt"
+    env = dict(os.environ, FULL0=str(d / "full0.pt"), PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29600 + ["dp2_z2", "dp2_z3", "tp2"].index(mode)),
+           os.path.join(ROOT, "tests", "multirank_gpu_worker.py"), mode, str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-4000:]
+    got = torch.load(out, weights_only=True)
+    # dp: the mean of the two half-batch losses is the full-batch loss (equal token counts); bf16 kernels
+    for a, b in zip(got["losses"], ref_losses):
+        assert abs(a - b) < 2e-2 * abs(b), (mode, got["losses"], ref_losses)
+    num = den = 0.0
+    for k, v in ref_params.items():
+        num += (got["params"][k] - v).norm().item() ** 2
+        den += v.norm().item() ** 2
+    assert (num / den) ** 0.5 < 5e-3, mode
