@@ -67,6 +67,11 @@ def init_distributed(backend: str | None = None, timeout_minutes: float = 30.0, 
     rank, local, world = env_rank_info()
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    # test knobs: LLMT_DIST_BACKEND overrides the backend, LLMT_SHARED_DEVICE=1 puts every rank on GPU 0
+    # (several ranks on one GPU need gloo: RCCL refuses two ranks on one device)
+    backend = os.environ.get("LLMT_DIST_BACKEND") or backend
+    if os.environ.get("LLMT_SHARED_DEVICE") == "1":
+        local = 0
     if device_type == "cuda":
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)

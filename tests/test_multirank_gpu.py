@@ -68,3 +68,22 @@ def test_two_ranks_on_one_gpu_match_single_process(reference, mode):
         num += (got["params"][k] - v).norm().item() ** 2
         den += v.norm().item() ** 2
     assert (num / den) ** 0.5 < 5e-3, mode
+
+
+def test_bench_two_ranks_through_the_launcher(tmp_path):
+    """`bench.py --gpus 2` exactly as a user runs it (no torchrun): the in-process launcher starts two rank
+    processes, they train the ZeRO-2 engine on the GPU (both on GPU 0 over gloo here) and rank 0 prints
+    one JSON line with the whole-job tokens/s."""
+    import json
+    env = dict(os.environ, LLMT_DIST_BACKEND="gloo", LLMT_SHARED_DEVICE="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LLMT_LAUNCHED"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--layers", "2", "--seq", "1024", "--micro-batch", "1"],
+                       env=env, capture_output=True, text=True, timeout=150, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["zero_stage"] == 2
+    assert out["value"] > 0 and out["config"]["global_batch"] == 2
