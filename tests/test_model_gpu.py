@@ -298,26 +298,47 @@ def test_checkpoint_keep_attention_skips_the_attention_recompute():
 
 @pytest.mark.parametrize("model_type", ["llama", "phi3"])
 def test_hf_enable_liger_kernel_on_hip(model_type):
-    """enable_liger_kernel on the GPU: the patched transformers RMSNorm / MLP run the HIP RMSNorm and
-    SwiGLU kernels (bf16) and agree with the unpatched model to bf16 tolerance, forward and backward."""
-    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    """enable_liger_kernel on the GPU, module by module: each patched transformers RMSNorm / MLP instance
+    (HIP RMSNorm and SwiGLU kernels, bf16) against an unpatched copy of the same module on the same input,
+    forward and backward, to bf16 tolerance; and the whole patched model's loss against the unpatched one."""
+    import copy as _copy
+
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig, apply_fused_kernels
     hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 8, "num_key_value_heads": 4,
           "hidden_size": 512, "intermediate_size": 1024, "vocab_size": 1000, "max_position_embeddings": 512}
     if model_type == "phi3":
         hc.update(pad_token_id=0, bos_token_id=1, eos_token_id=2)
-    outs = []
-    for patch in (False, True):
-        m = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=patch), dtype=torch.bfloat16,
-                       device="cuda")
-        m.init_weights(0)
-        ids = torch.randint(0, 1000, (2, 256), device="cuda", generator=torch.Generator("cuda").manual_seed(1))
-        h = m.hidden_states(ids)
-        (h.float() ** 2).mean().backward()
-        outs.append((h.detach().float(), {n: p.grad.float() for n, p in m.named_parameters() if p.grad is not None}))
-    (h0, g0), (h1, g1) = outs
+    m = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc)), dtype=torch.bfloat16, device="cuda")
+    m.init_weights(0)
 
     def rel(a, b):
+        a, b = a.float(), b.float()
         return ((a - b).norm() / (b.norm() + 1e-12)).item()
-    assert rel(h1, h0) < 2e-2
-    for k in g0:
-        assert rel(g1[k], g0[k]) < 5e-2, k
+
+    layer = m.hf_model.model.layers[0]
+    for name in ("input_layernorm", "mlp"):
+        orig = getattr(layer, name)
+        patched = _copy.deepcopy(orig)
+        assert apply_fused_kernels(patched), name
+        x = torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        x2 = x.detach().clone().requires_grad_(True)
+        y0, y1 = orig(x), patched(x2)
+        g = torch.randn_like(y0)
+        y0.backward(g)
+        y1.backward(g)
+        assert rel(y1, y0) < 1e-2, name
+        assert rel(x2.grad, x.grad) < 2e-2, name
+        for (n0, p0), (_, p1) in zip(orig.named_parameters(), patched.named_parameters()):
+            assert rel(p1.grad, p0.grad) < 2e-2, (name, n0)
+    ids = torch.randint(0, 1000, (2, 256), device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+    from llm_training_amd.lms.clm import CLM
+    losses = []
+    for patch in (False, True):
+        mm = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=patch), dtype=torch.bfloat16,
+                        device="cuda")
+        mm.init_weights(0)
+        lm = CLM({"model": None})
+        lm.model = mm
+        with torch.no_grad():
+            losses.append(lm.training_step({"input_ids": ids, "labels": ids})[0].item())
+    assert abs(losses[1] - losses[0]) < 2e-2 * abs(losses[0]), losses
