@@ -11,9 +11,53 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def dpo_main(out):
+    """DPO at dp2 x ZeRO-3 with the gather-only dp-sharded reference model (parallel/frozen.py)."""
+    from llm_training_amd.lms.preference import DPO
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+    from tests.multirank_gpu_common import CFG, pref_batches
+    dev = torch.device("cuda", 0)
+    pc = ParallelContext.create("auto", 1, dev)
+    lm = DPO({"model": {"model_class": "llm_training.models.Llama", "model_config": CFG.model_dump()}, "beta": 0.1})
+    lm.configure_model(pc, dev, torch.bfloat16, seed=5)
+    eng = DataParallelEngine(lm.model, pc, 3, lr=1e-3, weight_decay=0.0)
+    lm.on_engine_ready(eng)
+    assert lm.ref_shards is not None
+    lm.train()
+    losses = []
+    for b in pref_batches(dev):
+        B = b["chosen_input_ids"].shape[0] // pc.dp_size
+        local = {k: v[pc.dp_rank * B:(pc.dp_rank + 1) * B] for k, v in b.items()}
+        eng.begin_step(1)
+        eng.zero_grad()
+        eng.begin_micro(0)
+        loss, _, _ = lm.training_step(local)
+        loss.backward()
+        eng.finish_backward()
+        eng.clip_and_scale(1.0)
+        eng.step(1e-3)
+        t = loss.detach().float().reshape(1)
+        dist.all_reduce(t)
+        losses.append(t.item() / dist.get_world_size())
+    held = sum(p.numel() for p in lm.ref_model.parameters())
+    with eng.full_params_context():
+        eng.wait_params()
+        sd = {k: v.detach().float().cpu() for k, v in lm.model.state_dict().items()}
+    torch.cuda.synchronize()
+    if dist.get_rank() == 0:
+        torch.save({"losses": losses, "params": sd, "ref_held": held,
+                    "ref_shard_bytes": lm.ref_shards.resident_bytes()}, out)
+    dist.barrier()
+
+
 def main():
-    mode, out = sys.argv[1], sys.argv[2]  # mode: dp2_z2 | dp2_z3 | tp2
+    mode, out = sys.argv[1], sys.argv[2]  # mode: dp2_z2 | dp2_z3 | tp2 | dpo_z3
     dist.init_process_group("gloo")
+    if mode == "dpo_z3":
+        dpo_main(out)
+        dist.destroy_process_group()
+        return
     from llm_training_amd.lms.clm import CLM
     from llm_training_amd.models.llama import Llama
     from llm_training_amd.parallel.context import ParallelContext

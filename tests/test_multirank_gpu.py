@@ -87,3 +87,48 @@ def test_bench_two_ranks_through_the_launcher(tmp_path):
     out = lines[0]
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["zero_stage"] == 2
     assert out["value"] > 0 and out["config"]["global_batch"] == 2
+
+
+def test_dpo_zero3_sharded_reference_two_ranks_on_one_gpu(tmp_path):
+    """DPO at dp2 x ZeRO-3 on the GPU: the frozen reference model is gather-only dp-sharded (half its
+    bytes per rank, nothing held between steps) and training matches one process on the full batch."""
+    from llm_training_amd.lms.preference import DPO
+    from llm_training_amd.parallel.context import ParallelContext
+    from llm_training_amd.parallel.engine import DataParallelEngine
+    from tests.multirank_gpu_common import CFG, pref_batches
+    dev = torch.device("cuda", 0)
+    lm = DPO({"model": {"model_class": "llm_training.models.Llama", "model_config": CFG.model_dump()}, "beta": 0.1})
+    lm.configure_model(ParallelContext.single(dev), dev, torch.bfloat16, seed=5)
+    full_ref = sum(p.numel() * p.element_size() for p in lm.ref_model.parameters())
+    eng = DataParallelEngine(lm.model, ParallelContext.single(dev), 0, lr=1e-3, weight_decay=0.0)
+    lm.on_engine_ready(eng)
+    lm.train()
+    ref_losses = []
+    for b in pref_batches(dev):
+        eng.begin_step(1)
+        eng.zero_grad()
+        eng.begin_micro(0)
+        loss, _, _ = lm.training_step(b)
+        loss.backward()
+        eng.finish_backward()
+        eng.clip_and_scale(1.0)
+        eng.step(1e-3)
+        ref_losses.append(loss.item())
+    eng.wait_params()
+    ref_params = {k: v.detach().float().cpu() for k, v in lm.model.state_dict().items()}
+    out = tmp_path / "dpo.pt"
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29614",
+           os.path.join(ROOT, "tests", "multirank_gpu_worker.py"), "dpo_z3", str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-4000:]
+    got = torch.load(out, weights_only=True)
+    assert got["ref_held"] == 0 and got["ref_shard_bytes"] <= full_ref / 2 * 1.05
+    for a, b in zip(got["losses"], ref_losses):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (got["losses"], ref_losses)
+    num = den = 0.0
+    for k, v in ref_params.items():
+        num += (got["params"][k] - v).norm().item() ** 2
+        den += v.norm().item() ** 2
+    assert (num / den) ** 0.5 < 5e-3
