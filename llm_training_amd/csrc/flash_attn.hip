@@ -1300,7 +1300,31 @@ __device__ __forceinline__ float vadd(float a, float b) {
   return r;
 }
 
-template <int D, int RS = 0>
+// Widened row-per-lane store tail (cdna guide T21). w[g] holds this lane's 4 bf16 of 8-column group g
+// of its row: the lower lane half columns 8g..8g+3, the upper half 8g+4..8g+7. One permlane32_swap per
+// dword of each group pair (g, g+1) leaves the lower half 16 contiguous bytes of group g and the upper
+// half those of group g+1, so a lane issues NG / 2 dwordx4 stores instead of NG dwordx2. Run on every
+// lane (a pair's two halves share one row), store where the row exists.
+template <int NG>
+__device__ __forceinline__ void widen_pairs(uint2 (&w)[NG]) {
+#pragma unroll
+  for (int g = 0; g < NG; g += 2) {
+    const auto sx = __builtin_amdgcn_permlane32_swap(w[g].x, w[g + 1].x, false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(w[g].y, w[g + 1].y, false, false);
+    w[g].x = sx[0];
+    w[g + 1].x = sx[1];
+    w[g].y = sy[0];
+    w[g + 1].y = sy[1];
+  }
+}
+// row = the row's first element + 8 * (lane >> 5) (16-byte aligned)
+template <int NG>
+__device__ __forceinline__ void store_pairs(bf16* row, const uint2 (&w)[NG]) {
+#pragma unroll
+  for (int g = 0; g < NG; g += 2) *reinterpret_cast<uint4*>(row + 8 * g) = make_uint4(w[g].x, w[g].y, w[g + 1].x, w[g + 1].y);
+}
+
+template <int D, int RS = 0, int WS = 0>
 __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;  // k-steps of a D-deep product, 32-wide output tiles
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
@@ -1487,17 +1511,31 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (qrow < S) {
-    bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
+  if constexpr (WS) {
+    uint2 w[4 * NDT];
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        uint2 w;
-        w.x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
-        w.y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
-        *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
+        w[4 * dt + c].x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
+        w[4 * dt + c].y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
       }
+    widen_pairs(w);
+    if (qrow < S) store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
+  }
+  if (qrow < S) {
+    if constexpr (!WS) {
+      bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          uint2 w;
+          w.x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
+          w.y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
+          *reinterpret_cast<uint2*>(op + dt * 32 + 8 * c + 4 * hh) = w;
+        }
+    }
     if (hh == 0) {
       const float mu = (m == -INFINITY) ? 0.f : m;
       a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (mu + __log2f(lt)) * kLn2 : -INFINITY;
@@ -1511,7 +1549,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
 // V row reads -> dP^T = V.dO^T, dS = P (dP - delta) with P = exp2(S * scale * log2e - lse * log2e)
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
 // dQ = scale * sum; the row constants come straight from lse / delta (delta written by the prep kernel).
-template <int D, bool IL = true>
+template <int D, bool IL = true, bool WS = false>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
@@ -1678,7 +1716,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
     }
   }
 
-  if (qrow < S) {
+  if constexpr (WS) {
+    uint2 w[4 * NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        w[4 * dt + c].x = pack_bf16x2(dqt[dt][4 * c] * a.scale, dqt[dt][4 * c + 1] * a.scale);
+        w[4 * dt + c].y = pack_bf16x2(dqt[dt][4 * c + 2] * a.scale, dqt[dt][4 * c + 3] * a.scale);
+      }
+    widen_pairs(w);
+    if (qrow < S) store_pairs(a.out + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * a.dq_sh + 8 * hh, w);
+  } else if (qrow < S) {
     bf16* dqp = a.out + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * a.dq_sh;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
@@ -1758,27 +1807,32 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   // removed one-wave-per-SIMD ring forward 1.043; 3 = fwd3 with compiler-placed row-sum adds, 2 = with the
   // inline-asm adds (A/B reference); read per launch
   const char* fve = getenv("LLMT_FA_FWD_VARIANT");
-  const int variant = fve ? atoi(fve) : 3;  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
+  // 4 = 3 with the widened O store tail (T21), in one process: B4 S8192 2.199 vs 2.203 ms, B32 S1024 0.429
+  // vs 0.458, B64 S512 0.314 vs 0.343 ms (the per-block cost of short sequences / packed documents),
+  // bitwise-equal output (profiles/r3_attention_wide_store_ab.jsonl)
+  const int variant = fve ? atoi(fve) : 4;  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
   switch (D) {
     case 64:  // the v3 structure on 128-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a);
       else
-        fa_fwd3_kernel<64, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<64, 1, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       break;
     case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a);
       else
-        fa_fwd3_kernel<96, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<96, 1, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       break;
     case 128: {
       if (a.drop_thresh)  // dropout lives in the generic kernels
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
       else if (variant == 2)  // row sums through the inline-asm add (each behind its own wait state)
         fa_fwd3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else if (variant == 3)
+      else if (variant == 3)  // dwordx2 O store tail (A/B reference)
         fa_fwd3_kernel<128, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else if (variant == 4)
+        fa_fwd3_kernel<128, 1, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
     } break;
@@ -1842,7 +1896,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     const int64_t nT = (S + 31) / 32;
     if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
       fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
-      fa_bwd_dq3_kernel<96><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       if (dkdv_variant() == 3)
         fa_bwd_dkdv128_kernel<3, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
@@ -1851,7 +1905,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     }
     if (D == 64) {
       fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
-      fa_bwd_dq3_kernel<64><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       if (dkdv_variant() == 3)
         fa_bwd_dkdv128_kernel<3, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
@@ -1863,12 +1917,17 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     // kernel (removed, like the 8-wave role-split dK/dV kernel: 10.81 vs 9.89 ms, and the ring forward)
     {
       // LLMT_FA_DQ_VARIANT=0: V reads after the whole S^T chain (A/B reference, read per launch); the
-      // default interleaves them: B4 S8192 backward 8.00 -> 7.93 ms in one process, same gradients
+      // default interleaves them: B4 S8192 backward 8.00 -> 7.93 ms in one process, same gradients.
+      // 1 = the dwordx2 dQ store tail; the default (2) widens it (T21): B32 S1024 backward 1.541 ->
+      // 1.522 ms, B4 S8192 unchanged, same gradients
       const char* dqe = getenv("LLMT_FA_DQ_VARIANT");
-      if (dqe && atoi(dqe) == 0)
+      const int dqv = dqe ? atoi(dqe) : 2;
+      if (dqv == 0)
         fa_bwd_dq3_kernel<128, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else
+      else if (dqv == 1)
         fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else
+        fa_bwd_dq3_kernel<128, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     }
     const int variant = dkdv_variant();
     if (variant == 3)
