@@ -45,6 +45,8 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
                                int seg_runs, float drop_p, uint32_t drop_seed, hipStream_t stream);
 hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N, int K,
                      int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream);
+hipError_t llmt_gemm_splitk(const void* x, const void* y, float* slabs, int x_mn, int y_mn, int M, int N, int K,
+                            int64_t ldx, int64_t ldy, int64_t ldc, int nsplit, hipStream_t stream);
 int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D);
 hipError_t llmt_quant_int8(const void* x, int x_fp32, int8_t* q, float* scale, int64_t n, hipStream_t stream);
 hipError_t llmt_dequant_int8(const int8_t* q, const float* scale, void* y, int64_t n, hipStream_t stream);
@@ -399,6 +401,31 @@ void gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool a_mn, bo
         "gemm");
 }
 
+// slabs [nsplit, M, N] fp32 (contiguous): slab s = a . b^T over contraction slice s (layouts as gemm_)
+void gemm_splitk_(const at::Tensor& a, const at::Tensor& b, at::Tensor slabs, bool a_mn, bool b_mn) {
+  check_bf16_cuda(a, "a");
+  check_bf16_cuda(b, "b");
+  TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == at::kFloat && slabs.dim() == 3 && slabs.is_contiguous(),
+              "gemm_splitk: slabs must be a contiguous fp32 [nsplit, M, N] GPU tensor");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm_splitk: 2-D operands with unit column stride");
+  const int64_t M = a_mn ? a.size(1) : a.size(0), K = a_mn ? a.size(0) : a.size(1);
+  const int64_t N = b_mn ? b.size(1) : b.size(0), Kb = b_mn ? b.size(0) : b.size(1);
+  const int64_t ns = slabs.size(0);
+  TORCH_CHECK(K == Kb && (b_mn || !a_mn), "gemm_splitk: contraction sizes / layouts");
+  TORCH_CHECK(slabs.size(1) == M && slabs.size(2) == N, "gemm_splitk: slabs must be [nsplit, ", M, ", ", N, "]");
+  TORCH_CHECK(ns >= 1 && K % (32 * ns) == 0 && N % 4 == 0, "gemm_splitk: K must be a multiple of 32 * nsplit, N of 4");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm_splitk: dimension too large");
+  const int64_t lda = row_ld(a), ldb = row_ld(b);
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm_splitk: leading dimensions must be 16-byte multiples");
+  TORCH_CHECK(256 * lda * 2 < 0x7fffffffLL && 256 * ldb * 2 < 0x7fffffffLL, "gemm_splitk: leading dimension too large");
+  for (const at::Tensor* t : {&a, &b, static_cast<const at::Tensor*>(&slabs)})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "gemm_splitk: operands must be 16-byte aligned");
+  if (M == 0 || N == 0) return;
+  check(llmt_gemm_splitk(a.data_ptr(), b.data_ptr(), slabs.data_ptr<float>(), a_mn ? 1 : 0, b_mn ? 1 : 0, (int)M,
+                         (int)N, (int)K, lda, ldb, N, (int)ns, cur_stream()),
+        "gemm_splitk");
+}
+
 // ---------------------------------------------------------------- flash attention
 // q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (any batch/seq/head strides, unit stride on D).
 // seg: optional int32 segment ids (0 = padding): attention is restricted to the token's contiguous run of
@@ -500,6 +527,7 @@ TORCH_LIBRARY(llmt, m) {
   m.def("dequant_int8_(Tensor q, Tensor scale, Tensor(a!) y) -> ()");
   m.def("dequant_sum_(Tensor q, Tensor scale, Tensor(a!) out, int k, bool accumulate) -> ()");
   m.def("gemm_(Tensor a, Tensor b, Tensor(a!) c, bool a_mn, bool b_mn, bool accumulate) -> ()");
+  m.def("gemm_splitk_(Tensor a, Tensor b, Tensor(a!) slabs, bool a_mn, bool b_mn) -> ()");
   m.def(
       "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window, "
       "float dropout_p=0., int seed=0) -> (Tensor, Tensor)");
@@ -524,6 +552,7 @@ TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("dequant_int8_", &dequant_int8_);
   m.impl("dequant_sum_", &dequant_sum_);
   m.impl("gemm_", &gemm_);
+  m.impl("gemm_splitk_", &gemm_splitk_);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
 }

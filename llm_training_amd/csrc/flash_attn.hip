@@ -962,12 +962,36 @@ __device__ __forceinline__ void ring_barrier() { asm volatile("s_waitcnt lgkmcnt
 // flight are the prefetched rows of a slot the next DMA does not touch
 __device__ __forceinline__ void ring_barrier_nodrain() { asm volatile("s_barrier" ::: "memory"); }
 
+// Widened row-per-lane store tail (cdna guide T21). w[g] holds this lane's 4 bf16 of 8-column group g
+// of its row: the lower lane half columns 8g..8g+3, the upper half 8g+4..8g+7. One permlane32_swap per
+// dword of each group pair (g, g+1) leaves the lower half 16 contiguous bytes of group g and the upper
+// half those of group g+1, so a lane issues NG / 2 dwordx4 stores instead of NG dwordx2. Run on every
+// lane (a pair's two halves share one row), store where the row exists.
+template <int NG>
+__device__ __forceinline__ void widen_pairs(uint2 (&w)[NG]) {
+#pragma unroll
+  for (int g = 0; g < NG; g += 2) {
+    const auto sx = __builtin_amdgcn_permlane32_swap(w[g].x, w[g + 1].x, false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(w[g].y, w[g + 1].y, false, false);
+    w[g].x = sx[0];
+    w[g + 1].x = sx[1];
+    w[g].y = sy[0];
+    w[g + 1].y = sy[1];
+  }
+}
+// row = the row's first element + 8 * (lane >> 5) (16-byte aligned)
+template <int NG>
+__device__ __forceinline__ void store_pairs(bf16* row, const uint2 (&w)[NG]) {
+#pragma unroll
+  for (int g = 0; g < NG; g += 2) *reinterpret_cast<uint4*>(row + 8 * g) = make_uint4(w[g].x, w[g].y, w[g + 1].x, w[g + 1].y);
+}
+
 // grid: ceil(S/128) * Hkv * B blocks (1-D), 4 waves x 32 keys; query tiles of 32 rows over all q heads of
 // the kv group; NS-slot LDS-DMA ring.
 // D = 96 (Phi-3) runs the same structure on 256-byte LDS rows: the DMA rows read 64 bytes past each
 // 192-byte row (never past the tensor: the descriptors end at the last row's D elements) and only the
 // first D / 16 k-steps / D / 32 output tiles are used.
-template <int V, int D = 128>
+template <int V, int D = 128, bool WS = false>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, const float* ld) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
@@ -1252,7 +1276,25 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
     wait_vm<0>();  // no LDS-DMA may outlive the workgroup
   }
 
-  if (kr < S) {
+  if constexpr (WS) {  // widened store tail (widen_pairs): 16-byte stores of dK / dV rows
+    uint2 wk[4 * NDT], wv[4 * NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int g = 4 * dt + c;
+        wk[g].x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
+        wk[g].y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
+        wv[g].x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
+        wv[g].y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
+      }
+    widen_pairs(wk);
+    widen_pairs(wv);
+    if (kr < S) {
+      store_pairs(a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh + 8 * hh, wk);
+      store_pairs(a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh + 8 * hh, wv);
+    }
+  } else if (kr < S) {
     bf16* dkp = a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh;
     bf16* dvp = a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh;
 #pragma unroll
@@ -1298,30 +1340,6 @@ __device__ __forceinline__ float vadd(float a, float b) {
   float r;
   asm("s_nop 0\n\tv_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
-}
-
-// Widened row-per-lane store tail (cdna guide T21). w[g] holds this lane's 4 bf16 of 8-column group g
-// of its row: the lower lane half columns 8g..8g+3, the upper half 8g+4..8g+7. One permlane32_swap per
-// dword of each group pair (g, g+1) leaves the lower half 16 contiguous bytes of group g and the upper
-// half those of group g+1, so a lane issues NG / 2 dwordx4 stores instead of NG dwordx2. Run on every
-// lane (a pair's two halves share one row), store where the row exists.
-template <int NG>
-__device__ __forceinline__ void widen_pairs(uint2 (&w)[NG]) {
-#pragma unroll
-  for (int g = 0; g < NG; g += 2) {
-    const auto sx = __builtin_amdgcn_permlane32_swap(w[g].x, w[g + 1].x, false, false);
-    const auto sy = __builtin_amdgcn_permlane32_swap(w[g].y, w[g + 1].y, false, false);
-    w[g].x = sx[0];
-    w[g + 1].x = sx[1];
-    w[g].y = sy[0];
-    w[g + 1].y = sy[1];
-  }
-}
-// row = the row's first element + 8 * (lane >> 5) (16-byte aligned)
-template <int NG>
-__device__ __forceinline__ void store_pairs(bf16* row, const uint2 (&w)[NG]) {
-#pragma unroll
-  for (int g = 0; g < NG; g += 2) *reinterpret_cast<uint4*>(row + 8 * g) = make_uint4(w[g].x, w[g].y, w[g + 1].x, w[g + 1].y);
 }
 
 template <int D, int RS = 0, int WS = 0>
@@ -1751,7 +1769,9 @@ using namespace llmt;
 //   sched-group pinned schedule of the same loop measured 9.17 vs 8.12 ms at B4 S8192 and was removed.)
 static int dkdv_variant() {
   const char* e = getenv("LLMT_FA_BWD_VARIANT");
-  return e ? atoi(e) : 3;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
+  // 4 = 3 with the widened dK / dV store tail: B32 S1024 1.496 -> 1.476 ms, B64 S512 1.058 -> 1.029 ms,
+  // S8192 unchanged, bitwise-equal gradients (profiles/r3_attention_wide_store_ab.jsonl)
+  return e ? atoi(e) : 4;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
 }
 
 static void set_dropout(AttnArgs& a, float p, uint32_t seed) {
@@ -1897,8 +1917,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
       fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      if (dkdv_variant() == 3)
-        fa_bwd_dkdv128_kernel<3, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      if (dkdv_variant() >= 3)
+        fa_bwd_dkdv128_kernel<3, 96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
         fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       return hipGetLastError();
@@ -1906,8 +1926,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     if (D == 64) {
       fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      if (dkdv_variant() == 3)
-        fa_bwd_dkdv128_kernel<3, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      if (dkdv_variant() >= 3)
+        fa_bwd_dkdv128_kernel<3, 64, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
         fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       return hipGetLastError();
@@ -1932,6 +1952,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     const int variant = dkdv_variant();
     if (variant == 3)
       fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 4)
+      fa_bwd_dkdv128_kernel<3, 128, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else
       fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     return hipGetLastError();

@@ -7,11 +7,13 @@
 //   dgrad    dx = dy . W    : X = dy [T, N]  K-major,   Y = W [N, K]   MN-major (contraction = W's rows)
 //   wgrad    dW = dy^T . x  : X = dy [T, N]  MN-major,  Y = x [T, K]   MN-major (contraction = tokens)
 //
-// The projections and the lm_head of the models are these GEMMs. hipBLASLt's default
-// solutions reach 1.0 (forward), 1.37 (dgrad) and 1.5 (wgrad) PF/s on the Llama-3-8B shapes
-// (profiles/r1_llama8b_1gpu_v2_kernel_stats.md, profiles/r1_gemm_layouts_random_data.jsonl).
+// The projections and the lm_head of the models are these GEMMs. Two kernels: the
+// two-group ping-pong kernel (gemm_pp_kernel, default; 1.23-1.28 PF/s on the Llama-3-8B shapes at 32768
+// tokens) and the single-group ring kernel below (LLMT_GEMM_KERNEL=ring; 1.10-1.16). hipBLASLt reaches
+// 1.41-1.61 on the forward layout, so the framework uses these only as timed weight-gradient candidates
+// (profiles/r3_gemm_pingpong.md).
 //
-// Structure (one 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N), 256 x 256 output tile):
+// Ring kernel structure (one 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N), 256 x 256 output tile):
 //  * K advances in 32-deep stages. Each stage's X and Y tiles (16 KB each) arrive by LDS-DMA
 //    (`buffer_load_dwordx4 ... lds`, one 1-KB piece per wave-instruction) into a ring of kNS LDS slots,
 //    kNS-1 stages ahead of the MFMAs, behind a counted `s_waitcnt vmcnt` and ONE raw barrier per stage:
@@ -35,6 +37,8 @@
 //    window must fit 32 bits; reads past the end of an operand come back as zeros (descriptor range
 //    check). K must be a multiple of 32; rows / columns past M / N are computed on padding and not stored.
 #include "common.h"
+
+#include <cstring>
 
 namespace llmt {
 namespace {
@@ -361,6 +365,159 @@ hipError_t launch(const GemmArgs& a, int out_mode, hipStream_t stream) {
   return gemm_waves() == 8 ? launch_nw<XMN, YMN, 8>(a, out_mode, stream) : launch_nw<XMN, YMN, 4>(a, out_mode, stream);
 }
 
+// ---------------------------------------------------------------- ping-pong kernel
+// The same tile (256 x 256, 8 waves as 2 (M) x 4 (N), wave tile 128 x 64, 32-deep stages in a ring of NS
+// 32-KB LDS slots filled by LDS-DMA) with the waves split into two groups that alternate roles between
+// barriers (cdna guide §5 'The 256² 8-phase template', MI355X_MICROARCH 'Two waves per SIMD'): waves 0-3
+// (output rows 0..127) and waves 4-7 (rows 128..255) share each SIMD pairwise, and while one group runs
+// its 32 MFMAs of a stage the other reads its fragments of the stage from LDS and issues its share of the
+// DMA NS-1 stages ahead (group 0 fetches the X image, group 1 the Y image: 4 one-KB pieces per wave per
+// stage). Group 1 starts one barrier late, so every interval between two barriers pairs one group's
+// matrix work with the other group's LDS / DMA work on every SIMD.
+// Ordering (per wave, stage j): [read fragments of j; DMA of stage j+NS-1 into the slot of stage j-1;
+// vmcnt(4 (NS-2)) -> this wave's pieces of stage j+1 have landed; lgkmcnt(0); barrier] [32 MFMAs;
+// barrier]. A slot is rewritten only after both groups' reads of it retired before an earlier barrier, and
+// a stage is read only after every wave's pieces of it were waited for before an earlier barrier. DMAs
+// past the last stage read an empty descriptor range (zeros into slots no one reads) so the wait counts
+// stay constant. Split-K: blockIdx.y selects a contiguous slice of the stages, written as an fp32 slab.
+template <bool XMN, bool YMN, int OUT, int NS>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g, int nk, int64_t slab) {
+  constexpr int AH = NS - 1;  // stages in flight ahead of the one being read
+  __shared__ __attribute__((aligned(16))) char smem[NS * kSlot];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2, wq = w & 3;
+  int tm, tn;
+  tile_coords(g.M, g.N, tm, tn);
+  const int row0 = tm * kBM, col0 = tn * kBN;
+  const int64_t k0 = (int64_t)blockIdx.y * nk * kBK;  // first contraction index of this split
+
+  Opnd<XMN, 4> X;
+  Opnd<YMN, 4> Y;
+  if constexpr (!XMN)
+    X.init(g.x + k0, g.ldx, g.M, g.K - k0, row0, wq, lane);
+  else
+    X.init(g.x + k0 * g.ldx, g.ldx, g.K - k0, g.M, row0, wq, lane);
+  if constexpr (!YMN)
+    Y.init(g.y + k0, g.ldy, g.N, g.K - k0, col0, wq, lane);
+  else
+    Y.init(g.y + k0 * g.ldy, g.ldy, g.K - k0, g.N, col0, wq, lane);
+  const uint32_t lbase = g_lds(smem);
+
+  auto issue = [&](int t, int slot) {
+    const uint32_t sb = lbase + (uint32_t)(slot * kSlot);
+    if (grp == 0) {
+      const GRsrc r = X.rsrc(t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g_dma16(r, sb + (wq + 4 * i) * 1024, X.off[i]);
+    } else {
+      const GRsrc r = Y.rsrc(t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g_dma16(r, sb + kImg + (wq + 4 * i) * 1024, Y.off[i]);
+    }
+  };
+
+  gbf8 fy[4], fx[8];
+  gf4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = gf4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < AH; ++t) issue(t, t);
+  g_wait_vm<4 * (AH - 1)>();
+  g_barrier();
+  if (grp == 1) g_barrier();  // the stagger: group 1 runs one interval behind
+
+  int slot = 0, islot = AH;
+  for (int j = 0; j < nk; ++j) {
+    // ---- load segment: fragments of stage j, DMA of stage j + AH
+    const char* img = smem + slot * kSlot;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) fy[jj] = Y.frag(img + kImg, wq * 64 + jj * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fx[i] = X.frag(img, grp * 128 + i * 16, lane);
+    issue(j + AH, islot);
+    g_wait_vm<4 * (AH - 1)>();
+    g_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- compute segment
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fy[jj], fx[i], acc[i][jj], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    g_barrier();
+    slot = slot + 1 == NS ? 0 : slot + 1;
+    islot = islot + 1 == NS ? 0 : islot + 1;
+  }
+  if (grp == 0) g_barrier();  // equal barrier counts in both groups
+  g_wait_vm<0>();             // no LDS-DMA outlives the workgroup
+
+  const int fr = lane & 15, fc = lane >> 4;
+  char* cbase = reinterpret_cast<char*>(g.c) + (int64_t)blockIdx.y * slab * (OUT == 0 || OUT == 3 ? 2 : 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = row0 + grp * 128 + i * 16 + fr;
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int n = col0 + wq * 64 + jj * 16 + fc * 4;
+      if (n >= g.N) continue;
+      const gf4 v = acc[i][jj];
+      if constexpr (OUT == 0 || OUT == 3) {
+        uint2* p = reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(cbase) + (int64_t)m * g.ldc + n);
+        float a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+        if constexpr (OUT == 3) {
+          const uint2 o = *p;
+          a0 += bf16_lo(o.x);
+          a1 += bf16_hi(o.x);
+          a2 += bf16_lo(o.y);
+          a3 += bf16_hi(o.y);
+        }
+        uint2 o;
+        o.x = pack_bf16x2(a0, a1);
+        o.y = pack_bf16x2(a2, a3);
+        *p = o;
+      } else {
+        float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(cbase) + (int64_t)m * g.ldc + n);
+        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+        if constexpr (OUT == 2) {
+          const float4 c = *p;
+          o.x += c.x;
+          o.y += c.y;
+          o.z += c.z;
+          o.w += c.w;
+        }
+        *p = o;
+      }
+    }
+  }
+}
+
+template <bool XMN, bool YMN>
+hipError_t launch_pp(const GemmArgs& a, int out_mode, int ksplit, int64_t slab, hipStream_t stream) {
+  const int64_t nwg = (int64_t)((a.M + kBM - 1) / kBM) * ((a.N + kBN - 1) / kBN);
+  const int nk = a.K / kBK / ksplit;
+  const dim3 grid((unsigned)nwg, (unsigned)ksplit), block(512);
+  switch (out_mode) {
+    case 0: gemm_pp_kernel<XMN, YMN, 0, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
+    case 1: gemm_pp_kernel<XMN, YMN, 1, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
+    case 2: gemm_pp_kernel<XMN, YMN, 2, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
+    default: gemm_pp_kernel<XMN, YMN, 3, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
+  }
+  return hipGetLastError();
+}
+
+// LLMT_GEMM_KERNEL=ring selects the single-group ring kernel above (read per call, for A/B runs)
+inline bool use_pp() {
+  const char* e = getenv("LLMT_GEMM_KERNEL");
+  return !(e && strcmp(e, "ring") == 0);
+}
+
 }  // namespace
 }  // namespace llmt
 
@@ -375,8 +532,32 @@ extern "C" hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn,
   if (ldx % 8 || ldy % 8 || ldc % 4) return hipErrorInvalidValue;
   if (256 * ldx * 2 >= 0x7fffffffLL || 256 * ldy * 2 >= 0x7fffffffLL) return hipErrorInvalidValue;
   GemmArgs a{reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(y), c, M, N, K, ldx, ldy, ldc};
+  if (use_pp()) {
+    if (!x_mn && !y_mn) return launch_pp<false, false>(a, out_mode, 1, 0, stream);
+    if (!x_mn && y_mn) return launch_pp<false, true>(a, out_mode, 1, 0, stream);
+    if (x_mn && y_mn) return launch_pp<true, true>(a, out_mode, 1, 0, stream);
+    return hipErrorInvalidValue;
+  }
   if (!x_mn && !y_mn) return launch<false, false>(a, out_mode, stream);
   if (!x_mn && y_mn) return launch<false, true>(a, out_mode, stream);
   if (x_mn && y_mn) return launch<true, true>(a, out_mode, stream);
   return hipErrorInvalidValue;  // X MN-major with Y K-major: no linear-layer GEMM has this layout
+}
+
+// Split-K form of the ping-pong kernel: slabs[s] (fp32 [M, N], row stride ldc, slab stride M * ldc) gets
+// X . Y^T over contraction slice s of nsplit equal slices (summed by llmt_splitk_reduce). K must be a
+// multiple of 32 * nsplit.
+extern "C" hipError_t llmt_gemm_splitk(const void* x, const void* y, float* slabs, int x_mn, int y_mn, int M, int N,
+                                       int K, int64_t ldx, int64_t ldy, int64_t ldc, int nsplit, hipStream_t stream) {
+  using namespace llmt;
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (nsplit < 1 || K <= 0 || K % (kBK * nsplit) != 0 || N % 4 != 0) return hipErrorInvalidValue;
+  if (ldx % 8 || ldy % 8 || ldc % 4) return hipErrorInvalidValue;
+  if (256 * ldx * 2 >= 0x7fffffffLL || 256 * ldy * 2 >= 0x7fffffffLL) return hipErrorInvalidValue;
+  GemmArgs a{reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(y), slabs, M, N, K, ldx, ldy, ldc};
+  const int64_t slab = (int64_t)M * ldc;
+  if (!x_mn && !y_mn) return launch_pp<false, false>(a, 1, nsplit, slab, stream);
+  if (!x_mn && y_mn) return launch_pp<false, true>(a, 1, nsplit, slab, stream);
+  if (x_mn && y_mn) return launch_pp<true, true>(a, 1, nsplit, slab, stream);
+  return hipErrorInvalidValue;
 }

@@ -97,6 +97,8 @@ _LAYOUT_CACHE: dict[tuple, str] = {}
 # largest weight-gradient output (elements) offered the split-K candidates (fp32 slabs: 8 bytes / element)
 _SPLITK_MAX_OUT = int(os.environ.get("LLMT_WGRAD_SPLITK_MAX", str(1 << 26)))
 _SPLITK = (2, 4)  # contraction splits offered (slabs: n_split x N x K fp32)
+# offer the hand-written GEMM (direct and split-K) among the timed weight-gradient candidates
+_OWN_WGRAD = os.environ.get("LLMT_GEMM_OWN", "1").strip().lower() not in ("0", "false", "off")
 
 
 def _tr_ok(*ts: torch.Tensor) -> bool:
@@ -254,6 +256,18 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
                 variants[f"nt{ns}"] = _split(x, dy, False, True, _ld(x), _ld(dy), ns)
                 variants[f"tt{ns}"] = _split(lambda: transpose(x), dy, True, True, M, _ld(dy), ns)
                 variants[f"nn{ns}"] = _split(x, lambda: transpose(dy), False, False, _ld(x), M, ns)
+        if _OWN_WGRAD and M % 32 == 0 and N % 4 == 0:
+            # the hand-written ping-pong GEMM (csrc/gemm.hip) reads both token-major operands directly
+            # (transposed LDS reads, no materialised transposes); split into 2 / 4 contraction slices for
+            # outputs that fill the chip in few 256 x 256 tiles
+            variants["hip"] = lambda: lib().gemm_(dy, x, o2, True, True, accumulate)
+            for ns in _SPLITK:
+                if N * K <= _SPLITK_MAX_OUT and M % (32 * ns) == 0:
+                    def _own_split(ns=ns):
+                        slabs = torch.empty(ns, N, K, device=out.device, dtype=torch.float32)
+                        lib().gemm_splitk_(dy, x, slabs, True, True)
+                        lib().splitk_reduce_(slabs, o2, accumulate)
+                    variants[f"hip{ns}"] = _own_split
         # static rule: wide outputs (gate_up, lm_head) transpose the smaller operand x, the rest dy
         default = "tt" if N >= 4 * K else "nn"
         key = ("wgrad", M, N, K, _ld(x), _ld(dy), out.dtype, sk)

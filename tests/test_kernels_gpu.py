@@ -343,11 +343,14 @@ def test_rope_attention_fused_matches_reference():
 
 
 # ----------------------------------------------------------------------------- GEMM (csrc/gemm.hip)
+@pytest.mark.parametrize("kernel", ["pp", "ring"])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("out", ["bf16", "bf16_acc", "fp32", "fp32_acc"])
 @pytest.mark.parametrize("M,N,K", [(520, 776, 352), (64, 128, 32), (8, 264, 96), (1024, 512, 4096)])
-def test_gemm_layouts(layout, out, M, N, K):
-    # nt = forward (x . W^T), nn = dgrad (dy . W), tn = wgrad (dy^T . x); partial tiles on every edge
+def test_gemm_layouts(layout, out, M, N, K, kernel, monkeypatch):
+    # nt = forward (x . W^T), nn = dgrad (dy . W), tn = wgrad (dy^T . x); partial tiles on every edge.
+    # pp = the two-group ping-pong kernel (default), ring = the single-group ring kernel
+    monkeypatch.setenv("LLMT_GEMM_KERNEL", kernel)
     torch.manual_seed(0)
     xb = torch.randn(M, K, device=DEV).bfloat16()
     yb = torch.randn(N, K, device=DEV).bfloat16()
@@ -360,6 +363,26 @@ def test_gemm_layouts(layout, out, M, N, K):
     lib().gemm_(a, b, c, layout == "tn", layout != "nt", acc)
     want = xb.float() @ yb.float().t() + (c0.float() if acc else 0.0)
     assert _rel(c, want) < (1e-4 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("M,N,K,ns", [(520, 776, 384, 2), (304, 1032, 4096, 4), (64, 128, 256, 4)])
+def test_gemm_splitk(layout, M, N, K, ns):
+    # fp32 slabs of the contraction slices (the weight-gradient split-K candidate) sum to the product
+    torch.manual_seed(0)
+    xb = torch.randn(M, K, device=DEV).bfloat16()
+    yb = torch.randn(N, K, device=DEV).bfloat16()
+    a = xb.t().contiguous() if layout == "tn" else xb
+    b = yb if layout == "nt" else yb.t().contiguous()
+    slabs = torch.full((ns, M, N), float("nan"), device=DEV)
+    lib().gemm_splitk_(a, b, slabs, layout == "tn", layout != "nt")
+    k = K // ns
+    for s in range(ns):  # each slab holds exactly its own slice
+        want = xb[:, s * k:(s + 1) * k].float() @ yb[:, s * k:(s + 1) * k].float().t()
+        assert _rel(slabs[s], want) < 1e-4
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    lib().splitk_reduce_(slabs, out, False)
+    assert _rel(out, xb.float() @ yb.float().t()) < 1e-2
 
 
 def test_gemm_strided_operands():
