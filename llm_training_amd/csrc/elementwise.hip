@@ -11,6 +11,8 @@
 // Backward is the same kernel with the rotation negated (rotate by -theta).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace llmt {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
@@ -50,6 +52,43 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16x8* __restric
     dgu[t * 2 * I8 + j] = pack8(da);
     dgu[t * 2 * I8 + I8 + j] = pack8(db);
   }
+}
+
+// Row-blocked forms (default): grid (ceil(I8 / 256), T), one 16-byte group per thread, no grid-stride loop
+// and no 64-bit index division (the flat grid-stride forms above divide a 64-bit element index by I8 per
+// item). T = 32768, I = 14336: forward 0.563 -> 0.496 ms (5.0 -> 5.7 TB/s), backward 0.962 -> 0.857 ms,
+// bitwise-equal outputs (profiles/r3_elementwise_kernels.jsonl)
+__global__ __launch_bounds__(256) void swiglu_fwd_rows_kernel(const bf16x8* __restrict__ gu, bf16x8* __restrict__ c,
+                                                              int I8) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= I8) return;
+  const int64_t t = blockIdx.y;
+  float a[8], b[8], o[8];
+  unpack8(gu[t * 2 * I8 + j], a);
+  unpack8(gu[t * 2 * I8 + I8 + j], b);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = a[i] * sigmoidf_(a[i]) * b[i];
+  c[t * I8 + j] = pack8(o);
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_rows_kernel(const bf16x8* __restrict__ gu, const bf16x8* __restrict__ dc,
+                                                              bf16x8* __restrict__ dgu, int I8) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= I8) return;
+  const int64_t t = blockIdx.y;
+  float a[8], b[8], g[8], da[8], db[8];
+  unpack8(gu[t * 2 * I8 + j], a);
+  unpack8(gu[t * 2 * I8 + I8 + j], b);
+  unpack8(dc[t * I8 + j], g);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float s = sigmoidf_(a[i]);
+    const float silu = a[i] * s;
+    da[i] = g[i] * b[i] * s * (1.f + a[i] * (1.f - s));
+    db[i] = g[i] * silu;
+  }
+  dgu[t * 2 * I8 + j] = pack8(da);
+  dgu[t * 2 * I8 + I8 + j] = pack8(db);
 }
 
 // In-place rotary embedding (HF rotate_half convention): for i < D/2,
@@ -102,10 +141,24 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const
 
 using namespace llmt;
 
+// LLMT_EW_ROWS=0 selects the flat grid-stride SwiGLU kernels (read per call, for A/B runs)
+static bool ew_rows(int64_t T) {
+  const char* e = getenv("LLMT_EW_ROWS");
+  return T <= 65535 * 16 && !(e && e[0] == '0');
+}
+
 extern "C" hipError_t llmt_swiglu_fwd(const void* gu, void* c, int64_t T, int I, hipStream_t stream) {
   if (I % 8) return hipErrorInvalidValue;
   const int64_t n8 = T * (I / 8);
   if (n8 == 0) return hipSuccess;
+  if (ew_rows(T)) {
+    for (int64_t t0 = 0; t0 < T; t0 += 65535) {  // grid.y limit
+      const int64_t nt = T - t0 < 65535 ? T - t0 : 65535;
+      swiglu_fwd_rows_kernel<<<dim3((I / 8 + 255) / 256, (unsigned)nt), 256, 0, stream>>>(
+          (const bf16x8*)gu + t0 * (I / 4), (bf16x8*)c + t0 * (I / 8), I / 8);
+    }
+    return hipGetLastError();
+  }
   swiglu_fwd_kernel<<<stream_grid(n8, 256), 256, 0, stream>>>((const bf16x8*)gu, (bf16x8*)c, n8, I / 8);
   return hipGetLastError();
 }
@@ -115,6 +168,14 @@ extern "C" hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu,
   if (I % 8) return hipErrorInvalidValue;
   const int64_t n8 = T * (I / 8);
   if (n8 == 0) return hipSuccess;
+  if (ew_rows(T)) {
+    for (int64_t t0 = 0; t0 < T; t0 += 65535) {
+      const int64_t nt = T - t0 < 65535 ? T - t0 : 65535;
+      swiglu_bwd_rows_kernel<<<dim3((I / 8 + 255) / 256, (unsigned)nt), 256, 0, stream>>>(
+          (const bf16x8*)gu + t0 * (I / 4), (const bf16x8*)dc + t0 * (I / 8), (bf16x8*)dgu + t0 * (I / 4), I / 8);
+    }
+    return hipGetLastError();
+  }
   swiglu_bwd_kernel<<<stream_grid(n8, 256), 256, 0, stream>>>((const bf16x8*)gu, (const bf16x8*)dc, (bf16x8*)dgu,
                                                                n8, I / 8);
   return hipGetLastError();

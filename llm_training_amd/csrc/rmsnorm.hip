@@ -13,6 +13,8 @@
 // accumulates into) the bf16/fp32 weight gradient.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace llmt {
 
 template <int NC, bool RES>
@@ -216,8 +218,15 @@ extern "C" int llmt_rmsnorm_bwd_nblocks(int T) {
   // >= 16 rows per block and 2 blocks per CU: one block per CU (the old 256 cap) left the
   // memory pipe under-filled (1.8 TB/s at T=8192, H=4096); the fp32 partials (nblk*H*4 B) stay well
   // below the activation traffic (3*T*H*2 B)
+  // LLMT_RMSNORM_BWD_BLOCKS caps the grid (read once): at T = 32768, H = 4096 the 512 cap measured 0.270 ms,
+  // 1024 0.286, 2048 0.325, 4096 0.319 (profiles/r3_elementwise_kernels.jsonl)
+  static const int cap = [] {
+    const char* e = getenv("LLMT_RMSNORM_BWD_BLOCKS");
+    const int v = e ? atoi(e) : 512;
+    return v > 0 ? v : 512;
+  }();
   int nblk = (T + 15) / 16;
-  if (nblk > 512) nblk = 512;
+  if (nblk > cap) nblk = cap;
   if (nblk < 1) nblk = 1;
   return nblk;
 }
