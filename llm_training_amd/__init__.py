@@ -18,5 +18,5 @@ if not logger.handlers:
     _h = logging.StreamHandler()
     _h.setFormatter(logging.Formatter("[%(asctime)s] [%(levelname)s] %(message)s", "%Y-%m-%d %H:%M:%S"))
     logger.addHandler(_h)
-    logger.setLevel(logging.INFO)
+    logger.setLevel(os.environ.get("LLMT_LOG_LEVEL", "INFO").upper())  # e.g. DEBUG: GEMM layout choices
     logger.propagate = False

@@ -28,7 +28,7 @@ from torch.autograd import Function
 from . import reference as ref
 from .native import lib, use_native
 
-log = logging.getLogger(__name__)
+log = logging.getLogger("llm_training.ops")
 
 # ----------------------------------------------------------------------------- GEMM dispatch
 # The three GEMMs of a linear layer (fwd x @ W^T, dgrad dy @ W, wgrad dy^T @ x) go to one of:
@@ -122,20 +122,24 @@ def _layout(key: tuple, variants: dict, default: str, can_time: bool) -> str:
     if not (can_time and _LAYOUT_TUNE and len(variants) > 1) or os.environ.get("LLMT_DETERMINISTIC") == "1" \
             or torch.cuda.is_current_stream_capturing():
         return default
-    best, best_ms = default, float("inf")
-    for name, fn in variants.items():
+    for fn in variants.values():
         fn()  # warm-up (and hipBLASLt's own solution choice for the problem)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(3):
-            fn()
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1) / 3
-        if ms < best_ms:
-            best, best_ms = name, ms
+    # two interleaved rounds of 2 runs per variant, the faster round kept: a clock or power swing during
+    # one variant's window cannot decide the choice on its own
+    times = {name: float("inf") for name in variants}
+    for _ in range(2):
+        for name, fn in variants.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(2):
+                fn()
+            e1.record()
+            e1.synchronize()
+            times[name] = min(times[name], e0.elapsed_time(e1) / 2)
+    best = min(times, key=times.get)
     _LAYOUT_CACHE[key] = best
-    log.debug("GEMM layout %s -> %s (%.3f ms)", key, best, best_ms)
+    log.debug("GEMM layout %s -> %s (%s)", key, best, ", ".join(f"{k} {v:.3f}" for k, v in sorted(times.items(),
+                                                                                         key=lambda kv: kv[1])))
     return best
 
 
