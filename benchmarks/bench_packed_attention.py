@@ -71,6 +71,24 @@ def main():
         seg, frac = segments(B, S, n, a.equal, g)
         seg = seg.to(dev) if n > 1 else None
         info = F_.segment_info(seg) if seg is not None else None
+        if seg is not None and os.environ.get("LLMT_SEG_ORDER_AB") == "1":
+            os.environ["LLMT_SEG_ORDER"] = "0"
+            info0 = F_.segment_info(seg)
+            os.environ["LLMT_SEG_ORDER"] = "1"
+            t_new, t_old = [], []
+            for _ in range(3):
+                t_new.append(timeit(lambda: F_.flash_attention(q, k, v, causal=True, segment_ids=seg, seg_info=info)))
+                t_old.append(timeit(lambda: F_.flash_attention(q, k, v, causal=True, segment_ids=seg, seg_info=info0)))
+            bn, bo = [], []
+            for _ in range(3):
+                bn.append(timeit(lambda: F_.flash_attention(q, k, v, causal=True, segment_ids=seg,
+                                                            seg_info=info).backward(do)))
+                bo.append(timeit(lambda: F_.flash_attention(q, k, v, causal=True, segment_ids=seg,
+                                                            seg_info=info0).backward(do)))
+            print(json.dumps({"docs": n, "B": B, "S": S, "D": a.D, "Hkv": a.Hkv, "fwd_ms_ordered": round(min(t_new), 4),
+                              "fwd_ms_index_order": round(min(t_old), 4),
+                              "fwd_bwd_ms_ordered": round(min(bn), 4), "fwd_bwd_ms_index_order": round(min(bo), 4)}),
+                  flush=True)
 
         def fwd():
             return F_.flash_attention(q, k, v, causal=True, segment_ids=seg, seg_info=info)

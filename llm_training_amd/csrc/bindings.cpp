@@ -429,17 +429,19 @@ void gemm_splitk_(const at::Tensor& a, const at::Tensor& b, at::Tensor slabs, bo
 // ---------------------------------------------------------------- flash attention
 // q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (any batch/seq/head strides, unit stride on D).
 // seg: optional int32 segment ids (0 = padding): attention is restricted to the token's contiguous run of
-// equal ids. [B, S] = ids only (every tile compares ids); [3, B, S] = ids, run start, run end per token
-// (ops/fused.py segment_info): key tiles outside a query block's runs are skipped and tiles inside one
-// run take the unmasked path.
+// equal ids. [B, S] = ids only (every tile compares ids); [3, B, S] = ids, run start, run end per token:
+// key tiles outside a query block's runs are skipped and tiles inside one run take the unmasked path;
+// ops/fused.py segment_info appends the work orders of the query and key blocks (heaviest first).
 static int seg_layout(const c10::optional<at::Tensor>& seg, int64_t B, int64_t S, const int** sp) {
   *sp = nullptr;
   if (!seg.has_value() || !seg->defined()) return 0;
   TORCH_CHECK(seg->scalar_type() == at::kInt && seg->is_contiguous() && seg->is_cuda(), "flash_attn: seg must be "
               "contiguous int32 on the GPU");
-  TORCH_CHECK(seg->numel() == B * S || seg->numel() == 3 * B * S, "flash_attn: seg must be [B, S] or [3, B, S]");
+  const int64_t nord = 2 * B * ((S + 127) / 128);  // query- and key-block work orders (segment_info)
+  TORCH_CHECK(seg->numel() == B * S || seg->numel() == 3 * B * S || seg->numel() == 3 * B * S + nord,
+              "flash_attn: seg must be [B, S], [3, B, S] or segment_info's [3 B S + 2 B ceil(S / 128)]");
   *sp = seg->data_ptr<int>();
-  return seg->numel() == 3 * B * S ? 1 : 0;
+  return seg->numel() == 3 * B * S + nord ? 2 : seg->numel() == 3 * B * S ? 1 : 0;
 }
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                                   const c10::optional<at::Tensor>& seg, double scale, bool causal,

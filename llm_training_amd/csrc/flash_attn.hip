@@ -169,6 +169,11 @@ struct AttnArgs {
   const int* seg;
   const int* rs;  // run start / end of each token (packed segments), or null
   const int* re;
+  // packed segments: (b, 128-row block) pairs in descending order of their work (key tiles of a query
+  // block / query tiles of a key block, causal), so the query- / key-parallel kernels start the heaviest
+  // blocks first as they do for dense causal rows (ops/fused.py segment_info); null otherwise
+  const int* qord;
+  const int* kord;
   bf16* dk;
   bf16* dv;
   float* dk_part;
@@ -221,6 +226,21 @@ __device__ __forceinline__ RunInfo block_run(const AttnArgs& a, int b, int lo, i
 // does the segment compare matter for the tile [t0, t1] against a block described by ri?
 __device__ __forceinline__ bool seg_mask(const AttnArgs& a, const RunInfo& ri, int t0, int t1) {
   return a.seg && !(ri.uni && t0 >= ri.rs && t1 <= ri.re);
+}
+
+// (batch row, 128-row block) of the i-th block of a 1-D grid (i counts blocks of one head): heaviest first.
+// Dense rows: query blocks from the last (most key tiles under the causal mask), key blocks from the first.
+// Packed rows: the order segment_info sorted by work (qord / kord), which the run layout decides.
+__device__ __forceinline__ void block_of(const AttnArgs& a, int i, int nblk, bool query, int& b, int& blk) {
+  const int* ord = query ? a.qord : a.kord;
+  if (ord) {
+    const int bm = ord[i];
+    b = bm / nblk;
+    blk = bm - b * nblk;
+  } else {
+    b = i % a.B;
+    blk = query ? nblk - 1 - i / a.B : i / a.B;
+  }
 }
 
 // ============================================================================ forward
@@ -1005,8 +1025,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
   int L = (int)blockIdx.x;
   const int hk = L % a.Hkv;
   L /= a.Hkv;
-  const int b = L % a.B;
-  const int kb = L / a.B;
+  int b, kb;
+  block_of(a, L, (S + 127) / 128, false, b, kb);
   const int ks = kb * 128, kw = ks + wid * 32, kr = kw + r;
   const int nT = (S + 31) / 32;
   const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
@@ -1358,8 +1378,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
   L /= a.Hkv;
   const int h = hk * grp + L % grp;
   L /= grp;
-  const int b = L % a.B;
-  const int mb = nqb - 1 - L / a.B;
+  int b, mb;
+  block_of(a, L, nqb, true, b, mb);
   const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
   const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
   const float sl2 = a.scale * kLog2e;
@@ -1561,6 +1581,267 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
   }
 }
 
+// ============================================================================ forward, head-chained
+// fa_fwd3 with NH query heads per workgroup (same batch row and query block, so the same key-tile range,
+// masks and segment runs): the NH heads' tiles form one sequence through the K/V LDS-DMA ring, so the
+// first tile of head j+1 is in flight under the last tile of head j and its Q fragments are loaded there
+// too; head j's O / LSE are written at the boundary. A block then pays the prologue (Q + first K/V tile
+// latency with nothing to hide it) once per NH heads: that fixed cost is ~6.5 tiles' worth per block,
+// the whole kernel at short sequences / packed documents (profiles/r3_attention_bwd_atomic_floor.md).
+// Grid: ceil(S/128) * (Hq / NH) * B blocks, head chains fastest, heaviest query blocks first.
+template <int D, int NH>
+__global__ __launch_bounds__(256, 2) void fa_fwd3c_kernel(AttnArgs a) {
+  constexpr int NKK = D / 16, NDT = D / 32;
+  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
+  using KI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  const int nqb = (S + 127) / 128;
+  int L = (int)blockIdx.x;
+  int h0;
+  if (grp % NH == 0) {  // GQA: kv head fastest (the blocks of one XCD share a kv head's K/V in its L2)
+    const int hk = L % a.Hkv;
+    L /= a.Hkv;
+    h0 = hk * grp + (L % (grp / NH)) * NH;
+    L /= grp / NH;
+  } else {  // chains span kv heads (MHA): consecutive heads
+    const int nch = a.Hq / NH;
+    h0 = (L % nch) * NH;
+    L /= nch;
+  }
+  int b, mb;
+  block_of(a, L, nqb, true, b, mb);
+  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const float sl2 = a.scale * kLog2e;
+  int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
+
+  auto load_q = [&](int h, bfv8 (&qd)[NKK]) {
+    const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) qd[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+  };
+  bfv8 qf[NKK];
+  load_q(h0, qf);
+  // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
+  asm volatile("" : "+v"(sq));
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
+  f32v16 ot[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  // O / LSE of head h from the running state, then the state reset for the next head
+  auto finish = [&](int h) {
+    const float lt = l + __shfl_xor(l, 32, 64);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    uint2 w[4 * NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        w[4 * dt + c].x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
+        w[4 * dt + c].y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
+      }
+    widen_pairs(w);
+    if (qrow < S) {
+      store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
+      if (hh == 0) {
+        const float mu = (m == -INFINITY) ? 0.f : m;
+        a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (mu + __log2f(lt)) * kLn2 : -INFINITY;
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
+    m = -INFINITY;
+    l = 0.f;
+  };
+
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
+  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+
+  if (T == 0) {
+#pragma unroll
+    for (int j = 0; j < NH; ++j) finish(h0 + j);
+    return;
+  }
+  // K/V descriptors of the chain head being fetched, rebuilt when the fetch moves to the next kv head;
+  // records end with the last row's D elements (the 256-byte DMA rows of D < 128 read past a row -> zeros
+  // instead of a fault)
+  const int64_t krec = ((int64_t)(S - 1) * a.k_ss + D) * 2, vrec = ((int64_t)(S - 1) * a.v_ss + D) * 2;
+  int fhk = h0 / grp;
+  Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)fhk * a.k_sh, krec);
+  Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)fhk * a.v_sh, vrec);
+  const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
+  // tile u of the chain = tile u % T of head u / T, in ring slot u & 1
+  auto issue = [&](int u, int j, int t) {
+    const char* slot = smem + __builtin_amdgcn_readfirstlane((u & 1) * SLOT);
+    const int n0 = kv_beg + t * BN;
+    int vk[4], vv[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int row = 16 * wid + 4 * n + (lane >> 4);
+      const int ch = (lane & 15) ^ KI::swz(row);
+      vk[n] = ((n0 + row) * a.k_ss + ch * 8) * 2;
+      vv[n] = ((n0 + row) * a.v_ss + ch * 8) * 2;
+    }
+    const int hk = (h0 + j) / grp;
+    if (hk != fhk) {  // wave-uniform: a new kv head (MHA, or a chain crossing a GQA group)
+      fhk = hk;
+      krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, krec);
+      vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, vrec);
+    }
+    dma_tile9(krs, vrs, srs, slot + 16 * wid * 256, IMG, slot + 2 * IMG, vk, vv, (n0 + lane) * 4);
+  };
+  int ro[NKK], to[NDT][2];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
+  {
+    const int g = lane >> 4, i16 = lane & 15;
+    const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      to[dt][0] = KI::toff(BN, row, dt * 32 + col);
+      to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
+    }
+  }
+
+  issue(0, 0, 0);
+  wait_vm<0>();
+  ring_barrier();
+  int j = 0, t = 0;
+  const int U = NH * T;
+  for (int u = 0; u < U; ++u) {
+    const char* slot = smem + __builtin_amdgcn_readfirstlane((u & 1) * SLOT);
+    const int n0 = kv_beg + t * BN;
+    const bool last = t == T - 1;
+    if (u + 1 < U) {
+      if (last)
+        issue(u + 1, j + 1, 0);
+      else
+        issue(u + 1, j, t + 1);
+    }
+    bfv8 fr[16];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) fr[8 * tt + kk] = lds_b128(slot + 8192 * tt + ro[kk]);
+    __builtin_amdgcn_sched_barrier(0);
+    f32v16 st[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[tt][i] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) st[tt] = mfma32(fr[8 * tt + kk], qf[kk], st[tt]);
+    }
+    // the next head's Q into the registers the S^T chain just consumed: the loads fly under the rest of
+    // the tile (softmax, P.V)
+    if (last && j + 1 < NH) load_q(h0 + j + 1, qf);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const char* base = slot + IMG + 256 * (32 * tt + 16 * s2);
+          const s16v4 lo = lds_tr(base + to[dt][0]), hi = lds_tr(base + to[dt][1]);
+          fr[8 * tt + 4 * s2 + dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    const bool m_causal = a.causal && (n0 + BN - 1 > qw);
+    const bool m_window = a.window >= 0 && (n0 < qw + 31 - a.window);
+    const bool m_end = n0 + BN > S;
+    const bool m_seg = seg_mask(a, qr, n0, n0 + BN - 1);
+    if (m_causal || m_window || m_end || m_seg || qw + 31 >= S) {
+      const int* Ss = reinterpret_cast<const int*>(slot + 2 * IMG);
+      const int lim = qrow - n0 - 4 * hh, lo = qrow - a.window - n0 - 4 * hh, hi = S - 1 - n0 - 4 * hh;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          int4 sk = make_int4(sq, sq, sq, sq);
+          if (m_seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * tt + 8 * c + 4 * hh);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int ko = 32 * tt + 8 * c + jj;
+            bool ok = (ko <= hi) && (qrow < S);
+            if (a.causal) ok = ok && (ko <= lim);
+            if (a.window >= 0) ok = ok && (ko >= lo);
+            if (m_seg) ok = ok && ((&sk.x)[jj] == sq);
+            if (!ok) st[tt][4 * c + jj] = -INFINITY;
+          }
+        }
+    }
+    float mx0 = vmax3(st[0][0], st[0][1], st[0][2]), mx1 = vmax3(st[1][0], st[1][1], st[1][2]);
+#pragma unroll
+    for (int i = 3; i < 15; i += 2) {
+      mx0 = vmax3(mx0, st[0][i], st[0][i + 1]);
+      mx1 = vmax3(mx1, st[1][i], st[1][i + 1]);
+    }
+    float smax = vmax3(mx0, st[0][15], vmax3(mx1, st[1][15], mx1));
+    smax = fmaxf(smax, __shfl_xor(smax, 32, 64)) * sl2;
+    if (__any(smax > m + kThr)) {
+      const float mnew = fmaxf(m, smax);
+      const float alpha = (mnew == -INFINITY) ? 1.f : fexp2(m - mnew);
+      m = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
+    }
+    const float nm = (m == -INFINITY) ? 0.f : -m;
+    float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        st[tt][i] = fexp2(fmaf(st[tt][i], sl2, nm));
+        st[tt][i + 1] = fexp2(fmaf(st[tt][i + 1], sl2, nm));
+        rs0 += st[tt][i];
+        rs1 += st[tt][i + 1];
+      }
+    l += rs0 + rs1;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bfv8 pb = acc_as_b(st[tt], s2);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) ot[dt] = mfma32(fr[8 * tt + 4 * s2 + dt], pb, ot[dt]);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    wait_vm<0>();  // this wave's DMA of tile u + 1 (and the next head's Q loads)
+    if (last) {
+      finish(h0 + j);
+      if (j + 1 < NH) {
+        // the asm wait above retired the Q loads; this statement makes hipcc place its own wait for
+        // them here (already satisfied) instead of in front of the next tile's MFMAs, after the DMA
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
+      }
+      ++j;
+      t = 0;
+    } else {
+      ++t;
+    }
+    ring_barrier();
+  }
+  wait_vm<0>();  // the last head's O stores
+}
+
 // ============================================================================ backward dQ, D = 128, v3
 // The forward v3 structure applied to the query-parallel dQ pass (grid, block order, K/V LDS-DMA ring,
 // two workgroups per CU): per 32-key half of a 64-key tile, batched K row reads -> S^T = K.Q^T, batched
@@ -1583,8 +1864,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   L /= a.Hkv;
   const int h = hk * grp + L % grp;
   L /= grp;
-  const int b = L % a.B;
-  const int mb = nqb - 1 - L / a.B;
+  int b, mb;
+  block_of(a, L, nqb, true, b, mb);
   const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
   const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
   const bf16* dop = a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh;
@@ -1816,6 +2097,10 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   if (seg && seg_runs) {
     a.rs = seg + (int64_t)B * S;
     a.re = seg + 2 * (int64_t)B * S;
+    if (seg_runs == 2) {  // + the work orders of the query / key blocks
+      a.qord = seg + 3 * (int64_t)B * S;
+      a.kord = a.qord + (int64_t)B * ((S + 127) / 128);
+    }
   }
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv;
   a.q_sb = q_sb; a.q_ss = q_ss; a.q_sh = q_sh; a.k_sb = k_sb; a.k_ss = k_ss; a.k_sh = k_sh;
@@ -1831,28 +2116,48 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   // vs 0.458, B64 S512 0.314 vs 0.343 ms (the per-block cost of short sequences / packed documents),
   // bitwise-equal output (profiles/r3_attention_wide_store_ab.jsonl)
   const int variant = fve ? atoi(fve) : 4;  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
+  // head chains (fa_fwd3c: 4 query heads per workgroup, bitwise-equal output) pay where a block's heads
+  // have their own K/V: MHA B8 S4096 H32 D128 1.567 -> 1.391 ms; with GQA they lose (B4 S8192 Hq32 Hkv8
+  // 2.230 -> 2.507 ms, S1024 0.451 -> 0.465; profiles/r3_attention_head_chain_ab.jsonl). Default: chains for
+  // MHA (Phi-3), one head per workgroup for GQA (Llama); variants 5 / 6 force chains of 2 / 4.
+  const int grp = Hq / Hkv;
+  const int chain = variant == 5 ? (Hq % 2 == 0 ? 2 : 0)
+                  : (variant == 6 || (variant == 4 && grp == 1)) ? (Hq % 4 == 0 ? 4 : 0) : 0;
+  const unsigned nb1 = (unsigned)((S + 127) / 128 * Hq * B);
   switch (D) {
     case 64:  // the v3 structure on 128-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a);
+      else if (chain == 4)
+        fa_fwd3c_kernel<64, 4><<<nb1 / 4, 256, 0, stream>>>(a);
+      else if (chain == 2)
+        fa_fwd3c_kernel<64, 2><<<nb1 / 2, 256, 0, stream>>>(a);
       else
-        fa_fwd3_kernel<64, 1, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<64, 1, 1><<<nb1, 256, 0, stream>>>(a);
       break;
     case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
         fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a);
+      else if (chain == 4)
+        fa_fwd3c_kernel<96, 4><<<nb1 / 4, 256, 0, stream>>>(a);
+      else if (chain == 2)
+        fa_fwd3c_kernel<96, 2><<<nb1 / 2, 256, 0, stream>>>(a);
       else
-        fa_fwd3_kernel<96, 1, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<96, 1, 1><<<nb1, 256, 0, stream>>>(a);
       break;
     case 128: {
       if (a.drop_thresh)  // dropout lives in the generic kernels
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
       else if (variant == 2)  // row sums through the inline-asm add (each behind its own wait state)
-        fa_fwd3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<128><<<nb1, 256, 0, stream>>>(a);
       else if (variant == 3)  // dwordx2 O store tail (A/B reference)
-        fa_fwd3_kernel<128, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else if (variant == 4)
-        fa_fwd3_kernel<128, 1, 1><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+        fa_fwd3_kernel<128, 1><<<nb1, 256, 0, stream>>>(a);
+      else if (chain == 4)
+        fa_fwd3c_kernel<128, 4><<<nb1 / 4, 256, 0, stream>>>(a);
+      else if (chain == 2)
+        fa_fwd3c_kernel<128, 2><<<nb1 / 2, 256, 0, stream>>>(a);
+      else if (variant >= 4)
+        fa_fwd3_kernel<128, 1, 1><<<nb1, 256, 0, stream>>>(a);
       else
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
     } break;
@@ -1893,6 +2198,10 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   if (seg && seg_runs) {
     a.rs = seg + (int64_t)B * S;
     a.re = seg + 2 * (int64_t)B * S;
+    if (seg_runs == 2) {  // + the work orders of the query / key blocks
+      a.qord = seg + 3 * (int64_t)B * S;
+      a.kord = a.qord + (int64_t)B * ((S + 127) / 128);
+    }
   }
   a.dk = (bf16*)dk; a.dv = (bf16*)dv;
   const int64_t part = (int64_t)B * S * Hq * D;

@@ -587,9 +587,12 @@ class _FlashAttnFn(Function):
 
 
 def segment_info(segment_ids: torch.Tensor) -> torch.Tensor:
-    """[3, B, S] int32 for the flash kernels: segment id, first and last index of the contiguous run of
-    equal ids containing each token. Computed once per forward (a handful of scans) and shared by every
-    layer; lets a query block skip all key tiles outside its runs (ops on device, no host sync)."""
+    """Run layout of packed rows for the flash kernels, int32, flat: [3, B, S] (segment id, first and last
+    index of the contiguous run of equal ids containing each token) followed by two work orders of the
+    B x ceil(S / 128) (row, 128-token block) pairs — query blocks by their key tiles, key blocks by their
+    query tiles under the causal mask, heaviest first — so the kernels start long blocks first as they do
+    on dense rows. Computed once per forward (a handful of scans and two small sorts, on device, no host
+    sync) and shared by every layer; lets a query block skip all key tiles outside its runs."""
     seg = segment_ids.to(torch.int32)
     B, S = seg.shape
     idx = torch.arange(S, device=seg.device, dtype=torch.int32).expand(B, S)
@@ -599,7 +602,18 @@ def segment_info(segment_ids: torch.Tensor) -> torch.Tensor:
     end[:, :-1] = start[:, 1:]
     rs = torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), dim=1).values
     re = torch.where(end, idx, torch.full_like(idx, S)).flip(1).cummin(dim=1).values.flip(1)
-    return torch.stack([seg, rs.to(torch.int32), re.to(torch.int32)]).contiguous()
+    runs = torch.stack([seg, rs.to(torch.int32), re.to(torch.int32)])
+    if os.environ.get("LLMT_SEG_ORDER", "1") == "0":  # A/B: the [3, B, S] layout alone (index-order blocks)
+        return runs.contiguous()
+    nb = (S + 127) // 128
+    starts = torch.arange(nb, device=seg.device, dtype=torch.int64) * 128
+    # query block: 64-key tiles from its first query's run start to the diagonal
+    tq = (torch.clamp(starts + 128, max=S) - (rs[:, starts].long() // 64) * 64 + 63) // 64
+    # key block: 32-row query tiles from the block to its last key's run end
+    tk = (re[:, torch.clamp(starts + 127, max=S - 1)].long() + 1 - starts + 31) // 32
+    qord = torch.argsort(-tq.reshape(-1), stable=True).to(torch.int32)
+    kord = torch.argsort(-tk.reshape(-1), stable=True).to(torch.int32)
+    return torch.cat([runs.reshape(-1), qord, kord])
 
 
 def _native_seg(segment_ids, seg_info):

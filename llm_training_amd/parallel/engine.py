@@ -203,7 +203,12 @@ class DataParallelEngine:
         self.native = self.cuda and use_native(torch.empty(0, device=dev, dtype=torch.bfloat16))
         if any(p.dtype == torch.float16 for p in model.parameters()) or grad_dtype == torch.float16:
             self.native = False  # fp16 precisions: the bf16/fp32 optimizer and norm kernels do not apply
-        self.comm_stream = torch.cuda.Stream(device=dev) if (self.cuda and self.overlap) else None
+        # collectives on a high-priority stream (SURVEY §5.8 b): when RCCL kernels and compute kernels are
+        # both queued, the dispatcher places the collective's workgroups first, so the reduce-scatter /
+        # all-gather progress is not gated on the compute kernels' tail (LLMT_COMM_PRIORITY=0: default)
+        comm_prio = -1 if os.environ.get("LLMT_COMM_PRIORITY", "1") != "0" else 0
+        self.comm_stream = (torch.cuda.Stream(device=dev, priority=comm_prio) if (self.cuda and self.overlap)
+                            else None)
         if self.cuda and (self.dp > 1 or self.pc.tp_size > 1):
             # RCCL kernels share the CUs with the GEMMs of the compute stream: hipBLASLt's stream-K
             # solutions assume every workgroup of their launch is resident (partial tiles are handed
