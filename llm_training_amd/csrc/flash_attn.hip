@@ -1362,25 +1362,54 @@ __device__ __forceinline__ float vadd(float a, float b) {
   return r;
 }
 
-template <int D, int RS = 0, int WS = 0>
-__global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
+// DMA of one 64-key K/V tile (+ its 64 segment ids) of the query-parallel kernels into ring slot `slot`:
+// with NW = 4 waves each wave fetches 16 K and 16 V rows (4 + 4 one-KB pieces), with NW = 8 eight of each
+// (2 + 2); every wave also fetches the segment ids (the same 256 bytes)
+template <int NW>
+__device__ __forceinline__ void kv_tile_dma(const char* slot, int n0, int wid, int lane, const AttnArgs& a,
+                                            const Rsrc& krs, const Rsrc& vrs, const Rsrc& srs) {
+  constexpr int IMG = 64 * 256;
+  using KI = Img<128>;
+  constexpr int RPW = 64 / NW;  // rows per wave
+  int vk[RPW / 4], vv[RPW / 4];
+#pragma unroll
+  for (int n = 0; n < RPW / 4; ++n) {
+    const int row = RPW * wid + 4 * n + (lane >> 4);
+    const int ch = (lane & 15) ^ KI::swz(row);
+    vk[n] = ((n0 + row) * a.k_ss + ch * 8) * 2;
+    vv[n] = ((n0 + row) * a.v_ss + ch * 8) * 2;
+  }
+  const char* k0 = slot + RPW * wid * 256;
+  if constexpr (NW == 4)
+    dma_tile9(krs, vrs, srs, k0, IMG, slot + 2 * IMG, vk, vv, (n0 + lane) * 4);
+  else
+    dma_tile5(krs, vrs, srs, k0, k0 + 4 * 256, k0 + IMG, k0 + IMG + 4 * 256, slot + 2 * IMG, vk[0], vk[1], vv[0], vv[1],
+              (n0 + lane) * 4);
+}
+
+// NW = 8: two query heads of one kv group per workgroup, side by side (waves 0-3 head h, waves 4-7 head
+// h + 1, 32 queries each): every K/V tile of the LDS-DMA ring then serves 256 query rows instead of 128,
+// crossing L2 -> LDS half as often, and each wave issues half the DMA pieces (2 K + 2 V rows groups).
+template <int D, int RS = 0, int WS = 0, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;  // k-steps of a D-deep product, 32-wide output tiles
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
   using KI = Img<128>;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), wq = wid & 3;
   const int S = a.S, grp = a.Hq / a.Hkv;
   const int nqb = (S + 127) / 128;
   int L = (int)blockIdx.x;
   const int hk = L % a.Hkv;
   L /= a.Hkv;
-  const int h = hk * grp + L % grp;
-  L /= grp;
+  const int hpb = NW / 4;  // query heads per workgroup
+  const int h = hk * grp + (L % (grp / hpb)) * hpb + (wid >> 2);
+  L /= grp / hpb;
   int b, mb;
   block_of(a, L, nqb, true, b, mb);
-  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const int qs = mb * 128, qw = qs + wq * 32, qrow = qw + r;
   const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
   const float sl2 = a.scale * kLog2e;
   int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
@@ -1412,19 +1441,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3_kernel(AttnArgs a) {
     const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
     const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
     const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
-    auto issue = [&](int t) {
-      const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
-      const int n0 = kv_beg + t * BN;
-      int vk[4], vv[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int row = 16 * wid + 4 * n + (lane >> 4);
-        const int ch = (lane & 15) ^ KI::swz(row);
-        vk[n] = ((n0 + row) * a.k_ss + ch * 8) * 2;
-        vv[n] = ((n0 + row) * a.v_ss + ch * 8) * 2;
-      }
-      dma_tile9(krs, vrs, srs, slot + 16 * wid * 256, IMG, slot + 2 * IMG, vk, vv, (n0 + lane) * 4);
-    };
+    auto issue = [&](int t) { kv_tile_dma<NW>(smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT), kv_beg + t * BN, wid,
+                                              lane, a, krs, vrs, srs); };
     // loop-invariant LDS offsets: K row reads (two 32-key halves) and V^T transposed reads
     int ro[NKK], to[NDT][2];
 #pragma unroll
@@ -1848,25 +1866,27 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3c_kernel(AttnArgs a) {
 // V row reads -> dP^T = V.dO^T, dS = P (dP - delta) with P = exp2(S * scale * log2e - lse * log2e)
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
 // dQ = scale * sum; the row constants come straight from lse / delta (delta written by the prep kernel).
-template <int D, bool IL = true, bool WS = false>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
+// NW = 8: two query heads of one kv group per workgroup sharing the K/V ring (as fa_fwd3_kernel)
+template <int D, bool IL = true, bool WS = false, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
   using KI = Img<128>;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), wq = wid & 3;
   const int S = a.S, grp = a.Hq / a.Hkv;
   const int nqb = (S + 127) / 128;
   int L = (int)blockIdx.x;
   const int hk = L % a.Hkv;
   L /= a.Hkv;
-  const int h = hk * grp + L % grp;
-  L /= grp;
+  const int hpb = NW / 4;  // query heads per workgroup
+  const int h = hk * grp + (L % (grp / hpb)) * hpb + (wid >> 2);
+  L /= grp / hpb;
   int b, mb;
   block_of(a, L, nqb, true, b, mb);
-  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
+  const int qs = mb * 128, qw = qs + wq * 32, qrow = qw + r;
   const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
   const bf16* dop = a.dout + (int64_t)b * a.d_sb + (int64_t)h * a.d_sh;
   const float sl2 = a.scale * kLog2e;
@@ -1904,19 +1924,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
     const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
     const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
     const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
-    auto issue = [&](int t) {
-      const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
-      const int n0 = kv_beg + t * BN;
-      int vk[4], vv[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int row = 16 * wid + 4 * n + (lane >> 4);
-        const int ch = (lane & 15) ^ KI::swz(row);
-        vk[n] = ((n0 + row) * a.k_ss + ch * 8) * 2;
-        vv[n] = ((n0 + row) * a.v_ss + ch * 8) * 2;
-      }
-      dma_tile9(krs, vrs, srs, slot + 16 * wid * 256, IMG, slot + 2 * IMG, vk, vv, (n0 + lane) * 4);
-    };
+    auto issue = [&](int t) { kv_tile_dma<NW>(smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT), kv_beg + t * BN, wid,
+                                              lane, a, krs, vrs, srs); };
     int ro[NKK], to[NDT][2];
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
@@ -2044,6 +2053,16 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
 
 using namespace llmt;
 
+// GQA head pairs (two query heads per 8-wave workgroup sharing the K/V ring, fa_fwd3_kernel /
+// fa_bwd_dq3_kernel NW = 8) against one head per 4-wave workgroup, in one process
+// (profiles/r3_attention_head_pairs_ab.jsonl): B4 S8192 Hq32 Hkv8 forward 2.183 -> 2.111 ms, backward
+// 8.146 -> 7.889 ms (dQ); B2 S4096 equal; B32 S1024 forward 0.446 -> 0.486, backward 1.483 -> 1.532 (one
+// workgroup per CU exposes the per-block prologue that two independent workgroups hide). In the Llama-3-8B
+// step, though, pairs on every dense S8192 call lost 5 ms/step (1497.5 / 1498.7 vs 1492.6 / 1493.0 ms,
+// alternating runs on one box): an 8-wave workgroup waits for a whole CU's worth of free slots while the
+// optimizer stream's kernels overlap the forward. Opt-in only (forward variant 7, dQ variant 3).
+static bool pairs_pay(const int*, int) { return false; }
+
 // dK/dV kernel variant, read on every launch so one process can A/B them (LLMT_FA_BWD_VARIANT):
 //   1 = end-of-tile barrier after an LDS drain and scalar softmax (A/B reference), 3 = barrier without
 //   the drain (rows prefetched for the next tile stay in flight across it) and packed softmax. (A
@@ -2156,6 +2175,8 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
         fa_fwd3c_kernel<128, 4><<<nb1 / 4, 256, 0, stream>>>(a);
       else if (chain == 2)
         fa_fwd3c_kernel<128, 2><<<nb1 / 2, 256, 0, stream>>>(a);
+      else if (grp % 2 == 0 && (variant == 7 || (variant == 4 && pairs_pay(seg, S))))  // GQA head pairs
+        fa_fwd3_kernel<128, 1, 1, 8><<<nb1 / 2, 512, 0, stream>>>(a);
       else if (variant >= 4)
         fa_fwd3_kernel<128, 1, 1><<<nb1, 256, 0, stream>>>(a);
       else
@@ -2251,7 +2272,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       // 1.522 ms, B4 S8192 unchanged, same gradients
       const char* dqe = getenv("LLMT_FA_DQ_VARIANT");
       const int dqv = dqe ? atoi(dqe) : 2;
-      if (dqv == 0)
+      if ((Hq / Hkv) % 2 == 0 && (dqv == 3 || (dqv == 2 && pairs_pay(seg, S))))  // GQA head pairs
+        fa_bwd_dq3_kernel<128, true, true, 8><<<(S + 127) / 128 * (Hq / 2) * B, 512, 0, stream>>>(a);
+      else if (dqv == 0)
         fa_bwd_dq3_kernel<128, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (dqv == 1)
         fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
