@@ -2135,13 +2135,13 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   // vs 0.458, B64 S512 0.314 vs 0.343 ms (the per-block cost of short sequences / packed documents),
   // bitwise-equal output (profiles/r3_attention_wide_store_ab.jsonl)
   const int variant = fve ? atoi(fve) : 4;  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
-  // head chains (fa_fwd3c: 4 query heads per workgroup, bitwise-equal output) pay where a block's heads
-  // have their own K/V: MHA B8 S4096 H32 D128 1.567 -> 1.391 ms; with GQA they lose (B4 S8192 Hq32 Hkv8
-  // 2.230 -> 2.507 ms, S1024 0.451 -> 0.465; profiles/r3_attention_head_chain_ab.jsonl). Default: chains for
-  // MHA (Phi-3), one head per workgroup for GQA (Llama); variants 5 / 6 force chains of 2 / 4.
+  // head chains (fa_fwd3c: 4 query heads per workgroup, bitwise-equal output) pay standalone where a
+  // block's heads have their own K/V: MHA B8 S4096 H32 D128 1.567 -> 1.391 ms, D96 1.631 -> 1.245 ms; with
+  // GQA they lose (B4 S8192 Hq32 Hkv8 2.230 -> 2.507 ms; profiles/r3_attention_head_chain_ab.jsonl). In the
+  // Phi-3 IT step (packed MHA) they cost 3 ms/step (688.4 / 690.3 vs 685.9 / 686.2 ms alternating on one
+  // box), so chains are opt-in: variants 5 / 6 = chains of 2 / 4; 8 = one head per workgroup.
   const int grp = Hq / Hkv;
-  const int chain = variant == 5 ? (Hq % 2 == 0 ? 2 : 0)
-                  : (variant == 6 || (variant == 4 && grp == 1)) ? (Hq % 4 == 0 ? 4 : 0) : 0;
+  const int chain = variant == 5 ? (Hq % 2 == 0 ? 2 : 0) : variant == 6 ? (Hq % 4 == 0 ? 4 : 0) : 0;
   const unsigned nb1 = (unsigned)((S + 127) / 128 * Hq * B);
   switch (D) {
     case 64:  // the v3 structure on 128-byte rows (256-byte LDS pitch)
