@@ -106,3 +106,39 @@ def test_varlen_skips_cross_document_tiles():
     packed = _time(lambda: run(seg))
     print(f"causal fwd+bwd {full:.3f} ms, 8 packed docs {packed:.3f} ms ({full / packed:.2f}x)")
     assert full / packed >= 3.0, (full, packed)
+
+
+def _fwd_bwd(q, k, v, do, seg):
+    qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+    info = F_.segment_info(seg) if seg is not None else None
+    o = F_.flash_attention(qq, kk, vv, causal=True, segment_ids=seg, seg_info=info)
+    o.backward(do)
+    return o.detach(), qq.grad, kk.grad, vv.grad
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(8, 2, 128), (4, 4, 128), (4, 4, 96), (4, 4, 64)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_attention_kernel_variants_bitwise(Hq, Hkv, D, packed, monkeypatch):
+    """The opt-in forward / dQ forms — MHA head chains of 2 / 4 (forward variants 5 / 6), GQA head pairs
+    on 8-wave workgroups (forward 7, dQ 3) — and the packed-block work order (against LLMT_SEG_ORDER=0)
+    compute exactly what the default kernels compute: same per-head math, only the block -> workgroup
+    assignment differs."""
+    torch.manual_seed(0)
+    B, S = 2, 1024
+    q = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    do = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    seg = _layout(S, [300, 17, 129, 64, 1, 200], 40).expand(B, S).contiguous() if packed else None
+    base = _fwd_bwd(q, k, v, do, seg)
+    forms = [("LLMT_FA_FWD_VARIANT", "5"), ("LLMT_FA_FWD_VARIANT", "6")]
+    if D == 128 and Hq // Hkv % 2 == 0:
+        forms += [("LLMT_FA_FWD_VARIANT", "7"), ("LLMT_FA_DQ_VARIANT", "3")]
+    if packed:
+        forms += [("LLMT_SEG_ORDER", "0")]
+    for env, val in forms:
+        monkeypatch.setenv(env, val)
+        got = _fwd_bwd(q, k, v, do, seg)
+        monkeypatch.delenv(env)
+        for name, x, y in zip(("o", "dq", "dk", "dv"), got, base):
+            assert torch.equal(x, y), f"{env}={val}: {name} differs"
