@@ -15,6 +15,7 @@ import sqlite3
 
 
 def _short(name: str, width: int = 90) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*\)$", "", name)  # drop argument lists
     return name if len(name) <= width else name[: width - 3] + "..."
 
