@@ -43,19 +43,49 @@ class JSONLLogger:
 
 
 class CSVLogger(JSONLLogger):
+    """``metrics.csv`` with one header: a resumed run appends to the existing file under its header, and
+    a metric that appears later (the first validation loss) rewrites the file once with the widened
+    header instead of being dropped (Lightning's CSVLogger keeps every key as well)."""
+
     def __init__(self, save_dir: str = "logs", name: str = "run", version: str | None = None, **kw):
         super().__init__(save_dir, name, version)
-        self._keys = None
+        self._keys: list[str] | None = None
         self._w = None
+
+    @property
+    def path(self) -> str:
+        return os.path.join(self.log_dir, "metrics.csv")
+
+    def _open(self, keys: list[str]):
+        """(Re)open for appending with header ``keys``; existing rows are rewritten under it if the file's
+        header is narrower."""
+        if self._f is not None:
+            self._f.close()
+        old_keys, rows = [], []
+        if os.path.exists(self.path) and os.path.getsize(self.path) > 0:
+            with open(self.path, newline="") as f:
+                r = csv.DictReader(f)
+                old_keys = list(r.fieldnames or [])
+                if any(k not in old_keys for k in keys):
+                    rows = list(r)
+        merged = old_keys + [k for k in keys if k not in old_keys]
+        if rows or not old_keys:
+            with open(self.path, "w", newline="") as f:
+                w = csv.DictWriter(f, fieldnames=merged)
+                w.writeheader()
+                w.writerows(rows)
+        self._keys = merged
+        self._f = open(self.path, "a", newline="")
+        self._w = csv.DictWriter(self._f, fieldnames=self._keys)
 
     def log_metrics(self, metrics: dict, step: int):
         row = {"step": step, **metrics}
         if self._w is None:
             os.makedirs(self.log_dir, exist_ok=True)
-            self._f = open(os.path.join(self.log_dir, "metrics.csv"), "a", newline="")
-            self._keys = list(row)
-            self._w = csv.DictWriter(self._f, fieldnames=self._keys, extrasaction="ignore")
-            self._w.writeheader()
+            self._open(list(row))
+        elif any(k not in self._keys for k in row):
+            self._f.flush()
+            self._open(self._keys + [k for k in row if k not in self._keys])
         self._w.writerow(row)
         self._f.flush()
 

@@ -342,3 +342,56 @@ def test_hf_enable_liger_kernel_on_hip(model_type):
         with torch.no_grad():
             losses.append(lm.training_step({"input_ids": ids, "labels": ids})[0].item())
     assert abs(losses[1] - losses[0]) < 2e-2 * abs(losses[0]), losses
+
+
+def test_cli_fit_and_resume_on_gpu(tmp_path):
+    """The whole framework path on the GPU: `llm-training fit` (YAML, trainer loop, FSDP2 strategy at
+    bf16-true, DummyDataModule, ModelCheckpoint, CSV logger) on the HIP kernels, then a second `fit` that
+    resumes from `ckpt_path: last` and continues the step count; both runs' losses are finite and the
+    resumed run starts where the first stopped."""
+    import csv
+    import os
+
+    from llm_training_amd.cli.main import main
+
+    def write(name, steps, ckpt=None):
+        cfg = tmp_path / name
+        cfg.write_text(f"""
+seed_everything: 1
+trainer:
+  strategy: {{class_path: llm_training.lightning.FSDP2Strategy}}
+  precision: bf16-true
+  logger:
+    class_path: llm_training.lightning.CSVLogger
+    init_args: {{save_dir: {tmp_path}/logs, name: g}}
+  max_steps: {steps}
+  log_every_n_steps: 1
+  gradient_clip_val: 1.0
+  callbacks:
+    - class_path: llm_training.lightning.ModelCheckpoint
+      init_args: {{dirpath: {tmp_path}/ckpt, every_n_train_steps: 2, save_top_k: 1, save_last: true}}
+model:
+  class_path: llm_training.lms.CLM
+  init_args.config:
+    model:
+      model_class: llm_training.models.Llama
+      model_config: {{vocab_size: 512, hidden_size: 256, intermediate_size: 512, num_hidden_layers: 2,
+                      num_attention_heads: 4, num_key_value_heads: 2, max_position_embeddings: 512}}
+    optim:
+      optimizer_class: torch.optim.AdamW
+      optimizer_kwargs: {{lr: 1e-3}}
+data:
+  class_path: llm_training.data.DummyDataModule
+  init_args.config: {{batch_size: 2, vocab_size: 512, max_length: 256, num_samples: 64, base_seed: 3}}
+{'' if ckpt is None else 'ckpt_path: ' + ckpt}
+""")
+        return cfg
+
+    assert main(["fit", "--config", str(write("a.yaml", 4))]) == 0
+    assert os.path.exists(tmp_path / "ckpt" / "last.ckpt")
+    assert main(["fit", "--config", str(write("b.yaml", 6, "last"))]) == 0
+    rows = [r for f in sorted((tmp_path / "logs" / "g").glob("**/metrics.csv")) for r in csv.DictReader(open(f))]
+    steps = sorted({int(float(r["step"])) for r in rows if r.get("step")})
+    losses = [float(r["Loss/Train/Step"]) for r in rows if r.get("Loss/Train/Step")]
+    assert losses and all(x == x and x < 20 for x in losses)
+    assert max(steps) >= 5, steps

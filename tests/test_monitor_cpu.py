@@ -167,3 +167,25 @@ def test_strategies_map_offload_knobs():
     assert FSDP2Strategy(offload_policy={"class_path": "torch.distributed.fsdp.CPUOffloadPolicy"}).offload_optimizer
     assert not FSDP2Strategy(offload_policy={"class_path": "torch.distributed.fsdp.OffloadPolicy"}).offload_optimizer
     assert not FSDP2Strategy().offload_optimizer
+
+
+def test_csv_logger_one_header_across_resume_and_late_keys(tmp_path):
+    """A resumed run appends under the existing header; a metric first logged later (validation loss)
+    widens the header once and keeps every earlier row."""
+    import csv
+
+    from llm_training_amd.runtime.loggers import CSVLogger
+    a = CSVLogger(save_dir=str(tmp_path), name="r")
+    a.log_metrics({"loss": 1.0}, 1)
+    a.log_metrics({"loss": 0.9}, 2)
+    a.finalize("success")
+    b = CSVLogger(save_dir=str(tmp_path), name="r")  # the resumed run, same directory
+    b.log_metrics({"loss": 0.8}, 3)
+    b.log_metrics({"loss": 0.7, "val": 0.75}, 4)
+    b.log_metrics({"loss": 0.6}, 5)
+    b.finalize("success")
+    text = open(tmp_path / "r" / "metrics.csv").read()
+    assert text.count("step") == 1
+    rows = list(csv.DictReader(open(tmp_path / "r" / "metrics.csv")))
+    assert [int(r["step"]) for r in rows] == [1, 2, 3, 4, 5]
+    assert rows[3]["val"] == "0.75" and rows[0]["val"] == "" and rows[4]["loss"] == "0.6"
