@@ -380,6 +380,8 @@ class Trainer:
     def train_step(self, batches: list[dict]):
         eng, lm = self.engine, self.lm
         t0 = time.perf_counter()
+        if self.meter is not None and self.meter.t0 is None:
+            self.meter.start()  # the first logged rate covers the first step's own time
         self.profiler.before_step(self.state.global_step + 1)
         self.watchdog.arm()
         for cb in self.callbacks:
@@ -440,13 +442,17 @@ class Trainer:
             _call(cb, "on_train_batch_end", self, lm, None, batches[-1], self.state.batch_idx)
 
     def _count_tokens(self, batches: list[dict]):
-        ids = [b.get("input_ids") for b in batches if isinstance(b, dict)]
-        ids = [t for t in ids if isinstance(t, torch.Tensor)]
+        # input_ids, or chosen_input_ids + rejected_input_ids of the preference objectives
+        ids = [v for b in batches if isinstance(b, dict) for k, v in b.items()
+               if k.endswith("input_ids") and isinstance(v, torch.Tensor)]
         if not ids:
             return
         S = int(ids[0].shape[-1])
         if S not in self._fpt:
-            self._fpt[S] = model_flops_per_token(getattr(self.lm.model, "config", None), S)
+            fpt = model_flops_per_token(getattr(self.lm.model, "config", None), S)
+            if getattr(self.lm, "ref_model", None) is not None:
+                fpt *= 4.0 / 3.0  # DPO: the frozen reference model's forward (1/3 of forward + backward)
+            self._fpt[S] = fpt
         self.meter.fpt = self._fpt[S]
         self.meter.update(sum(t.numel() for t in ids))
 

@@ -395,3 +395,68 @@ data:
     losses = [float(r["Loss/Train/Step"]) for r in rows if r.get("Loss/Train/Step")]
     assert losses and all(x == x and x < 20 for x in losses)
     assert max(steps) >= 5, steps
+
+
+def _jsonl_losses(path, key):
+    import json
+    return [json.loads(l)[key] for l in open(path) if key in json.loads(l)]
+
+
+@pytest.mark.parametrize("objective", ["it", "dpo", "orpo"])
+def test_data_to_kernels_through_the_trainer(tmp_path, objective):
+    """Instruction tuning (chat template, group-by-length packing with segment ids, NEFTune) and DPO /
+    ORPO (paired chosen / rejected rows, frozen reference model) from JSON files through the data modules,
+    the Trainer (FSDP2 strategy, bf16-true) and the HIP kernels: finite losses, and the DPO loss starts at
+    log 2 (policy = reference)."""
+    import json
+    import math
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from helpers import toy_tokenizer
+
+    from llm_training_amd.runtime.loggers import JSONLLogger
+    from llm_training_amd.runtime.strategies import FSDP2Strategy
+    from llm_training_amd.runtime.trainer import Trainer
+
+    tok = toy_tokenizer()
+    model = {"model_class": "llm_training.models.Llama",
+             "model_config": {"vocab_size": 128, "hidden_size": 256, "intermediate_size": 512, "num_hidden_layers": 2,
+                              "num_attention_heads": 4, "num_key_value_heads": 2, "max_position_embeddings": 512}}
+    optim = {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 1e-3}}
+    if objective == "it":
+        from llm_training_amd.data.instruction_tuning import InstructionTuningDataModule
+        rows = [{"messages": [{"role": "user", "content": "hello world how are you " * (i % 7 + 1)},
+                              {"role": "assistant", "content": "fine thanks good answer " * (i % 5 + 1)}]}
+                for i in range(48)]
+        f = tmp_path / "it.jsonl"
+        f.write_text("\n".join(json.dumps(r) for r in rows))
+        dm = InstructionTuningDataModule({"dataset_kwargs": {"path": "json", "data_files": str(f)}, "tokenizer": tok,
+                                          "chat_template": "chatml", "max_length": 256,
+                                          "packing_method": "group_by_length", "overlong_handling_method": "truncate",
+                                          "batch_size": 2, "pad_to_multiple_of": 64, "enable_cache": False})
+        from llm_training_amd.lms.clm import CLM
+        lm = CLM({"model": model, "optim": optim, "neftune_alpha": 5.0})
+        key = "Loss/Train/Step"
+    else:
+        from llm_training_amd.data.preference_tuning import PreferenceTuningDataModule
+        rows = [{"chosen": [{"role": "user", "content": "question " * (i % 4 + 1)},
+                            {"role": "assistant", "content": "good answer yes " * (i % 3 + 1)}],
+                 "rejected": [{"role": "user", "content": "question " * (i % 4 + 1)},
+                              {"role": "assistant", "content": "bad no"}]} for i in range(24)]
+        f = tmp_path / "p.jsonl"
+        f.write_text("\n".join(json.dumps(r) for r in rows))
+        dm = PreferenceTuningDataModule({"dataset_kwargs": {"path": "json", "data_files": str(f)}, "tokenizer": tok,
+                                         "chat_template": "chatml", "batch_size": 2, "pad_to_multiple_of": 64,
+                                         "enable_cache": False})
+        from llm_training_amd.lms.preference import DPO, ORPO
+        lm = (DPO if objective == "dpo" else ORPO)({"model": model, "optim": optim, "beta": 0.1})
+        key = "Loss/Train/Step"
+    t = Trainer(strategy=FSDP2Strategy(), precision="bf16-true", logger=JSONLLogger(str(tmp_path / "log"), "r"),
+                max_steps=4, log_every_n_steps=1, gradient_clip_val=1.0, seed=3)
+    t.fit(lm, dm)
+    losses = _jsonl_losses(tmp_path / "log" / "r" / "metrics.jsonl", key)
+    assert len(losses) >= 3 and all(math.isfinite(x) for x in losses), losses
+    if objective == "dpo":
+        assert abs(losses[0] - math.log(2)) < 1e-2, losses
