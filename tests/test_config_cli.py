@@ -131,3 +131,63 @@ def test_container_recipes_reference_existing_files():
         assert os.path.exists(os.path.join(root, f)), f
     sh = open(os.path.join(root, "docker", "install.sh")).read()
     assert "python -m llm_training_amd._build" in sh and "gfx950" in sh
+
+
+def test_pre_process_then_fit_from_the_saved_data(tmp_path):
+    """`llm-training pre-process` on a YAML (local JSON data, a local HF tokenizer directory) writes the
+    processed datasets and info.txt; `llm-training fit` with the same YAML then trains from the saved data
+    (reference scripts/pre_process_data.py + pre_processed_data_path)."""
+    import json
+    import random
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from helpers import toy_tokenizer
+
+    from llm_training_amd.cli.main import main
+    tok_dir = tmp_path / "tok"
+    toy_tokenizer().save_pretrained(str(tok_dir))
+    rng = random.Random(0)
+    words = "hello world how are you the a of to and is it in that good bad yes no".split()
+    data = tmp_path / "d.jsonl"
+    data.write_text("\n".join(json.dumps({"text": " ".join(rng.choice(words) for _ in range(rng.randint(5, 40)))})
+                              for _ in range(80)))
+    cfg = tmp_path / "pt.yaml"
+    cfg.write_text(f"""
+seed_everything: 2
+trainer:
+  strategy: ddp
+  precision: 32-true
+  logger:
+    class_path: llm_training.lightning.CSVLogger
+    init_args: {{save_dir: {tmp_path}/logs, name: p}}
+  max_steps: 3
+  log_every_n_steps: 1
+model:
+  class_path: llm_training.lms.CLM
+  init_args.config:
+    model:
+      model_class: llm_training.models.Llama
+      model_config: {{vocab_size: 64, hidden_size: 32, intermediate_size: 64, num_hidden_layers: 1,
+                      num_attention_heads: 2, num_key_value_heads: 1}}
+    optim:
+      optimizer_class: torch.optim.AdamW
+      optimizer_kwargs: {{lr: 1e-2}}
+data:
+  class_path: llm_training.data.PreTrainingDataModule
+  init_args.config:
+    dataset_kwargs: {{path: json, data_files: {data}}}
+    tokenizer:
+      class_path: HFTokenizer
+      init_args: {{path: {tok_dir}}}
+    max_length: 32
+    packing_method: BEST_FIT_BIN_PACKING
+    batch_size: 2
+    pre_processed_data_path: {tmp_path}/processed
+""")
+    assert main(["pre-process", "--config", str(cfg)]) == 0
+    assert (tmp_path / "processed" / "info.txt").exists()
+    assert main(["fit", "--config", str(cfg)]) == 0
+    import csv
+    rows = list(csv.DictReader(open(tmp_path / "logs" / "p" / "metrics.csv")))
+    assert len(rows) == 3 and all(float(r["Loss/Train/Step"]) == float(r["Loss/Train/Step"]) for r in rows)
