@@ -495,13 +495,15 @@ class Trainer:
             d.update({k: float(v) for k, v in consumed.items()})
             if i == len(rows) - 1:
                 d.update(rates)
-            self.last_metrics = d
+            # the latest value of every metric (Lightning's callback_metrics): a validation loss logged
+            # at an earlier step stays visible to ModelCheckpoint(monitor=...) after later train rows
+            self.last_metrics.update(d)
             if self.is_global_zero:
                 for lg in self.loggers:
                     _call(lg, "log_metrics", d, step)
         if self.is_global_zero and self.enable_progress_bar:
             d = self.last_metrics
-            loss = next((d[k] for k in d if k.startswith("Loss/Train") or k == "Loss/Train/Step"), float("nan"))
+            loss = d.get("Loss/Train/Step", next((d[k] for k in d if k.startswith("Loss/Train")), float("nan")))
             logger.info("step %d | loss %.4f | lr %.3e | grad_norm %.3f | %.0f tok/s | %.1f TFLOP/s/gpu",
                         self.state.global_step, loss, d.get("lr", float("nan")), d.get("Gradient Norm", float("nan")),
                         d.get("Throughput/tokens_per_sec", float("nan")),

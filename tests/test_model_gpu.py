@@ -460,3 +460,65 @@ def test_data_to_kernels_through_the_trainer(tmp_path, objective):
     assert len(losses) >= 3 and all(math.isfinite(x) for x in losses), losses
     if objective == "dpo":
         assert abs(losses[0] - math.log(2)) < 1e-2, losses
+
+
+@pytest.mark.parametrize("arch", ["phi3", "hf-qwen2"])
+def test_it_trainer_validation_accumulation_best_checkpoint(tmp_path, arch):
+    """Packed instruction tuning through the Trainer on the HIP kernels for a Phi-3 (head_dim 96) and a
+    transformers Qwen2 model (the kernels through AttentionInterface), with a validation split,
+    validation every 2 steps, gradient accumulation 2 and ModelCheckpoint(monitor="Loss/Val", save_top_k=1):
+    finite train / validation losses, and exactly one complete best checkpoint kept."""
+    import json
+    import math
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from helpers import toy_tokenizer
+
+    from llm_training_amd.data.instruction_tuning import InstructionTuningDataModule
+    from llm_training_amd.lms.clm import CLM
+    from llm_training_amd.runtime.callbacks import ModelCheckpoint
+    from llm_training_amd.runtime.loggers import JSONLLogger
+    from llm_training_amd.runtime.strategies import FSDP2Strategy
+    from llm_training_amd.runtime.trainer import Trainer
+
+    tok = toy_tokenizer()
+    rows = [{"messages": [{"role": "user", "content": "hello world how are you " * (i % 7 + 1)},
+                          {"role": "assistant", "content": "fine thanks good answer " * (i % 5 + 1)}]}
+            for i in range(80)]
+    f = tmp_path / "it.jsonl"
+    f.write_text("\n".join(json.dumps(r) for r in rows))
+    dm = InstructionTuningDataModule({"dataset_kwargs": {"path": "json", "data_files": str(f)}, "tokenizer": tok,
+                                      "chat_template": "chatml", "max_length": 256, "validation_split": 0.2,
+                                      "packing_method": "group_by_length", "overlong_handling_method": "truncate",
+                                      "batch_size": 2, "pad_to_multiple_of": 64, "enable_cache": False})
+    if arch == "phi3":
+        model = {"model_class": "llm_training.models.Phi3",
+                 "model_config": {"vocab_size": 128, "hidden_size": 384, "intermediate_size": 768,
+                                  "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 4,
+                                  "max_position_embeddings": 512, "original_max_position_embeddings": 512,
+                                  "rope_scaling": None, "pad_token_id": 1}}
+    else:
+        model = {"model_class": "llm_training.models.HFCausalLM",
+                 "model_config": {"hf_config": {"model_type": "qwen2", "vocab_size": 128, "hidden_size": 256,
+                                                "intermediate_size": 512, "num_hidden_layers": 2,
+                                                "num_attention_heads": 4, "num_key_value_heads": 2,
+                                                "max_position_embeddings": 512}}}
+    lm = CLM({"model": model, "optim": {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 1e-3}},
+              "neftune_alpha": 5.0})
+    ck = ModelCheckpoint(dirpath=str(tmp_path / "ck"), every_n_train_steps=2, save_top_k=1, monitor="Loss/Val",
+                         mode="min")
+    t = Trainer(strategy=FSDP2Strategy(), precision="bf16-true", logger=JSONLLogger(str(tmp_path / "log"), "r"),
+                max_steps=4, log_every_n_steps=1, gradient_clip_val=1.0, accumulate_grad_batches=2,
+                val_check_interval=2, limit_val_batches=2, callbacks=[ck], seed=5)
+    t.fit(lm, dm)
+    rows = [json.loads(l) for l in open(tmp_path / "log" / "r" / "metrics.jsonl")]
+    train = [r["Loss/Train/Step"] for r in rows if "Loss/Train/Step" in r]
+    val = [r["Loss/Val"] for r in rows if "Loss/Val" in r]
+    assert len(train) >= 3 and all(math.isfinite(x) for x in train), train
+    assert val and all(math.isfinite(x) for x in val), rows
+    kept = [p for p in os.listdir(tmp_path / "ck") if p.endswith(".ckpt") and p != "last.ckpt"]
+    # step 2 saves before its validation runs (Lightning's order) and is unranked; step 4 is ranked by the
+    # step-2 validation loss, which stays visible after the later train rows, and is the one kept
+    assert len(kept) == 1 and kept[0].endswith("step=4.ckpt"), kept
