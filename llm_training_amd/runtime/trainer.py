@@ -133,6 +133,7 @@ class Trainer:
         if gradient_clip_algorithm != "norm":
             raise ValueError("only norm clipping is supported")
         self.val_check_interval = val_check_interval
+        self.check_val_every_n_epoch = check_val_every_n_epoch
         self.log_every_n_steps = max(1, int(log_every_n_steps))
         self.num_nodes = num_nodes
         self.limit_train_batches = limit_train_batches
@@ -362,14 +363,25 @@ class Trainer:
         return self
 
     def _should_validate(self, nbe: int) -> bool:
-        v = self.val_check_interval
-        if v is None or self.datamodule.datasets.get("validation") is None:
+        """Lightning's validation schedule, checked after each optimizer step: an int val_check_interval
+        counts training batches (micro-batches, so accumulation does not stretch it); a float — 1.0 when
+        unset, i.e. at the end of every epoch — is a fraction of the batches an epoch steps through,
+        gated by check_val_every_n_epoch."""
+        if self.datamodule.datasets.get("validation") is None:
             return False
-        if isinstance(v, float) and v <= 1.0:
-            every = max(1, int(nbe * v) // self.accumulate_grad_batches)
+        v = 1.0 if self.val_check_interval is None else self.val_check_interval
+        accum = self.accumulate_grad_batches
+        if isinstance(v, float):
+            if not 0.0 < v <= 1.0:
+                raise ValueError(f"val_check_interval as a float must be in (0, 1], got {v}")
+            n = self.check_val_every_n_epoch
+            if n is None or (self.state.epoch + 1) % int(n) != 0:
+                return False
+            every = max(1, int((nbe // accum) * accum * v))
         else:
-            every = int(v)
-        return self.state.global_step % every == 0
+            every = max(1, int(v))
+        done = self.state.batch_idx  # batches of this epoch stepped through, this step included
+        return done // every > (done - accum) // every
 
     def to_device(self, batch: dict) -> dict:
         out = {}

@@ -511,7 +511,7 @@ def test_it_trainer_validation_accumulation_best_checkpoint(tmp_path, arch):
                          mode="min")
     t = Trainer(strategy=FSDP2Strategy(), precision="bf16-true", logger=JSONLLogger(str(tmp_path / "log"), "r"),
                 max_steps=4, log_every_n_steps=1, gradient_clip_val=1.0, accumulate_grad_batches=2,
-                val_check_interval=2, limit_val_batches=2, callbacks=[ck], seed=5)
+                val_check_interval=4, limit_val_batches=2, callbacks=[ck], seed=5)  # every 4 batches = 2 steps
     t.fit(lm, dm)
     rows = [json.loads(l) for l in open(tmp_path / "log" / "r" / "metrics.jsonl")]
     train = [r["Loss/Train/Step"] for r in rows if "Loss/Train/Step" in r]

@@ -189,3 +189,29 @@ def test_csv_logger_one_header_across_resume_and_late_keys(tmp_path):
     rows = list(csv.DictReader(open(tmp_path / "r" / "metrics.csv")))
     assert [int(r["step"]) for r in rows] == [1, 2, 3, 4, 5]
     assert rows[3]["val"] == "0.75" and rows[0]["val"] == "" and rows[4]["loss"] == "0.6"
+
+
+def test_validation_schedule_follows_lightning():
+    """val_check_interval: an int counts training batches (accumulation does not stretch it), a float is a
+    fraction of the epoch (None = 1.0 = every epoch end) gated by check_val_every_n_epoch."""
+    from types import SimpleNamespace
+
+    from llm_training_amd.runtime.trainer import Trainer
+
+    def when(nbe=12, accum=1, epochs=2, **kw):
+        t = Trainer(strategy="ddp", precision="32-true", accumulate_grad_batches=accum, **kw)
+        t.datamodule = SimpleNamespace(datasets={"validation": [1]})
+        t.state.epoch, out = 0, []
+        for ep in range(epochs):
+            t.state.epoch, t.state.batch_idx = ep, 0
+            while t.state.batch_idx + accum <= nbe:
+                t.state.batch_idx += accum
+                if t._should_validate(nbe):
+                    out.append((ep, t.state.batch_idx))
+        return out
+
+    assert when(val_check_interval=4, accum=2) == [(0, 4), (0, 8), (0, 12), (1, 4), (1, 8), (1, 12)]
+    assert when() == [(0, 12), (1, 12)]                                  # default: every epoch end
+    assert when(nbe=13, accum=2) == [(0, 12), (1, 12)]                   # the dropped remainder batch
+    assert when(val_check_interval=0.5, accum=2) == [(0, 6), (0, 12), (1, 6), (1, 12)]
+    assert when(check_val_every_n_epoch=2) == [(1, 12)]
