@@ -85,8 +85,26 @@ class LossScaler:
 IGNORED_TRAINER_ARGS = {"num_sanity_val_steps", "benchmark", "fast_dev_run",
                         "overfit_batches", "profiler", "detect_anomaly", "barebones", "plugins",
                         "sync_batchnorm", "reload_dataloaders_every_n_epochs", "enable_model_summary",
-                        "inference_mode", "use_distributed_sampler", "min_epochs", "min_steps", "max_time",
+                        "inference_mode", "use_distributed_sampler", "min_epochs", "min_steps",
                         "limit_test_batches", "limit_predict_batches", "move_metrics_to_cpu"}
+
+
+def parse_max_time(v: Any) -> float | None:
+    """Lightning's ``max_time``: "DD:HH:MM:SS", a dict of timedelta fields, or a timedelta -> seconds."""
+    import datetime
+    if v is None:
+        return None
+    if isinstance(v, datetime.timedelta):
+        return v.total_seconds()
+    if isinstance(v, dict):
+        return datetime.timedelta(**v).total_seconds()
+    if isinstance(v, str):
+        parts = v.split(":")
+        if len(parts) != 4:
+            raise ValueError(f"max_time {v!r}: expected DD:HH:MM:SS")
+        d, h, m, sec = (float(x) for x in parts)
+        return datetime.timedelta(days=d, hours=h, minutes=m, seconds=sec).total_seconds()
+    raise TypeError(f"max_time must be a DD:HH:MM:SS string, a dict or a timedelta, got {type(v).__name__}")
 
 
 class TrainerState:
@@ -116,7 +134,8 @@ class Trainer:
                  devices: Any = "auto", accelerator: Any = "auto", limit_train_batches: Any = None,
                  limit_val_batches: Any = None, enable_checkpointing: bool = True, enable_progress_bar: bool = True,
                  default_root_dir: str = "logs", num_sanity_val_steps: int = 0, seed: int | None = None,
-                 deterministic: bool = False, benchmark: Any = None, gemm_tuning: str | None = None, **unused):
+                 deterministic: bool = False, benchmark: Any = None, gemm_tuning: str | None = None,
+                 max_time: Any = None, **unused):
         self.strategy: Strategy = resolve_strategy(strategy)
         # devices / num_nodes decide how many ranks llm_training_amd.launch starts; inside a rank the
         # accelerator picks the device type (cpu -> gloo ranks)
@@ -134,6 +153,8 @@ class Trainer:
             raise ValueError("only norm clipping is supported")
         self.val_check_interval = val_check_interval
         self.check_val_every_n_epoch = check_val_every_n_epoch
+        self.max_time = parse_max_time(max_time)  # seconds of fit time (Lightning Timer), None = unlimited
+        self._fit_t0 = 0.0
         self.log_every_n_steps = max(1, int(log_every_n_steps))
         self.num_nodes = num_nodes
         self.limit_train_batches = limit_train_batches
@@ -331,6 +352,7 @@ class Trainer:
                 _call(cb, "teardown", self, lm)
 
     def _fit(self, lm, datamodule=None, ckpt_path: str | None = None):
+        self._fit_t0 = time.monotonic()
         self.setup(lm, datamodule, ckpt_path)
         for cb in self.callbacks:
             _call(cb, "on_fit_start", self, lm)
@@ -346,11 +368,18 @@ class Trainer:
                 self.train_step(batches)  # advances batch_idx before the batch-end callbacks run
                 if self.max_steps > 0 and self.state.global_step >= self.max_steps:
                     self.should_stop = True
+                if self.max_time is not None and self._time_is_up():
+                    self.should_stop = True
                 if self._should_validate(nbe):
                     self.validate()
-            if self.state.batch_idx + accum > nbe:  # epoch completed (not an early stop mid-epoch)
+            epoch_done = self.state.batch_idx + accum > nbe
+            if epoch_done or self.should_stop:
+                # Lightning ends the epoch loop also when max_steps / max_time stop it early, so the
+                # epoch-end hooks (ModelCheckpoint(save_on_train_epoch_end) among them) run; the counters
+                # only advance for a completed epoch, so a resume continues mid-epoch
                 for cb in self.callbacks:
                     _call(cb, "on_train_epoch_end", self, lm)
+            if epoch_done:
                 self.state.epoch += 1
                 self.state.batch_idx = 0
         self._flush_logs(force=True)
@@ -361,6 +390,16 @@ class Trainer:
         for lg in self.loggers:
             _call(lg, "finalize", "success")
         return self
+
+    def _time_is_up(self) -> bool:
+        """max_time reached? Rank 0's clock decides for every rank (Lightning's Timer broadcasts its
+        decision), so all ranks leave the loop after the same step."""
+        up = time.monotonic() - self._fit_t0 >= self.max_time
+        if self.pc is not None and self.pc.world_size > 1:
+            t = torch.tensor([1.0 if up else 0.0], device=self.device)
+            dist.broadcast(t, src=0)
+            up = bool(t.item())
+        return up
 
     def _should_validate(self, nbe: int) -> bool:
         """Lightning's validation schedule, checked after each optimizer step: an int val_check_interval

@@ -25,14 +25,17 @@ def test_lr_schedules_match_reference_formulas():
     assert abs(lin.lr_at(0) - 0.25) < 1e-9 and abs(lin.lr_at(13)) < 1e-9 and abs(lin.lr_at(8) - 0.5) < 1e-9
 
 
-def _lm(seed=0):
+def _lm(seed=0, total_steps=None):
+    sched = {"num_warmup_steps": 2, "min_lr": 1e-4}
+    if total_steps is not None:
+        sched["num_total_steps"] = total_steps
     return CLM({"model": {"model_class": "llm_training.models.Llama",
                           "model_config": {"vocab_size": 96, "hidden_size": 32, "intermediate_size": 64,
                                            "num_hidden_layers": 2, "num_attention_heads": 4,
                                            "num_key_value_heads": 2}},
                 "optim": {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 5e-3},
                           "lr_scheduler_class": "llm_training.lr_schedulers.CosineAnnealingWarmupLR",
-                          "lr_scheduler_kwargs": {"num_warmup_steps": 2, "min_lr": 1e-4}}})
+                          "lr_scheduler_kwargs": sched}})
 
 
 def _dm():
@@ -228,3 +231,39 @@ def test_convert_deepspeed_zero3_merges_frozen_fragments(tmp_path):
     got = load_file(os.path.join(out, "model.safetensors"))
     for k, v in hf.items():
         assert torch.equal(got[k], v.float()), k
+
+
+def test_early_stop_runs_epoch_end_checkpoint_and_resumes_mid_epoch(tmp_path):
+    """max_steps stopping mid-epoch still runs the epoch-end hooks (Lightning), so a reference-style
+    ModelCheckpoint(save_on_train_epoch_end=True) writes the final state; resuming from it continues in
+    the same epoch, step for step equal to an uninterrupted run."""
+    log_full, log_a, log_b = tmp_path / "full", tmp_path / "a", tmp_path / "b"
+    Trainer(strategy="ddp", precision="32-true", logger=JSONLLogger(str(log_full), "r"), max_steps=8,
+            log_every_n_steps=1, seed=3).fit(_lm(total_steps=8), _dm())
+    t = Trainer(strategy="ddp", precision="32-true", logger=JSONLLogger(str(log_a), "r"), max_steps=5,
+                log_every_n_steps=1, seed=3,
+                callbacks=[ModelCheckpoint(dirpath=str(tmp_path / "ck"), save_on_train_epoch_end=True)])
+    t.fit(_lm(total_steps=8), _dm())
+    ck = tmp_path / "ck" / "epoch=0-step=5.ckpt"
+    assert (ck / "meta.json").exists() and t.state.epoch == 0 and t.state.batch_idx == 5
+    Trainer(strategy="ddp", precision="32-true", logger=JSONLLogger(str(log_b), "r"), max_steps=8,
+            log_every_n_steps=1, seed=3).fit(_lm(total_steps=8), _dm(), ckpt_path=str(ck))
+    full, resumed = _losses(log_full / "r"), _losses(log_b / "r")
+    assert sorted(resumed) == [6, 7, 8]
+    for s in resumed:
+        assert abs(resumed[s] - full[s]) < 1e-5, (s, resumed[s], full[s])
+
+
+def test_max_time():
+    import datetime
+
+    from llm_training_amd.runtime.trainer import parse_max_time
+    assert parse_max_time("00:12:00:00") == 12 * 3600
+    assert parse_max_time({"days": 1, "minutes": 30}) == 86400 + 1800
+    assert parse_max_time(datetime.timedelta(seconds=90)) == 90
+    assert parse_max_time(None) is None
+    with pytest.raises(ValueError):
+        parse_max_time("12:00")
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=20, max_time={"seconds": 0}, seed=1)
+    t.fit(_lm(total_steps=8), _dm())
+    assert t.global_step == 1  # time is checked after each optimizer step, as Lightning's Timer does
