@@ -1,6 +1,8 @@
 """Memory-bound kernels of the Llama-3-8B step at 32768 tokens: SwiGLU forward / backward (row-blocked vs
 flat grid-stride kernels, LLMT_EW_ROWS read per call, interleaved in one process) and RMSNorm forward /
-backward (+ residual). Prints ms and achieved TB/s (bytes the kernel must move / time).
+backward (+ residual), RoPE in place on the q / k heads of the fused QKV buffer (token-blocked vs flat,
+LLMT_ROPE_ROWS; Llama-3-8B 32 + 8 heads of 128 and Phi-3-mini 32 + 32 heads of 96, packed positions).
+Prints ms and achieved TB/s (bytes the kernel must move / time).
     python benchmarks/bench_elementwise.py"""
 import json
 import os
@@ -46,9 +48,22 @@ y, r_out, rstd = L.rmsnorm_fwd(x, res, w, 1e-5)
 out["rmsnorm_fwd_res_ms"] = [timed(lambda: L.rmsnorm_fwd(x, res, w, 1e-5))]
 dy = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
 out["rmsnorm_bwd_res_ms"] = [timed(lambda: L.rmsnorm_bwd(dy, r_out, w, rstd, res, None, False, True))]
+from llm_training_amd.ops.rope_utils import compute_rope_tables  # noqa: E402
+rope_gb = {}
+for name, hq, hkv, D in (("llama", 32, 8, 128), ("phi3", 32, 32, 96)):
+    qkv = torch.randn(T, hq + 2 * hkv, D, device="cuda", dtype=torch.bfloat16)
+    pos = (torch.arange(T, device="cuda") % 1024).contiguous()  # packed documents of 1024 tokens
+    cos, sin = compute_rope_tables(D, 4096, 10000.0, device="cuda")
+    rope_gb[f"rope_{name}"] = T * (hq + hkv) * D * 2 * 2 / 1e9
+    for rnd in range(3):
+        for mode in ("1", "0"):
+            os.environ["LLMT_ROPE_ROWS"] = mode
+            out.setdefault(f"rope_{name}_ms_rows{mode}", []).append(
+                timed(lambda: L.rope_(qkv, pos, cos, sin, hq + hkv, False)))
+    os.environ.pop("LLMT_ROPE_ROWS")
 res_j = {k: round(sorted(v)[len(v) // 2], 4) for k, v in out.items()}
 gb = {"swiglu_fwd": T * I * 2 * 3 / 1e9, "swiglu_bwd": T * I * 2 * 5 / 1e9, "rmsnorm_fwd_res": T * H * 2 * 4 / 1e9,
-      "rmsnorm_bwd_res": T * H * 2 * 4 / 1e9}
+      "rmsnorm_bwd_res": T * H * 2 * 4 / 1e9, **rope_gb}
 for k, v in list(res_j.items()):
     base = next(n for n in gb if k.startswith(n))
     res_j[k.replace("_ms", "_tbs")] = round(gb[base] / v, 2)

@@ -137,9 +137,61 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const
   }
 }
 
+// Token-blocked form (default): a 64 x 4 block rotates 4 tokens, the 64 lanes of a row walking that
+// token's (head, 8-pair group) items; the position and its table row are read once per item from L1
+// and there is no 64-bit division per item (the flat form divides a 64-bit index three times)
+template <typename PosT>
+__global__ __launch_bounds__(256) void rope_rows_kernel(bf16* __restrict__ qkv, const PosT* __restrict__ pos,
+                                                        const float* __restrict__ cos_t,
+                                                        const float* __restrict__ sin_t, int64_t T, int nheads, int D,
+                                                        int64_t stride_t, int stride_h, float sign, int64_t P,
+                                                        int* __restrict__ err) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + threadIdx.y;
+  if (t >= T) return;
+  const int half = D >> 1;
+  const int groups = half >> 3;
+  int64_t p = (int64_t)pos[t];
+  if (p < 0 || p >= P) {
+    if (err && threadIdx.x == 0) err[0] = 1;
+    p = p < 0 ? 0 : P - 1;
+  }
+  bf16* row = qkv + t * stride_t;
+  const float* crow = cos_t + p * half;
+  const float* srow = sin_t + p * half;
+  for (int it = threadIdx.x; it < nheads * groups; it += 64) {
+    const int h = it / groups;
+    const int g = it - h * groups;
+    bf16* base = row + h * stride_h + g * 8;
+    bf16x8* lo = reinterpret_cast<bf16x8*>(base);
+    bf16x8* hi = reinterpret_cast<bf16x8*>(base + half);
+    float c[8], s[8];
+    *reinterpret_cast<float4*>(c) = reinterpret_cast<const float4*>(crow + g * 8)[0];
+    *reinterpret_cast<float4*>(c + 4) = reinterpret_cast<const float4*>(crow + g * 8)[1];
+    *reinterpret_cast<float4*>(s) = reinterpret_cast<const float4*>(srow + g * 8)[0];
+    *reinterpret_cast<float4*>(s + 4) = reinterpret_cast<const float4*>(srow + g * 8)[1];
+    float x1[8], x2[8], y1[8], y2[8];
+    unpack8(*lo, x1);
+    unpack8(*hi, x2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sn = sign * s[i];
+      y1[i] = x1[i] * c[i] - x2[i] * sn;
+      y2[i] = x2[i] * c[i] + x1[i] * sn;
+    }
+    *lo = pack8(y1);
+    *hi = pack8(y2);
+  }
+}
+
 }  // namespace llmt
 
 using namespace llmt;
+
+// LLMT_ROPE_ROWS=0 selects the flat grid-stride RoPE kernel (read per call, for A/B runs)
+static bool rope_rows() {
+  const char* e = getenv("LLMT_ROPE_ROWS");
+  return !(e && e[0] == '0');
+}
 
 // LLMT_EW_ROWS=0 selects the flat grid-stride SwiGLU kernels (read per call, for A/B runs)
 static bool ew_rows(int64_t T) {
@@ -188,8 +240,18 @@ extern "C" hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const
   if (D % 16 || P <= 0) return hipErrorInvalidValue;
   const int64_t total = T * nheads * (D / 16);
   if (total == 0) return hipSuccess;
-  const int grid = stream_grid(total, 256);
   const float sign = inverse ? -1.f : 1.f;
+  if (rope_rows()) {  // 4 tokens per 256-thread block; grid.x <= 2^31 - 1 holds for any T we address
+    const dim3 grid((unsigned)((T + 3) / 4)), block(64, 4);
+    if (pos_is_64)
+      rope_rows_kernel<int64_t><<<grid, block, 0, stream>>>((bf16*)qkv, (const int64_t*)pos, cos_t, sin_t, T, nheads,
+                                                            D, stride_t, stride_h, sign, P, err);
+    else
+      rope_rows_kernel<int32_t><<<grid, block, 0, stream>>>((bf16*)qkv, (const int32_t*)pos, cos_t, sin_t, T, nheads,
+                                                            D, stride_t, stride_h, sign, P, err);
+    return hipGetLastError();
+  }
+  const int grid = stream_grid(total, 256);
   if (pos_is_64)
     rope_kernel<int64_t><<<grid, 256, 0, stream>>>((bf16*)qkv, (const int64_t*)pos, cos_t, sin_t, T, nheads, D,
                                                    stride_t, stride_h, sign, P, err);

@@ -84,6 +84,39 @@ def test_rope_inplace_roundtrip(D):
     assert _rel(x, qkv) < 2e-2
 
 
+@pytest.mark.parametrize("D", [64, 96, 128])
+def test_rope_token_blocked_equals_flat(D, monkeypatch):
+    """The token-blocked RoPE kernel (default) is bitwise equal to the flat grid-stride one, on a token
+    count that is not a multiple of its 4-token block, int32 and int64 positions, forward and inverse;
+    an out-of-table position is clamped and flagged by both."""
+    from llm_training_amd.ops.native import check_kernel_errors
+    torch.manual_seed(0)
+    T, H = 1023, 10
+    qkv = torch.randn(T, H, D, device=DEV, dtype=torch.bfloat16)
+    cos, sin = compute_rope_tables(D, 2048, 10000.0, device=DEV)
+    for pos in (torch.randint(0, 2048, (T,), device=DEV), torch.randint(0, 2048, (T,), device=DEV).int()):
+        for inv in (False, True):
+            out = {}
+            for mode in ("1", "0"):
+                monkeypatch.setenv("LLMT_ROPE_ROWS", mode)
+                x = qkv.clone()
+                lib().rope_(x, pos, cos, sin, 6, inv)
+                out[mode] = x
+            assert torch.equal(out["1"], out["0"])
+            assert torch.equal(out["1"][:, 6:], qkv[:, 6:])
+    bad = torch.randint(0, 2048, (T,), device=DEV)
+    bad[7] = 5000
+    monkeypatch.setenv("LLMT_ROPE_ROWS", "1")
+    x = qkv.clone()
+    lib().rope_(x, bad, cos, sin, 6, False)
+    assert check_kernel_errors(raise_error=False), "out-of-table position not flagged"
+    monkeypatch.setenv("LLMT_ROPE_ROWS", "0")
+    y = qkv.clone()
+    lib().rope_(y, bad, cos, sin, 6, False)
+    assert torch.equal(x, y)
+    check_kernel_errors(raise_error=False)
+
+
 def test_swiglu_bwd_with_transposed_gradient(monkeypatch):
     """swiglu_bwd_tr: dgu equal to swiglu_bwd bitwise and dgu^T its exact transpose; through the ops, the
     gate_up weight gradient takes it (TN) and matches the path without it."""
