@@ -29,6 +29,10 @@ FUSED = {
     "llm_training.optim.FusedAdamW": "adamw",
     "deepspeed.ops.adam.FusedAdam": "deepspeed",
     "deepspeed.ops.adam.fused_adam.FusedAdam": "deepspeed",
+    # DeepSpeed's host Adam (used with optimizer offload): the same math; with an offloading strategy
+    # the engine runs its own threaded host AdamW (csrc/cpu_adam.cpp), on the GPU the fused kernel
+    "deepspeed.ops.adam.DeepSpeedCPUAdam": "deepspeed",
+    "deepspeed.ops.adam.cpu_adam.DeepSpeedCPUAdam": "deepspeed",
 }
 SUPPORTED = FUSED  # backwards-compatible name
 
@@ -58,7 +62,8 @@ def resolve_optimizer(name: str, kwargs: dict) -> dict:
             raise ValueError("deepspeed FusedAdam does not support amsgrad (neither does the fused AdamW)")
         if not _truthy(kw.pop("bias_correction", True)):
             raise ValueError("FusedAdam(bias_correction=False) is not supported by the fused AdamW")
-        adam_w = _truthy(kw.pop("adam_w_mode", True))
+        adam_w = _truthy(kw.pop("adam_w_mode", kw.pop("adamw_mode", True)))  # FusedAdam / DeepSpeedCPUAdam
+        kw.pop("fp32_optimizer_states", None)  # DeepSpeedCPUAdam: states are fp32 here anyway
         kw.pop("amsgrad", None)
         if not adam_w and float(kw.get("weight_decay", 0.0)) != 0.0:
             raise ValueError("FusedAdam(adam_w_mode=False) with L2 weight decay is not supported; use AdamW")

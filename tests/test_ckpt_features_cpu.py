@@ -175,6 +175,11 @@ def test_optimizer_resolution():
     from llm_training_amd.optim import resolve_optimizer
     assert resolve_optimizer("torch.optim.AdamW", {"lr": 1e-3})["kind"] == "fused"
     assert resolve_optimizer("deepspeed.ops.adam.FusedAdam", {"lr": 1e-3})["weight_decay"] == 0.0
+    cpu_adam = resolve_optimizer("deepspeed.ops.adam.DeepSpeedCPUAdam",
+                                 {"lr": 1e-3, "adamw_mode": True, "weight_decay": 0.1, "fp32_optimizer_states": True})
+    assert cpu_adam["kind"] == "fused" and cpu_adam["weight_decay"] == 0.1
+    with pytest.raises(ValueError):
+        resolve_optimizer("deepspeed.ops.adam.DeepSpeedCPUAdam", {"lr": 1e-3, "adamw_mode": False, "weight_decay": 0.1})
     hp = resolve_optimizer("torch.optim.AdamW", {"lr": 1e-3, "amsgrad": True})
     assert hp["kind"] == "generic" and hp["cls"] is torch.optim.AdamW and hp["kwargs"]["amsgrad"] is True
     assert resolve_optimizer("torch.optim.Adam", {"lr": 1e-3, "weight_decay": 0.1})["kind"] == "generic"
