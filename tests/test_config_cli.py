@@ -191,3 +191,48 @@ data:
     import csv
     rows = list(csv.DictReader(open(tmp_path / "logs" / "p" / "metrics.csv")))
     assert len(rows) == 3 and all(float(r["Loss/Train/Step"]) == float(r["Loss/Train/Step"]) for r in rows)
+
+
+def test_cli_validate_from_checkpoint_matches_fit(tmp_path):
+    """``llm-training validate --ckpt_path <ckpt>`` restores the trained weights and reproduces the
+    validation loss the fit logged at the same step."""
+    import json
+
+    from llm_training_amd.cli.main import cmd_validate, main
+    cfg = tmp_path / "tiny.yaml"
+    cfg.write_text(f"""
+seed_everything: 1
+trainer:
+  strategy: ddp
+  precision: 32-true
+  logger:
+    class_path: JSONLLogger
+    init_args: {{save_dir: {tmp_path}/logs, name: v}}
+  max_steps: 3
+  log_every_n_steps: 1
+  val_check_interval: 3
+  callbacks:
+    - class_path: ModelCheckpoint
+      init_args: {{dirpath: {tmp_path}/ck, every_n_train_steps: 3}}
+model:
+  class_path: llm_training.lms.CLM
+  init_args.config:
+    model:
+      model_class: llm_training.models.Llama
+      model_config: {{vocab_size: 64, hidden_size: 32, intermediate_size: 64, num_hidden_layers: 1,
+                      num_attention_heads: 2, num_key_value_heads: 1}}
+    optim:
+      optimizer_class: torch.optim.AdamW
+      optimizer_kwargs: {{lr: 1e-2}}
+data:
+  class_path: llm_training.data.DummyDataModule
+  init_args.config: {{batch_size: 2, vocab_size: 64, max_length: 16, num_samples: 48, base_seed: 3,
+                     validation_split: 8}}
+""")
+    assert main(["fit", "--config", str(cfg)]) == 0
+    rows = [json.loads(x) for x in open(tmp_path / "logs" / "v" / "metrics.jsonl")]
+    fit_val = [r["Loss/Val"] for r in rows if "Loss/Val" in r]
+    assert len(fit_val) == 1
+    ck = tmp_path / "ck" / "epoch=0-step=3.ckpt"
+    out = cmd_validate(["--config", str(cfg), "--ckpt_path", str(ck)])
+    assert out["Loss/Val"] == pytest.approx(fit_val[0], rel=1e-5)
