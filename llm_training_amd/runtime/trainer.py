@@ -82,7 +82,7 @@ class LossScaler:
         self.scale, self.good_steps, self.skipped = float(st["scale"]), int(st["good_steps"]), int(st["skipped"])
 # Lightning Trainer arguments that exist upstream but have no effect here: accepted (with a warning)
 # so reference configs load; anything else is a typo and raises, as jsonargparse would
-IGNORED_TRAINER_ARGS = {"num_sanity_val_steps", "benchmark", "fast_dev_run",
+IGNORED_TRAINER_ARGS = {"benchmark", "fast_dev_run",
                         "overfit_batches", "profiler", "detect_anomaly", "barebones", "plugins",
                         "sync_batchnorm", "reload_dataloaders_every_n_epochs", "enable_model_summary",
                         "inference_mode", "use_distributed_sampler", "min_epochs", "min_steps",
@@ -133,7 +133,7 @@ class Trainer:
                  check_val_every_n_epoch: int | None = 1, log_every_n_steps: int = 10, num_nodes: int = 1,
                  devices: Any = "auto", accelerator: Any = "auto", limit_train_batches: Any = None,
                  limit_val_batches: Any = None, enable_checkpointing: bool = True, enable_progress_bar: bool = True,
-                 default_root_dir: str = "logs", num_sanity_val_steps: int = 0, seed: int | None = None,
+                 default_root_dir: str = "logs", num_sanity_val_steps: int = 2, seed: int | None = None,
                  deterministic: bool = False, benchmark: Any = None, gemm_tuning: str | None = None,
                  max_time: Any = None, **unused):
         self.strategy: Strategy = resolve_strategy(strategy)
@@ -159,6 +159,7 @@ class Trainer:
         self.num_nodes = num_nodes
         self.limit_train_batches = limit_train_batches
         self.limit_val_batches = limit_val_batches
+        self.num_sanity_val_steps = int(num_sanity_val_steps)  # Lightning: -1 = the whole validation set
         self.enable_checkpointing = enable_checkpointing
         self.enable_progress_bar = enable_progress_bar
         self.default_root_dir = default_root_dir
@@ -356,6 +357,11 @@ class Trainer:
         self.setup(lm, datamodule, ckpt_path)
         for cb in self.callbacks:
             _call(cb, "on_fit_start", self, lm)
+        if self.num_sanity_val_steps != 0 and self.limit_val_batches not in (0, 0.0):
+            # Lightning's sanity check: a few validation batches before the first training step, so a
+            # broken validation path fails at once rather than after the first val_check_interval;
+            # nothing is logged or kept
+            self.validate(sanity=True)
         max_epochs = self.max_epochs if self.max_epochs is not None else (1 if self.max_steps <= 0 else 10 ** 9)
         lm.train()
         nbe = self.num_batches_per_epoch()
@@ -562,15 +568,33 @@ class Trainer:
         self._log_buffer.clear()
 
     @torch.no_grad()
-    def validate(self):
+    def _val_batch_limit(self, dl, sanity: bool) -> int | None:
+        """Batches to run (None = all): Lightning's limit_val_batches (an int count or a float fraction of
+        the loader), or num_sanity_val_steps (-1 = all) for the sanity check."""
+        if sanity:
+            return None if self.num_sanity_val_steps < 0 else self.num_sanity_val_steps
+        lim = self.limit_val_batches
+        if lim is None or (isinstance(lim, float) and lim >= 1.0):
+            return None
+        if isinstance(lim, float):
+            try:
+                return int(len(dl) * lim)
+            except TypeError:  # a loader without a length: a fraction cannot be applied
+                return None
+        return int(lim)
+
+    def validate(self, sanity: bool = False):
+        if self.datamodule.datasets.get("validation") is None:
+            return {}
         dl = self.datamodule.val_dataloader(self.pc.dp_rank, self.pc.dp_size)
         if dl is None:
             return {}
+        limit = self._val_batch_limit(dl, sanity)
         self.lm.eval()
         sums: dict[str, torch.Tensor] = {}
         n = 0
         for i, b in enumerate(dl):
-            if self.limit_val_batches is not None and i >= int(self.limit_val_batches):
+            if limit is not None and i >= limit:
                 break
             m = self.lm.validation_step(self.to_device(b), i)
             for k, v in m.items():
@@ -587,6 +611,9 @@ class Trainer:
         out = dict(zip(keys, vec.cpu().tolist()))
         if "Loss/Val" in out and "Perplexity/Val" in out:
             out["Perplexity/Val"] = math.exp(out["Loss/Val"])
+        if sanity:
+            logger.info("validation sanity check (%d batches): %s", n, out)
+            return out
         self.last_metrics.update(out)  # visible to ModelCheckpoint(monitor="Loss/Val")
         if self.is_global_zero:
             for lg in self.loggers:

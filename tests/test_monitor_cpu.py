@@ -215,3 +215,46 @@ def test_validation_schedule_follows_lightning():
     assert when(nbe=13, accum=2) == [(0, 12), (1, 12)]                   # the dropped remainder batch
     assert when(val_check_interval=0.5, accum=2) == [(0, 6), (0, 12), (1, 6), (1, 12)]
     assert when(check_val_every_n_epoch=2) == [(1, 12)]
+
+
+def test_sanity_check_and_fractional_val_limit(monkeypatch):
+    """num_sanity_val_steps (Lightning default 2) runs that many validation batches before training
+    without logging them; limit_val_batches as a float is a fraction of the loader, 0 disables both."""
+    from types import SimpleNamespace
+
+    from llm_training_amd.runtime.trainer import Trainer
+
+    t = Trainer(strategy="ddp", precision="32-true")
+    dl = list(range(10))
+    assert t._val_batch_limit(dl, sanity=True) == 2 and t._val_batch_limit(dl, sanity=False) is None
+    t.limit_val_batches = 0.5
+    assert t._val_batch_limit(dl, sanity=False) == 5
+    t.limit_val_batches = 1.0
+    assert t._val_batch_limit(dl, sanity=False) is None
+    t.limit_val_batches = 3
+    assert t._val_batch_limit(dl, sanity=False) == 3
+    t.num_sanity_val_steps = -1
+    assert t._val_batch_limit(dl, sanity=True) is None
+
+    calls = []
+
+    class LM:
+        def eval(self):
+            pass
+
+        def train(self, mode=True):
+            pass
+
+        def validation_step(self, b, i):
+            calls.append(i)
+            return {"Loss/Val": __import__("torch").tensor(1.0)}
+
+    t2 = Trainer(strategy="ddp", precision="32-true")
+    t2.lm = LM()
+    t2.pc = SimpleNamespace(dp_rank=0, dp_size=1, world_size=1, rank=0)
+    t2.device = __import__("torch").device("cpu")
+    t2.datamodule = SimpleNamespace(datasets={"validation": [0]}, val_dataloader=lambda r, s: [{"x": 1}] * 7)
+    out = t2.validate(sanity=True)
+    assert calls == [0, 1] and out == {"Loss/Val": 1.0} and "Loss/Val" not in t2.last_metrics
+    t2.validate()
+    assert len(calls) == 9 and t2.last_metrics["Loss/Val"] == 1.0
