@@ -267,3 +267,44 @@ def test_max_time():
     t = Trainer(strategy="ddp", precision="32-true", max_steps=20, max_time={"seconds": 0}, seed=1)
     t.fit(_lm(total_steps=8), _dm())
     assert t.global_step == 1  # time is checked after each optimizer step, as Lightning's Timer does
+
+
+def test_convert_to_hf_roundtrip_phi3_longrope(tmp_path):
+    """A trained Phi-3 (fused qkv / gate_up, LongRoPE, sliding window) exported by convert-to-hf loads in
+    transformers' Phi3ForCausalLM with the same logits, past the original context (long factors)."""
+    from transformers import AutoModelForCausalLM
+
+    from llm_training_amd.tools.convert_to_hf import convert
+    rs = {"type": "longrope", "short_factor": [1.0 + 0.1 * i for i in range(8)],
+          "long_factor": [2.0 + 0.3 * i for i in range(8)]}
+    lm = CLM({"model": {"model_class": "llm_training.models.Phi3",
+                        "model_config": {"vocab_size": 96, "hidden_size": 64, "intermediate_size": 96,
+                                         "num_hidden_layers": 2, "num_attention_heads": 4,
+                                         "num_key_value_heads": 4, "max_position_embeddings": 256,
+                                         "original_max_position_embeddings": 32, "rope_scaling": rs,
+                                         "sliding_window": 48, "pad_token_id": 0, "eos_token_id": 1,
+                                         "bos_token_id": 2}},
+              "optim": {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 5e-3}}})
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=2, seed=1, default_root_dir=str(tmp_path))
+    t.fit(lm, DummyDataModule({"batch_size": 2, "vocab_size": 96, "max_length": 64, "num_samples": 16,
+                               "base_seed": 5}))
+    ck = tmp_path / "ck"
+    t.save_checkpoint(str(ck))
+    out = convert(str(ck), str(tmp_path / "hf"), dtype="float32")
+    import json
+    exported = json.loads((tmp_path / "hf" / "config.json").read_text())
+    assert exported["sliding_window"] == 48  # the config value is exported unchanged, as the reference does
+    # the window counts like flash-attn's window_size=(W, W) in the reference (attention_op.py:588, and its
+    # eager mask :160-163): keys q-W..q, W+1 of them; transformers 5 counts W keys (kv > q - W), so
+    # the same model needs W+1 there
+    hf = AutoModelForCausalLM.from_pretrained(out, local_files_only=True, attn_implementation="eager",
+                                              sliding_window=49)
+    assert type(hf).__name__ == "Phi3ForCausalLM"
+    hf.eval()
+    lm.model.eval()
+    for S in (24, 80):  # inside and past original_max_position_embeddings
+        ids = torch.randint(3, 96, (2, S))
+        with torch.no_grad():
+            a = lm.model(input_ids=ids).logits
+            b = hf(input_ids=ids).logits
+        assert torch.allclose(a, b, atol=2e-4), (S, (a - b).abs().max())
