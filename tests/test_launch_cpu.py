@@ -75,6 +75,19 @@ def test_fit_devices_2_spawns_two_gloo_ranks_matching_one_process(tmp_path):
     assert g2 == pytest.approx(g1, rel=1e-4, abs=1e-5)
 
 
+def test_max_time_stops_every_rank_at_the_same_step(tmp_path):
+    """max_time on two gloo ranks: rank 0's clock decides (broadcast), so both ranks stop after the
+    same optimizer step and the job exits cleanly instead of one rank waiting in a collective."""
+    cfg = tmp_path / "mt.yaml"
+    cfg.write_text(TINY.format(out=tmp_path / "mt", bs=1).replace("max_steps: 4", "max_steps: 50\n  max_time: {seconds: 0}"))
+    r = subprocess.run([sys.executable, "-m", "llm_training_amd.cli.main", "fit", "--config", str(cfg),
+                        "--trainer.devices", "2", "--trainer.accelerator", "cpu"],
+                       env=_env(), cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    losses, _ = _losses(tmp_path / "mt" / "t" / "metrics.csv")
+    assert len(losses) == 1
+
+
 def test_failing_rank_ends_the_job_without_orphans(tmp_path):
     """Rank 1 fails at once while rank 0 would block for minutes: the parent returns rank 1's code
     within the grace period and rank 0 is gone."""
