@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
   for (int row = row0 + wid; row < row1; row += 4) {
     const int64_t base = (int64_t)row * H8;
     const float r = rstd[row];
-    bf16x8 xv[NC], gv[NC];
+    bf16x8 xv[NC], gv[NC], rv[NC];
     float dot = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -95,6 +95,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       if (col < H8) {
         xv[c] = x[base + col];
         gv[c] = dy[base + col];
+        // the residual gradient is read with x / dy, ahead of the row's reduction (not behind it)
+        if constexpr (DRES) rv[c] = dres[base + col];
         float xf[8], g[8], wf[8], nf[8];
         unpack8(xv[c], xf);
         unpack8(gv[c], g);
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
         for (int i = 0; i < 8; ++i) o[i] = r * (g[i] * wf[i] - xf[i] * r * dot);
         if constexpr (DRES) {
           float d2[8];
-          unpack8(dres[base + col], d2);
+          unpack8(rv[c], d2);
 #pragma unroll
           for (int i = 0; i < 8; ++i) o[i] += d2[i];
         }
