@@ -1,7 +1,7 @@
 """Memory-bound kernels of the Llama-3-8B step at 32768 tokens: SwiGLU forward / backward (row-blocked vs
 flat grid-stride kernels, LLMT_EW_ROWS read per call, interleaved in one process) and RMSNorm forward /
-backward (+ residual), RoPE in place on the q / k heads of the fused QKV buffer (token-blocked vs flat,
-LLMT_ROPE_ROWS; Llama-3-8B 32 + 8 heads of 128 and Phi-3-mini 32 + 32 heads of 96, packed positions).
+backward (+ residual), RoPE in place on the q / k heads of the fused QKV buffer (token-blocked / flat / LDS-staged,
+LLMT_ROPE_KERNEL; Llama-3-8B 32 + 8 heads of 128 and Phi-3-mini 32 + 32 heads of 96, packed positions).
 Prints ms and achieved TB/s (bytes the kernel must move / time).
     python benchmarks/bench_elementwise.py"""
 import json
@@ -56,11 +56,11 @@ for name, hq, hkv, D in (("llama", 32, 8, 128), ("phi3", 32, 32, 96)):
     cos, sin = compute_rope_tables(D, 4096, 10000.0, device="cuda")
     rope_gb[f"rope_{name}"] = T * (hq + hkv) * D * 2 * 2 / 1e9
     for rnd in range(3):
-        for mode in ("1", "0"):
-            os.environ["LLMT_ROPE_ROWS"] = mode
-            out.setdefault(f"rope_{name}_ms_rows{mode}", []).append(
+        for mode in ("rows", "flat", "lds"):
+            os.environ["LLMT_ROPE_KERNEL"] = mode
+            out.setdefault(f"rope_{name}_ms_{mode}", []).append(
                 timed(lambda: L.rope_(qkv, pos, cos, sin, hq + hkv, False)))
-    os.environ.pop("LLMT_ROPE_ROWS")
+    os.environ.pop("LLMT_ROPE_KERNEL")
 res_j = {k: round(sorted(v)[len(v) // 2], 4) for k, v in out.items()}
 gb = {"swiglu_fwd": T * I * 2 * 3 / 1e9, "swiglu_bwd": T * I * 2 * 5 / 1e9, "rmsnorm_fwd_res": T * H * 2 * 4 / 1e9,
       "rmsnorm_bwd_res": T * H * 2 * 4 / 1e9, **rope_gb}

@@ -183,9 +183,85 @@ __global__ __launch_bounds__(256) void rope_rows_kernel(bf16* __restrict__ qkv, 
   }
 }
 
+// LDS-staged form: a block copies the q / k part of TPB token rows into LDS with contiguous 16-byte
+// loads, rotates there, and writes the rows back with contiguous 16-byte stores. With a head dim whose
+// half is not a whole number of 128-byte lines (D = 96: 96-byte halves) the direct kernels' lo / hi
+// accesses split every line between two instructions; staged, every global access is a full line.
+// Requires heads contiguous in the row (stride_h == D). Opt-in (LLMT_ROPE_KERNEL=lds): 0.177 -> 0.167 ms
+// standalone for Phi-3 (D96) but slower for Llama (D128) and 1-2 ms slower in the Phi-3 IT step
+// (profiles/r3_elementwise_kernels.jsonl), so the token-blocked kernel stays the default.
+constexpr int ROPE_TPB = 2;
+template <typename PosT>
+__global__ __launch_bounds__(256) void rope_lds_kernel(bf16* __restrict__ qkv, const PosT* __restrict__ pos,
+                                                       const float* __restrict__ cos_t,
+                                                       const float* __restrict__ sin_t, int64_t T, int nheads, int D,
+                                                       int64_t stride_t, float sign, int64_t P,
+                                                       int* __restrict__ err) {
+  extern __shared__ bf16x8 rows[];  // [ROPE_TPB][nheads * D / 8]
+  const int64_t t0 = (int64_t)blockIdx.x * ROPE_TPB;
+  const int ntok = (int)(T - t0 < ROPE_TPB ? T - t0 : ROPE_TPB);
+  const int C = nheads * D / 8;  // 16-byte chunks per token
+  for (int i = threadIdx.x; i < ntok * C; i += 256) {
+    const int k = i / C;
+    rows[i] = reinterpret_cast<const bf16x8*>(qkv + (t0 + k) * stride_t)[i - k * C];
+  }
+  __syncthreads();
+  const int half = D >> 1;
+  const int groups = half >> 3;
+  const int items = nheads * groups;
+  bf16* lrow = reinterpret_cast<bf16*>(rows);
+  for (int it = threadIdx.x; it < ntok * items; it += 256) {
+    const int k = it / items;
+    const int r = it - k * items;
+    const int h = r / groups;
+    const int g = r - h * groups;
+    int64_t p = (int64_t)pos[t0 + k];
+    if (p < 0 || p >= P) {
+      if (err) err[0] = 1;
+      p = p < 0 ? 0 : P - 1;
+    }
+    bf16* base = lrow + (int64_t)k * nheads * D + h * D + g * 8;
+    bf16x8* lo = reinterpret_cast<bf16x8*>(base);
+    bf16x8* hi = reinterpret_cast<bf16x8*>(base + half);
+    const float* crow = cos_t + p * half + g * 8;
+    const float* srow = sin_t + p * half + g * 8;
+    float c[8], sn8[8];
+    *reinterpret_cast<float4*>(c) = reinterpret_cast<const float4*>(crow)[0];
+    *reinterpret_cast<float4*>(c + 4) = reinterpret_cast<const float4*>(crow)[1];
+    *reinterpret_cast<float4*>(sn8) = reinterpret_cast<const float4*>(srow)[0];
+    *reinterpret_cast<float4*>(sn8 + 4) = reinterpret_cast<const float4*>(srow)[1];
+    float x1[8], x2[8], y1[8], y2[8];
+    unpack8(*lo, x1);
+    unpack8(*hi, x2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sn = sign * sn8[i];
+      y1[i] = x1[i] * c[i] - x2[i] * sn;
+      y2[i] = x2[i] * c[i] + x1[i] * sn;
+    }
+    *lo = pack8(y1);
+    *hi = pack8(y2);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ntok * C; i += 256) {
+    const int k = i / C;
+    reinterpret_cast<bf16x8*>(qkv + (t0 + k) * stride_t)[i - k * C] = rows[i];
+  }
+}
+
 }  // namespace llmt
 
 using namespace llmt;
+
+static bool rope_rows();
+// LLMT_ROPE_KERNEL=lds|rows|flat (read per call, for A/B runs); LLMT_ROPE_ROWS=0 = flat (older switch)
+static int rope_kind() {
+  const char* k = getenv("LLMT_ROPE_KERNEL");
+  if (k && k[0] == 'l') return 2;
+  if (k && k[0] == 'f') return 0;
+  if (k && k[0] == 'r') return 1;
+  return rope_rows() ? 1 : 0;
+}
 
 // LLMT_ROPE_ROWS=0 selects the flat grid-stride RoPE kernel (read per call, for A/B runs)
 static bool rope_rows() {
@@ -241,7 +317,19 @@ extern "C" hipError_t llmt_rope(void* qkv, const void* pos, int pos_is_64, const
   const int64_t total = T * nheads * (D / 16);
   if (total == 0) return hipSuccess;
   const float sign = inverse ? -1.f : 1.f;
-  if (rope_rows()) {  // 4 tokens per 256-thread block; grid.x <= 2^31 - 1 holds for any T we address
+  const int kind = rope_kind();
+  const size_t lds = (size_t)ROPE_TPB * nheads * D * 2;
+  if (kind == 2 && stride_h == D && lds <= 64 * 1024 && stride_t % 8 == 0) {
+    const unsigned grid = (unsigned)((T + ROPE_TPB - 1) / ROPE_TPB);
+    if (pos_is_64)
+      rope_lds_kernel<int64_t><<<grid, 256, lds, stream>>>((bf16*)qkv, (const int64_t*)pos, cos_t, sin_t, T, nheads, D,
+                                                           stride_t, sign, P, err);
+    else
+      rope_lds_kernel<int32_t><<<grid, 256, lds, stream>>>((bf16*)qkv, (const int32_t*)pos, cos_t, sin_t, T, nheads, D,
+                                                           stride_t, sign, P, err);
+    return hipGetLastError();
+  }
+  if (kind >= 1) {  // 4 tokens per 256-thread block; grid.x <= 2^31 - 1 holds for any T we address
     const dim3 grid((unsigned)((T + 3) / 4)), block(64, 4);
     if (pos_is_64)
       rope_rows_kernel<int64_t><<<grid, block, 0, stream>>>((bf16*)qkv, (const int64_t*)pos, cos_t, sin_t, T, nheads,

@@ -86,8 +86,8 @@ def test_rope_inplace_roundtrip(D):
 
 @pytest.mark.parametrize("D", [64, 96, 128])
 def test_rope_token_blocked_equals_flat(D, monkeypatch):
-    """The token-blocked RoPE kernel (default) is bitwise equal to the flat grid-stride one, on a token
-    count that is not a multiple of its 4-token block, int32 and int64 positions, forward and inverse;
+    """The token-blocked and LDS-staged RoPE kernels are bitwise equal to the flat grid-stride one, on a
+    token count that is not a multiple of their token blocks, int32 and int64 positions, forward and inverse;
     an out-of-table position is clamped and flagged by both."""
     from llm_training_amd.ops.native import check_kernel_errors
     torch.manual_seed(0)
@@ -97,24 +97,23 @@ def test_rope_token_blocked_equals_flat(D, monkeypatch):
     for pos in (torch.randint(0, 2048, (T,), device=DEV), torch.randint(0, 2048, (T,), device=DEV).int()):
         for inv in (False, True):
             out = {}
-            for mode in ("1", "0"):
-                monkeypatch.setenv("LLMT_ROPE_ROWS", mode)
+            for mode in ("rows", "flat", "lds"):
+                monkeypatch.setenv("LLMT_ROPE_KERNEL", mode)
                 x = qkv.clone()
                 lib().rope_(x, pos, cos, sin, 6, inv)
                 out[mode] = x
-            assert torch.equal(out["1"], out["0"])
-            assert torch.equal(out["1"][:, 6:], qkv[:, 6:])
+            assert torch.equal(out["rows"], out["flat"]) and torch.equal(out["lds"], out["flat"])
+            assert torch.equal(out["rows"][:, 6:], qkv[:, 6:])
     bad = torch.randint(0, 2048, (T,), device=DEV)
     bad[7] = 5000
-    monkeypatch.setenv("LLMT_ROPE_ROWS", "1")
-    x = qkv.clone()
-    lib().rope_(x, bad, cos, sin, 6, False)
-    assert check_kernel_errors(raise_error=False), "out-of-table position not flagged"
-    monkeypatch.setenv("LLMT_ROPE_ROWS", "0")
-    y = qkv.clone()
-    lib().rope_(y, bad, cos, sin, 6, False)
-    assert torch.equal(x, y)
-    check_kernel_errors(raise_error=False)
+    res = {}
+    for mode in ("rows", "flat", "lds"):
+        monkeypatch.setenv("LLMT_ROPE_KERNEL", mode)
+        x = qkv.clone()
+        lib().rope_(x, bad, cos, sin, 6, False)
+        assert check_kernel_errors(raise_error=False), f"out-of-table position not flagged ({mode})"
+        res[mode] = x
+    assert torch.equal(res["rows"], res["flat"]) and torch.equal(res["lds"], res["flat"])
 
 
 def test_swiglu_bwd_with_transposed_gradient(monkeypatch):
