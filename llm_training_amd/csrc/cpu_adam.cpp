@@ -4,84 +4,16 @@
 // here the engine keeps the fp32 master / exp_avg / exp_avg_sq shards in pinned host memory, streams the
 // bf16 gradient shard down, runs this kernel and streams the bf16 parameter shard back up.
 //
-// One pass per element: read g (bf16 or fp32) + p/m/v (fp32), write p/m/v and the bf16 copy of p.
-// Same math as the GPU kernel (csrc/optim.hip adamw_kernel): decoupled weight decay, bias-corrected
-// step, gradient pre-scaled by the clip/accumulation factor. Split over at::get_num_threads() std::threads
-// in contiguous ranges (ATen's header-inline parallel_for is OpenMP pragmas, which an extension built
-// without -fopenmp runs on one thread); the inner loop is branch-free so the compiler vectorises it.
+// The element loop lives in cpu_adam_core.h (plain C++, also built under ASan / UBSan / TSan by the host
+// sanitizer test); it is split over at::get_num_threads() std::threads (ATen's header-inline parallel_for
+// is OpenMP pragmas, which an extension built without -fopenmp runs on one thread).
 #include <ATen/ATen.h>
 #include <ATen/Parallel.h>
 #include <torch/library.h>
 
-#include <algorithm>
-#include <cmath>
-#include <cstdint>
-#include <cstring>
-#include <thread>
-#include <vector>
+#include "cpu_adam_core.h"
 
 namespace {
-
-template <typename F>
-void parallel_ranges(int64_t n, int64_t grain, F&& f) {
-  const int64_t want = std::max<int64_t>(1, std::min<int64_t>(at::get_num_threads(), (n + grain - 1) / grain));
-  if (want == 1) {
-    f(0, n);
-    return;
-  }
-  const int64_t chunk = (n + want - 1) / want;
-  std::vector<std::thread> pool;
-  pool.reserve(want - 1);
-  for (int64_t t = 1; t < want; ++t) {
-    const int64_t b = t * chunk, e = std::min(n, b + chunk);
-    if (b < e) pool.emplace_back([&f, b, e] { f(b, e); });
-  }
-  f(0, std::min(n, chunk));
-  for (auto& th : pool) th.join();
-}
-
-inline float bf16_to_f32(uint16_t h) {
-  uint32_t u = static_cast<uint32_t>(h) << 16;
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
-}
-
-inline uint16_t f32_to_bf16(float f) {  // round to nearest even; NaN stays NaN
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<uint16_t>(u >> 16);
-}
-
-template <bool kOut, typename LoadG>
-void adamw_span(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, LoadG load_g,
-                uint16_t* __restrict__ pout, int64_t b, int64_t e, float lr, float b1, float b2, float eps, float wd,
-                float step_size, float inv_sqrt_bc2, float sc) {
-  const float decay = 1.f - lr * wd;
-  for (int64_t i = b; i < e; ++i) {
-    const float g = load_g(i) * sc;
-    const float mi = b1 * m[i] + (1.f - b1) * g;
-    const float vi = b2 * v[i] + (1.f - b2) * g * g;
-    const float pi = p[i] * decay - step_size * mi / (std::sqrt(vi) * inv_sqrt_bc2 + eps);
-    m[i] = mi;
-    v[i] = vi;
-    p[i] = pi;
-  }
-  // separate pass: the NaN-preserving rounding would keep the update loop from vectorising
-  if constexpr (kOut)
-    for (int64_t i = b; i < e; ++i) pout[i] = f32_to_bf16(p[i]);
-}
-
-template <typename LoadG>
-void adamw_range(float* p, float* m, float* v, LoadG load_g, uint16_t* pout, int64_t b, int64_t e, float lr, float b1,
-                 float b2, float eps, float wd, float step_size, float inv_sqrt_bc2, float sc) {
-  if (pout)
-    adamw_span<true>(p, m, v, load_g, pout, b, e, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, sc);
-  else
-    adamw_span<false>(p, m, v, load_g, pout, b, e, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2, sc);
-}
 
 void adamw_cpu_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g, const c10::optional<at::Tensor>& pout,
                 double lr, double b1, double b2, double eps, double wd, int64_t step, double gscale) {
@@ -102,29 +34,10 @@ void adamw_cpu_(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g, c
     po = reinterpret_cast<uint16_t*>(pout->data_ptr());
   }
   TORCH_CHECK(step >= 1, "adamw_cpu_: step counts from 1");
-  const float fb1 = static_cast<float>(b1), fb2 = static_cast<float>(b2);
-  const double bc1 = 1.0 - std::pow(b1, static_cast<double>(step));
-  const double bc2 = 1.0 - std::pow(b2, static_cast<double>(step));
-  const float step_size = static_cast<float>(lr / bc1);
-  const float inv_sqrt_bc2 = static_cast<float>(1.0 / std::sqrt(bc2));
-  float* pp = p.data_ptr<float>();
-  float* mm = m.data_ptr<float>();
-  float* vv = v.data_ptr<float>();
-  const float sc = static_cast<float>(gscale);
-  constexpr int64_t kGrain = 1 << 16;  // below 64K elements per thread the spawn cost dominates
-  if (g.scalar_type() == at::kBFloat16) {
-    const uint16_t* gg = reinterpret_cast<const uint16_t*>(g.data_ptr());
-    parallel_ranges(n, kGrain, [&](int64_t b, int64_t e) {
-      adamw_range(pp, mm, vv, [gg](int64_t i) { return bf16_to_f32(gg[i]); }, po, b, e, static_cast<float>(lr), fb1,
-                 fb2, static_cast<float>(eps), static_cast<float>(wd), step_size, inv_sqrt_bc2, sc);
-    });
-  } else {
-    const float* gg = g.data_ptr<float>();
-    parallel_ranges(n, kGrain, [&](int64_t b, int64_t e) {
-      adamw_range(pp, mm, vv, [gg](int64_t i) { return gg[i]; }, po, b, e, static_cast<float>(lr), fb1, fb2,
-                 static_cast<float>(eps), static_cast<float>(wd), step_size, inv_sqrt_bc2, sc);
-    });
-  }
+  const bool bf = g.scalar_type() == at::kBFloat16;
+  llmt::adamw_host(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                   bf ? reinterpret_cast<const uint16_t*>(g.data_ptr()) : nullptr, bf ? nullptr : g.data_ptr<float>(),
+                   po, n, lr, b1, b2, eps, wd, step, gscale, at::get_num_threads());
 }
 
 }  // namespace
