@@ -126,8 +126,24 @@ class Phi3(Llama):
 
     def _runtime(self, input_ids, position_ids, segment_ids, device, S, B):
         rt = super()._runtime(input_ids, position_ids, segment_ids, device, S, B)
-        tables = self.rope_long if S > self.config.original_max_position_embeddings else self.rope_short
-        rt["cos"], rt["sin"] = tables.get(device, S)
+        if self.rope_long is self.rope_short:
+            rt["cos"], rt["sin"] = self.rope_short.get(device, S)
+        else:
+            # LongRoPE factor choice as in the reference (phi3_model.py rotary cache, the Llama code at
+            # llama_model.py:343-352,367-371): long factors once max(position_ids) + 1, rounded up to a
+            # multiple of 4096, exceeds original_max_position_embeddings. Decided on the device without a
+            # host sync: the short and long tables are stacked and the positions shifted into the long half.
+            cs, ss = self.rope_short.get(device, S)
+            cl, sl = self.rope_long.get(device, S)
+            key = (str(device), cs.shape[0])
+            if getattr(self, "_rope_cat_key", None) != key:
+                self._rope_cat = (torch.cat([cs, cl]), torch.cat([ss, sl]))
+                self._rope_cat_key = key
+            pos = rt["positions"]
+            rounded = (pos.max() + 1 + 4095) // 4096 * 4096
+            use_long = (rounded > self.config.original_max_position_embeddings).to(pos.dtype)
+            rt["positions"] = pos + use_long * cs.shape[0]
+            rt["cos"], rt["sin"] = self._rope_cat
         sw = self.config.sliding_window
         rt["window"] = -1 if (sw is None or sw >= S) else int(sw)
         return rt

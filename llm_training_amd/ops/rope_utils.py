@@ -118,13 +118,15 @@ def rope_type(scaling: dict[str, Any] | None) -> str:
 
 def compute_rope_tables(head_dim: int, max_positions: int, base: float = 10000.0,
                         scaling: dict[str, Any] | None = None, max_position_embeddings: int | None = None,
-                        partial_rotary_factor: float = 1.0, device=None):
-    """Return fp32 (cos, sin) of shape [max_positions, rot_dim/2] with the attention factor folded in."""
+                        partial_rotary_factor: float = 1.0, device=None, seq_len: int | None = None):
+    """Return fp32 (cos, sin) of shape [max_positions, rot_dim/2] with the attention factor folded in.
+    ``seq_len``: the sequence length the length-dependent scalings (dynamic NTK, LongRoPE) see; default
+    ``max_positions``."""
     dim = int(head_dim * partial_rotary_factor)
     kind = rope_type(scaling)
     fn = ROPE_INIT_FUNCTIONS[kind]
     mpe = max_position_embeddings or max_positions
-    inv, attn_factor = fn(float(base), dim, mpe, dict(scaling or {}), max_positions)
+    inv, attn_factor = fn(float(base), dim, mpe, dict(scaling or {}), seq_len if seq_len is not None else max_positions)
     t = torch.arange(max_positions, dtype=torch.float64)
     freqs = torch.outer(t, inv)
     cos = (freqs.cos() * attn_factor).float()
@@ -147,13 +149,25 @@ class RopeTables:
         self._cache: dict[str, tuple[torch.Tensor, torch.Tensor, int]] = {}
 
     def get(self, device, min_positions: int):
-        key = str(device)
+        n = max(min_positions, self.max_position_embeddings)
+        n = (n + 8191) // 8192 * 8192
+        ntk = None
+        if rope_type(self.scaling) == "dynamic":
+            # the reference's rule (models/llama/llama_model.py:367-371, 328-341): the NTK rescale sees the
+            # sequence length rounded up to a multiple of 4096, and only once it exceeds
+            # max_position_embeddings (the original frequencies below that)
+            ntk = max(reference_rope_seq_len(min_positions), self.max_position_embeddings)
+        key = (str(device), ntk)
         hit = self._cache.get(key)
         if hit is not None and hit[2] >= min_positions:
             return hit[0], hit[1]
-        n = max(min_positions, self.max_position_embeddings)
-        n = (n + 8191) // 8192 * 8192
         cos, sin = compute_rope_tables(self.head_dim, n, self.base, self.scaling, self.max_position_embeddings,
-                                       device=device)
+                                       device=device, seq_len=ntk)
         self._cache[key] = (cos, sin, n)
         return cos, sin
+
+
+def reference_rope_seq_len(max_position_plus_one: int) -> int:
+    """The sequence length the reference's rotary cache is built for: max(position_ids) + 1 rounded up to a
+    multiple of 4096 (models/llama/llama_model.py:367-371, the same code in phi3_model.py)."""
+    return -(-int(max_position_plus_one) // 4096) * 4096

@@ -44,9 +44,11 @@ def test_phi3_matches_transformers():
     from llm_training_amd.models.phi3 import Phi3, Phi3Config
 
     half = 8
+    # original context 4096 as in Phi-3-mini-128k: the reference picks the long factors once
+    # max(position_ids) + 1, rounded up to a multiple of 4096, exceeds it (phi3_model.py:375-378)
     cfg = Phi3Config(vocab_size=128, hidden_size=64, intermediate_size=96, num_hidden_layers=2,
-                     num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=512,
-                     original_max_position_embeddings=64,
+                     num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=16384,
+                     original_max_position_embeddings=4096,
                      rope_scaling={"type": "longrope", "short_factor": [1.0 + 0.1 * i for i in range(half)],
                                    "long_factor": [1.5 + 0.2 * i for i in range(half)]}, pad_token_id=0)
     ours = Phi3(cfg, dtype=torch.float32)
@@ -55,12 +57,20 @@ def test_phi3_matches_transformers():
     hf = Phi3ForCausalLM(HFC(**hf_cfg))
     hf.load_state_dict(Phi3.convert_state_dict_to_hf(ours.state_dict(), cfg))
     hf.eval()
-    for S in (40, 100):  # short factors (<= 64) and long factors (> 64)
+    for S in (40, 4100):  # short factors (<= 4096) and long factors (> 4096)
         ids = torch.randint(1, cfg.vocab_size, (1, S))
         a = _ours_logits(ours, ids)
         with torch.no_grad():
             b = hf(input_ids=ids).logits
         assert torch.allclose(a, b, atol=3e-4, rtol=1e-3), (S, (a - b).abs().max())
+    # a long row whose positions restart (packed documents): max(position) + 1 decides, not the row length
+    ids = torch.randint(1, cfg.vocab_size, (1, 4100))
+    pos = (torch.arange(4100) % 2050).unsqueeze(0)
+    ours.eval()
+    with torch.no_grad():
+        a = ours(input_ids=ids, position_ids=pos).logits
+        b = hf(input_ids=ids, position_ids=pos).logits
+    assert torch.allclose(a, b, atol=3e-4, rtol=1e-3), ("reset positions", (a - b).abs().max())
 
 
 def test_rope_tables_match_transformers_default():
@@ -314,3 +324,30 @@ def test_hf_enable_liger_kernel_patches_and_matches(model_type):
     assert g0.keys() == g1.keys()
     for k in g0:
         assert torch.allclose(g0[k], g1[k], atol=1e-5, rtol=1e-4), k
+
+
+@pytest.mark.parametrize("rope_scaling,max_pos,S", [
+    ({"rope_type": "linear", "factor": 4.0}, 256, 100),
+    # NTK rescale past max_position_embeddings; the reference rescales for the length rounded up to a
+    # multiple of 4096 (llama_model.py:367-371), transformers for max(position) + 1: equal at S = 4096
+    ({"rope_type": "dynamic", "factor": 2.0}, 1024, 4096),
+    ({"rope_type": "yarn", "factor": 4.0, "original_max_position_embeddings": 64}, 256, 100),
+    ({"rope_type": "yarn", "factor": 8.0, "original_max_position_embeddings": 32, "beta_fast": 16.0,
+      "beta_slow": 2.0, "attention_factor": 1.3}, 256, 100),
+], ids=["linear", "dynamic", "yarn", "yarn-custom"])
+def test_llama_rope_scalings_match_transformers(rope_scaling, max_pos, S):
+    """Every RoPE parameterisation of the native Llama gives transformers' logits (same weights), past
+    the original context where the scaling matters."""
+    from transformers import LlamaConfig as HFC, LlamaForCausalLM
+
+    cfg = tiny_llama_cfg(rope_theta=10000.0, rope_scaling=dict(rope_scaling), max_position_embeddings=max_pos)
+    ours = Llama(cfg, dtype=torch.float32)
+    ours.init_weights(7)
+    hf = LlamaForCausalLM(HFC(**ours.hf_config_dict()))
+    hf.load_state_dict(Llama.convert_state_dict_to_hf(ours.state_dict(), cfg))
+    hf.eval()
+    ids = torch.randint(0, cfg.vocab_size, (1, S))
+    a = _ours_logits(ours, ids)
+    with torch.no_grad():
+        b = hf(input_ids=ids).logits
+    assert torch.allclose(a, b, atol=2e-4, rtol=1e-3), (rope_scaling, (a - b).abs().max())

@@ -280,8 +280,8 @@ def test_convert_to_hf_roundtrip_phi3_longrope(tmp_path):
     lm = CLM({"model": {"model_class": "llm_training.models.Phi3",
                         "model_config": {"vocab_size": 96, "hidden_size": 64, "intermediate_size": 96,
                                          "num_hidden_layers": 2, "num_attention_heads": 4,
-                                         "num_key_value_heads": 4, "max_position_embeddings": 256,
-                                         "original_max_position_embeddings": 32, "rope_scaling": rs,
+                                         "num_key_value_heads": 4, "max_position_embeddings": 16384,
+                                         "original_max_position_embeddings": 4096, "rope_scaling": rs,
                                          "sliding_window": 48, "pad_token_id": 0, "eos_token_id": 1,
                                          "bos_token_id": 2}},
               "optim": {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 5e-3}}})
@@ -302,7 +302,7 @@ def test_convert_to_hf_roundtrip_phi3_longrope(tmp_path):
     assert type(hf).__name__ == "Phi3ForCausalLM"
     hf.eval()
     lm.model.eval()
-    for S in (24, 80):  # inside and past original_max_position_embeddings
+    for S in (24, 4100):  # inside and past original_max_position_embeddings
         ids = torch.randint(3, 96, (2, S))
         with torch.no_grad():
             a = lm.model(input_ids=ids).logits
