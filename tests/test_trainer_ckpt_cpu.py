@@ -89,6 +89,21 @@ def test_convert_to_hf_roundtrip(tmp_path):
     assert torch.allclose(a, b, atol=1e-4), (a - b).abs().max()
 
 
+def test_reference_style_convert_script(tmp_path):
+    """``python scripts/convert_to_hf.py <ckpt> <out> --dtype float32`` (the reference's script interface)."""
+    import subprocess
+    import sys
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=1, seed=1, default_root_dir=str(tmp_path))
+    t.fit(_lm(), _dm())
+    ck = tmp_path / "ck"
+    t.save_checkpoint(str(ck))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "convert_to_hf.py"), str(ck),
+                        str(tmp_path / "hf"), "--dtype", "float32"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (tmp_path / "hf" / "config.json").exists()
+
+
 def test_training_time_estimator_stops(tmp_path):
     from llm_training_amd.runtime.callbacks import TrainingTimeEstimator
     est = TrainingTimeEstimator(num_test_steps=4, num_warmup_steps=2)
