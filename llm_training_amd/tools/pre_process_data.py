@@ -18,10 +18,15 @@ def pre_process(configs: list[str], overrides: list[str] | None = None):
     path = dm.config.pre_processed_data_path
     if not path:
         raise ValueError("data.init_args.config.pre_processed_data_path must be set")
-    dm.config.pre_processed_data_path = None
-    dm.prepare_data()
-    dm.setup()
-    dm.save_pre_processed_data(path)
+    if os.path.isdir(path) and os.listdir(path):
+        # as the reference: an existing non-empty output is kept (loaded, only info.txt is rewritten)
+        logger.info("pre_processed_data_path=%s is not empty, skipping", path)
+        dm.setup()
+    else:
+        dm.config.pre_processed_data_path = None
+        dm.prepare_data()
+        dm.setup()
+        dm.save_pre_processed_data(path)
     buf = io.StringIO()
     with redirect_stdout(buf):
         dm.print_dataset_info()

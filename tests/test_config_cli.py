@@ -187,6 +187,13 @@ data:
 """)
     assert main(["pre-process", "--config", str(cfg)]) == 0
     assert (tmp_path / "processed" / "info.txt").exists()
+    # a second run keeps the existing output (the reference skips a non-empty directory) and rewrites info.txt
+    train_files = sorted(p.name for p in (tmp_path / "processed" / "train").iterdir())
+    stamp = (tmp_path / "processed" / "train" / train_files[0]).stat().st_mtime_ns
+    (tmp_path / "processed" / "info.txt").unlink()
+    assert main(["pre-process", "--config", str(cfg)]) == 0
+    assert (tmp_path / "processed" / "info.txt").exists()
+    assert (tmp_path / "processed" / "train" / train_files[0]).stat().st_mtime_ns == stamp
     assert main(["fit", "--config", str(cfg)]) == 0
     import csv
     rows = list(csv.DictReader(open(tmp_path / "logs" / "p" / "metrics.csv")))
