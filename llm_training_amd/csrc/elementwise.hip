@@ -253,20 +253,19 @@ __global__ __launch_bounds__(256) void rope_lds_kernel(bf16* __restrict__ qkv, c
 
 using namespace llmt;
 
-static bool rope_rows();
-// LLMT_ROPE_KERNEL=lds|rows|flat (read per call, for A/B runs); LLMT_ROPE_ROWS=0 = flat (older switch)
+// LLMT_ROPE_ROWS=0 selects the flat grid-stride RoPE kernel (read per call, for A/B runs)
+static bool rope_rows() {
+  const char* e = getenv("LLMT_ROPE_ROWS");
+  return !(e && e[0] == '0');
+}
+
+// LLMT_ROPE_KERNEL=lds|rows|flat (read per call, for A/B runs) overrides LLMT_ROPE_ROWS
 static int rope_kind() {
   const char* k = getenv("LLMT_ROPE_KERNEL");
   if (k && k[0] == 'l') return 2;
   if (k && k[0] == 'f') return 0;
   if (k && k[0] == 'r') return 1;
   return rope_rows() ? 1 : 0;
-}
-
-// LLMT_ROPE_ROWS=0 selects the flat grid-stride RoPE kernel (read per call, for A/B runs)
-static bool rope_rows() {
-  const char* e = getenv("LLMT_ROPE_ROWS");
-  return !(e && e[0] == '0');
 }
 
 // LLMT_EW_ROWS=0 selects the flat grid-stride SwiGLU kernels (read per call, for A/B runs)
