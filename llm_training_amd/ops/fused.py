@@ -472,10 +472,14 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tenso
 # SwiGLU backward) for the weight gradient of the layer that consumes it next (gate_up): data_ptr -> dy^T.
 # At most one entry lives at a time; the consuming linear backward pops it.
 _DY_T: dict[int, torch.Tensor] = {}
-# opt-in (LLMT_SWIGLU_DY_T=1): the TN weight gradient it enables (4.8 vs 5.6 ms for gate_up) gains about
-# what the extra transposed write costs on Llama-3-8B (same-box steps, on / off / on: 21,666 / 21,632 /
-# 21,759 tok/s; with the first 16-bit LDS transpose 21,895 / 21,888 / 21,873)
-FUSED_DY_T = [os.environ.get("LLMT_SWIGLU_DY_T", "0") == "1"]
+# The TN weight gradient it enables (4.8 vs 5.6 ms for gate_up) against the extra transposed write:
+# on for wide MLPs (intermediate >= 12288): Llama-3-8B (I = 14336) same-box step pairs on / off 1476.0 /
+# 1481.9, 1475.9 / 1479.6, 1474.9 / 1477.1 ms, packed PT 1263.3 / 1267.7 ms; Phi-3-mini (I = 8192)
+# 684.7 / 681.8, 682.4 / 682.6 ms (neutral to slower), DPO 899.6 / 900.1 ms (profiles/r3_workloads_1gpu.jsonl).
+# LLMT_SWIGLU_DY_T=1 / 0 forces it; None = by width.
+_DY_T_ENV = os.environ.get("LLMT_SWIGLU_DY_T")
+FUSED_DY_T = [None if _DY_T_ENV is None else _DY_T_ENV == "1"]
+DY_T_MIN_I = 12288
 
 
 def drop_dy_t():
@@ -496,7 +500,8 @@ class _SwiGLUFn(Function):
         _DY_T.clear()
         I2 = gu.shape[-1]
         T = gu.numel() // I2
-        if (FUSED_DY_T[0] and TRANSPOSE_LAYOUTS[0] and T % 64 == 0 and (I2 // 2) % 64 == 0
+        on = FUSED_DY_T[0] if FUSED_DY_T[0] is not None else I2 // 2 >= DY_T_MIN_I
+        if (on and TRANSPOSE_LAYOUTS[0] and T % 64 == 0 and (I2 // 2) % 64 == 0
                 and T >= _TR_WGRAD_MIN_M and GEMM_MODES.get("wgrad") == "lt"):
             # dgu plus dgu^T in one pass: the gate_up weight gradient then runs hipBLASLt's TN kernel
             dgu, dgu_t = lib().swiglu_bwd_tr(gu, dc)
