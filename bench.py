@@ -125,6 +125,38 @@ def doc_lengths(S: int, n: int, g: torch.Generator) -> list[int]:
     return [b - a for a, b in zip(edges[:-1], edges[1:]) if b > a]
 
 
+def probe_collectives(pc, device, mb: float, iters: int = 5) -> dict:
+    """Bus bandwidth (GB/s) of an all-gather and a reduce-scatter of ``mb`` MB of bf16 over the data-parallel
+    group (the world when dp is 1: TP collectives then), the engine's per-unit collectives. busbw =
+    bytes of the full buffer / time x (n - 1) / n, the usual ring-normalised figure: one xGMI link direction
+    (~153 GB/s on a full-mesh MI355X node) bounds a ring."""
+    group = pc.dp_group if pc.dp_size > 1 else None
+    n = pc.dp_size if pc.dp_size > 1 else dist.get_world_size()
+    numel = int(mb * 1e6 / 2) // (n * 64) * (n * 64)
+    full = torch.empty(numel, dtype=torch.bfloat16, device=device)
+    part = torch.ones(numel // n, dtype=torch.bfloat16, device=device)
+    out = {"probe_group": n, "probe_mb": round(numel * 2 / 1e6, 1)}
+    for name, fn in (("ag", lambda: dist.all_gather_into_tensor(full, part, group=group)),
+                     ("rs", lambda: dist.reduce_scatter_tensor(part, full, group=group))):
+        fn()
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        b.synchronize()
+        sec = a.elapsed_time(b) / 1e3 / iters
+        t = torch.tensor([sec], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sec = float(t.item())
+        out[f"{name}_ms"] = round(sec * 1e3, 3)
+        out[f"{name}_busbw_gbs"] = round(numel * 2 / sec * (n - 1) / n / 1e9, 1)
+    del full, part
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +179,14 @@ def main():
                     help="run the dp>1 engine schedule (RCCL reduce-scatter/all-gather, comm stream) even on 1 GPU")
     ap.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
                     help="hipBLASLt solution selection (default: shipped TunableOp results)")
+    ap.add_argument("--step-timeout", type=float, default=180.0,
+                    help="watchdog: seconds one step (or the collective probe) may take before every rank dumps "
+                         "its stacks and the job exits non-zero (0: off)")
+    ap.add_argument("--setup-timeout", type=float, default=420.0,
+                    help="watchdog limit for process-group setup, model build and the first step")
+    ap.add_argument("--probe-mb", type=float, default=436.0,
+                    help="size of the untimed all-gather / reduce-scatter bandwidth probe (one Llama-3-8B layer "
+                         "unit in bf16); 0: skip")
     args = ap.parse_args()
     if args.workload == "gpt2-cpu":
         bench_gpt2_cpu(args)
@@ -162,10 +202,13 @@ def main():
     from llm_training_amd.parallel.context import ParallelContext, init_distributed
     from llm_training_amd.parallel.engine import DataParallelEngine
     from llm_training_amd.runtime.gemm_tuning import setup_gemm_tuning
+    from llm_training_amd.runtime.monitor import StepWatchdog
 
     metric, model_name, S_def, mb_def = WORKLOADS[args.workload]
     S = args.seq or S_def
     B = args.micro_batch or mb_def
+    wd = StepWatchdog(int(os.environ.get("RANK", "0")), args.step_timeout)
+    wd.arm("process-group setup and model build", args.setup_timeout if args.step_timeout > 0 else 0)
     rank, local, world, device = init_distributed()
     if args.force_sharded and world == 1:
         import socket
@@ -178,6 +221,15 @@ def main():
     gemm_mode = setup_gemm_tuning(args.gemm_tuning)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    comm_backend = None
+    if dist.is_initialized():
+        # the multi-GPU run must really be one RCCL communicator over every GPU (torch's "nccl" backend is
+        # RCCL on ROCm); LLMT_DIST_BACKEND=gloo is the test knob for several ranks on one GPU
+        comm_backend = dist.get_backend()
+        want = os.environ.get("LLMT_DIST_BACKEND") or "nccl"
+        if comm_backend != want or dist.get_world_size() != args.gpus:
+            raise SystemExit(f"expected a {want} process group of {args.gpus} ranks, got {comm_backend} "
+                             f"with {dist.get_world_size()}")
     lib()  # fail loudly if the HIP extension is missing
     pc = ParallelContext.create("auto", args.tp, device)
 
@@ -258,7 +310,16 @@ def main():
             attn_work.append(1.0)
         return batch
 
+    hang = os.environ.get("LLMT_BENCH_HANG")  # test knob "rank:step": that rank stops at that step
+    hang_rank, hang_step = (int(x) for x in hang.split(":")) if hang else (-1, -1)
+    n_step = [0]
+
     def step(batch):
+        if rank == hang_rank and n_step[0] == hang_step:
+            print(f"[rank {rank}] LLMT_BENCH_HANG: stopping at step {hang_step}", file=sys.stderr, flush=True)
+            while True:
+                time.sleep(1.0)
+        n_step[0] += 1
         engine.begin_step(1)
         engine.zero_grad()
         engine.begin_micro(0)
@@ -269,22 +330,54 @@ def main():
         engine.step(3e-5)
         return loss
 
+    # untimed: bandwidth of one layer-unit all-gather / reduce-scatter over the data-parallel group
+    rccl = {"backend": comm_backend, "world": world}
+    if dist.is_initialized() and args.probe_mb > 0:
+        wd.arm("collective bandwidth probe")
+        rccl.update(probe_collectives(pc, device, args.probe_mb))
+
     # fresh synthetic batches for every step (pre-generated so the timed loop does no data work)
     batches = [make_batch() for _ in range(args.warmup + args.steps)]
+    # the host runs at most one step ahead of the device (it waits for step i-1's event after queueing
+    # step i, so the device never idles): a step that hangs on the device trips the watchdog within
+    # --step-timeout of its start instead of at the final synchronize
+    prev = [None]
+
+    def run(i, label, limit=None):
+        wd.arm(label, limit)
+        out = step(batches[i])
+        ev = torch.cuda.Event()
+        ev.record()
+        if prev[0] is not None:
+            prev[0].synchronize()
+        prev[0] = ev
+        return out
+
     for i in range(args.warmup):
-        loss = step(batches[i])
+        loss = run(i, f"warm-up step {i}", args.setup_timeout if i == 0 and args.step_timeout > 0 else None)
+    wd.arm("synchronize before the timed steps")
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
+    prev[0] = None
+    meter = {}
+    engine.wait_meter = meter
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = step(batches[args.warmup + i])
+        loss = run(args.warmup + i, f"timed step {i}", args.setup_timeout if args.warmup == 0 and i == 0
+                   and args.step_timeout > 0 else None)
+    wd.arm("synchronize after the timed steps")
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
-    el = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+    el_host = time.perf_counter() - t0
+    engine.wait_meter = None
+    waits = engine.wait_meter_ms(meter)
+    rccl["exposed_comm_ms_per_step"] = round(waits.get("comm", 0.0) / args.steps, 3)
+    rccl["exposed_optimizer_wait_ms_per_step"] = round(waits.get("opt", 0.0) / args.steps, 3)
+    el = torch.tensor([el_host], device=device, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = el.item()
@@ -314,8 +407,9 @@ def main():
             cfg_out.update(packed_docs_per_row=args.packed_docs, attn_work_vs_causal=round(frac, 4))
         if phi3:
             cfg_out["neftune_alpha"] = 5.0
-        if args.force_sharded:
-            cfg_out["force_sharded"] = True
+        # the schedule actually run: one GPU defaults to ZeRO-0 (no collectives); several GPUs to ZeRO-2
+        # (the reference example's DeepSpeed stage); force_sharded runs the dp>1 schedule on one GPU
+        cfg_out["force_sharded"] = bool(args.force_sharded)
         out = {
             "metric": metric,
             "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
@@ -327,11 +421,14 @@ def main():
             "tflops_per_gpu": round(tps / world * fpt / 1e12, 1),
             "peak_mem_gib": round(peak_mem, 1),
             "final_loss": round(final_loss, 4),
+            "rccl": rccl,
         }
         print(json.dumps(out), flush=True)
+    wd.arm("shutdown")
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+    wd.disarm()
 
 
 if __name__ == "__main__":

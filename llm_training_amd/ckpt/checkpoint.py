@@ -165,6 +165,9 @@ def _meta(trainer) -> dict:
         "param_dtype": str(eng.param_dtype).replace("torch.", ""),
         "optimizer_kinds": eng.state_kinds(),
         "loss_scaler": trainer.scaler.state_dict() if getattr(trainer, "scaler", None) is not None else None,
+        # stateful callbacks (EarlyStopping counters), keyed by class name as Lightning's state_key
+        "callbacks": {type(cb).__name__: cb.state_dict() for cb in getattr(trainer, "callbacks", [])
+                      if hasattr(cb, "state_dict") and hasattr(cb, "load_state_dict")},
         "config": trainer.config_dict,
         "model_class": f"{type(trainer.lm.model).__module__}.{type(trainer.lm.model).__qualname__}",
         "model_config": trainer.lm.model.config.model_dump(mode="json"),
@@ -465,6 +468,10 @@ def load_checkpoint(trainer, path: str, load_optimizer: bool = True):
             trainer.scheduler.load_state_dict(meta["scheduler"])
         if getattr(trainer, "scaler", None) is not None and meta.get("loss_scaler"):
             trainer.scaler.load_state_dict(meta["loss_scaler"])
+        for cb in getattr(trainer, "callbacks", []):
+            st_cb = (meta.get("callbacks") or {}).get(type(cb).__name__)
+            if st_cb is not None and hasattr(cb, "load_state_dict"):
+                cb.load_state_dict(st_cb)
         # generator states: exact continuation of NEFTune noise / dropout when the layout is unchanged
         st = {k: v for k, v in side.items() if k in ("cpu", "cuda")}
         if st:

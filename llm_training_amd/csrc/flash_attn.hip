@@ -35,6 +35,7 @@
 
 #include <cstdlib>
 #include <initializer_list>
+#include <type_traits>
 
 namespace llmt {
 
@@ -1333,6 +1334,319 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, cons
   }
 }
 
+// ============================================================================ backward dK/dV, v5
+// The dK/dV pass of fa_bwd_dkdv128_kernel (same grid, ring, DMA, masks and fragment layouts) with the
+// loop rebuilt as a software pipeline for its one wave per SIMD (profiles/r4_dkdv_pipeline.md). Per
+// iteration t (one 32-row query tile):
+//  * phase A issues the 2*NKK S / dP MFMAs of tile t; in their gaps the Q / dO row fragments of tile t
+//    arrive just in time (two k-steps ahead), and the transposed Q^T / dO^T fragments of tile t-1 and the
+//    row constants of tile t are read for phase B;
+//  * phase B issues the 4*NDT dV / dK MFMAs of tile t-1 (operands P, dS of tile t-1 as bf16) while the
+//    softmax of tile t (P = exp2(S*scale*log2e - lse*log2e), dS = P (dP - delta)) runs in their gaps.
+// Only the bf16 P / dS operands (16 VGPRs) cross the iteration; the fp32 scores are produced and consumed
+// inside one iteration, so they never get parked in accumulator registers (the v3 loop opened every tile
+// with 32 serial accumulator reads, and a scores-carrying pipeline had hipcc copy them through AGPRs).
+// The MFMAs are inline asm with pinned register files: scores in VGPRs where the softmax reads them, the
+// kernel-resident K / V fragments in AGPRs (freeing 64 VGPRs), accumulators dK / dV left to hipcc (AGPRs).
+// An asm MFMA's result is read by VALU only in the next phase, behind at least one full MFMA chain.
+__device__ __forceinline__ void mfma_v0(f32v16& c, const bfv8& x, const bfv8& y) {  // c (VGPR) = x . y (AGPR)
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(x), "a"(y));
+}
+__device__ __forceinline__ void mfma_vv(f32v16& c, const bfv8& x, const bfv8& y) {  // c (VGPR) += x . y (AGPR)
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(x), "a"(y));
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const float* ld) {
+  constexpr int NKK = D / 16, NDT = D / 32;
+  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
+  constexpr int NDMA = 5;
+  constexpr int NB = 4 * NDT;  // phase-B MFMAs (dV then dK, s2-major)
+  using QI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  int b, kb;
+  block_of(a, L, (S + 127) / 128, false, b, kb);
+  const int ks = kb * 128, kw = ks + wid * 32, kr = kw + r;
+  const int nT = (S + 31) / 32;
+  const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
+  const bf16* vp = a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh;
+  const int sk = (a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;
+  const float sl2 = a.scale * kLog2e;
+
+  bfv8 kf[NKK], vf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    kf[kk] = gload8(kp + (int64_t)min(kr, S - 1) * a.k_ss + kk * 16 + hh * 8, kr < S);
+    vf[kk] = gload8(vp + (int64_t)min(kr, S - 1) * a.v_ss + kk * 16 + hh * 8, kr < S);
+  }
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
+  f32v16 dkt[NDT], dvt[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      dkt[dt][i] = 0.f;
+      dvt[dt][i] = 0.f;
+    }
+
+  const RunInfo kr_run = block_run(a, b, min(ks, S - 1), min(ks + 127, S - 1));
+  const int q_beg = a.causal ? ks : max(0, kr_run.rs) / 32 * 32;
+  int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
+  if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
+  const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
+  const int T = nq * grp;
+
+  if (T > 0) {
+    int dq_off[2], dd_off[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int row = 8 * wid + 4 * n + (lane >> 4);
+      const int ch = (lane & 15) ^ QI::swz(row);
+      dq_off[n] = (row * a.q_ss + ch * 8) * 2;
+      dd_off[n] = (row * a.d_ss + ch * 8) * 2;
+    }
+    const int ld_off = ((wid & 1) * 64 + lane) * 4;
+    asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]));
+    const int64_t q_rows = S - q_beg;
+    const int64_t nrec_q = ((q_rows - 1) * a.q_ss + D) * 2, nrec_d = ((q_rows - 1) * a.d_ss + D) * 2;
+    const int64_t nrec_l = (int64_t)nq * kLdTile * 4;
+    const bf16* qh0 = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * grp) * a.q_sh + (int64_t)q_beg * a.q_ss;
+    const bf16* dh0 = a.dout + (int64_t)b * a.d_sb + (int64_t)(hk * grp) * a.d_sh + (int64_t)q_beg * a.d_ss;
+    const float* lh0 = ld + (((int64_t)b * a.Hq + hk * grp) * nT + (q_beg >> 5)) * kLdTile;
+    const int step_q = BM * a.q_ss * 2, step_d = BM * a.d_ss * 2;
+    Rsrc qrs = make_rsrc4(qh0, nrec_q), drs = make_rsrc4(dh0, nrec_d), lrs = make_rsrc4(lh0, nrec_l);
+    int iss_g = 0, iss_q = 0, iss_n = 0, toff_q = 0, toff_d = 0, toff_l = 0;
+    auto issue = [&](const char* slot) {
+      const char* q0 = slot + 8 * wid * 256;
+      dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, slot + 2 * IMG + (wid & 1) * 256,
+                dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
+      if (++iss_n < T) {
+        toff_q += step_q;
+        toff_d += step_d;
+        toff_l += kLdTile * 4;
+        if (++iss_q == nq) {
+          iss_q = 0;
+          ++iss_g;
+          toff_q = toff_d = toff_l = 0;
+          qrs = make_rsrc4(qh0 + (int64_t)iss_g * a.q_sh, nrec_q);
+          drs = make_rsrc4(dh0 + (int64_t)iss_g * a.d_sh, nrec_d);
+          lrs = make_rsrc4(lh0 + (int64_t)iss_g * nT * kLdTile, nrec_l);
+        }
+      }
+    };
+    int cur_q = 0;
+    const bool seg_or_window = a.seg != nullptr || a.window >= 0;
+    struct TileMask {
+      int q0;
+      bool need, m_seg;
+    };
+    auto tile_mask = [&]() {
+      TileMask m;
+      m.q0 = q_beg + cur_q * BM;
+      m.need = a.causal && kw + 31 > m.q0;
+      m.m_seg = false;
+      if (seg_or_window) {
+        m.m_seg = seg_mask(a, kr_run, m.q0, m.q0 + 31);
+        m.need = m.need || m.m_seg || (a.window >= 0 && m.q0 + 31 - a.window > kw);
+      }
+      if (++cur_q == nq) cur_q = 0;
+      return m;
+    };
+    int ro[NKK], to[NDT][2];
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) ro[kk] = QI::roff(r, 2 * kk + hh);
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        to[dt][0] = QI::toff(BM, row, dt * 32 + col);
+        to[dt][1] = QI::toff(BM, row + 8, dt * 32 + col);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(ro[kk]));
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
+
+    // transposed fragment i of phase B: i < 2*NDT -> dO^T (dV product), else Q^T (dK product);
+    // s2 = (i / NDT) & 1, dt = i % NDT
+    auto trf = [&](const char* slot, int i) -> bfv8 {
+      const int s2 = (i / NDT) & 1, dt = i % NDT;
+      const char* base = slot + (i < 2 * NDT ? IMG : 0) + 4096 * s2;
+      const s16v4 lo = lds_tr(base + to[dt][0]), hi = lds_tr(base + to[dt][1]);
+      return __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    // S / dP of the tile in `cs` (first two k-steps prefetched in qa / da); with `ps` != null the
+    // transposed fragments of the previous tile are read into tf in the MFMA gaps
+    auto phase_a = [&](auto with_tr, const char* cs, const char* ps, bfv8 (&qa)[2], bfv8 (&da)[2], f32v16& sc,
+                       f32v16& dc, bfv8 (&tf)[NB], float (&lq)[16], float (&nd)[16]) {
+      bfv8 qf[NKK], df[NKK];
+      qf[0] = qa[0]; df[0] = da[0]; qf[1] = qa[1]; df[1] = da[1];
+      const float* Ls = reinterpret_cast<const float*>(cs + 2 * IMG);
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        if (kk + 2 < NKK) {
+          qf[kk + 2] = lds_b128(cs + ro[kk + 2]);
+          df[kk + 2] = lds_b128(cs + ro[kk + 2] + IMG);
+        }
+        // row constants of this tile (-lse*log2e at floats 96.., -delta at 32..), one 16-byte read per k-step
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if ((2 * c) * NKK / 8 == kk) {
+            const float4 l4 = *reinterpret_cast<const float4*>(Ls + 96 + 8 * c + 4 * hh);
+            lq[4 * c] = l4.x; lq[4 * c + 1] = l4.y; lq[4 * c + 2] = l4.z; lq[4 * c + 3] = l4.w;
+          }
+          if ((2 * c + 1) * NKK / 8 == kk) {
+            const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
+            nd[4 * c] = d4.x; nd[4 * c + 1] = d4.y; nd[4 * c + 2] = d4.z; nd[4 * c + 3] = d4.w;
+          }
+        }
+        if constexpr (decltype(with_tr)::value) {
+#pragma unroll
+          for (int i = kk * NB / NKK; i < (kk + 1) * NB / NKK; ++i) tf[i] = trf(ps, i);
+        }
+        if (kk == 0) {
+          mfma_v0(sc, qf[0], kf[0]);
+          mfma_v0(dc, df[0], vf[0]);
+        } else {
+          mfma_vv(sc, qf[kk], kf[kk]);
+          mfma_vv(dc, df[kk], vf[kk]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // masked elements (diagonal / window / packed tiles only) get S = -inf, so P = exp2(-inf) = 0 (the row
+    // constant is never +inf: rows past S or without keys carry -inf)
+    auto apply_mask = [&](const char* cs, const TileMask& m, f32v16& sc) {
+      const int* Sg = reinterpret_cast<const int*>(cs + 2 * IMG) + 64;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        int4 s4 = make_int4(sk, sk, sk, sk);
+        if (m.m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int qi = m.q0 + 8 * c + 4 * hh + j;
+          bool o = true;
+          if (a.causal) o = o && (kr <= qi);
+          if (a.window >= 0) o = o && (qi - kr <= a.window);
+          if (m.m_seg) o = o && ((&s4.x)[j] == sk);
+          if (!o) sc[4 * c + j] = -INFINITY;
+        }
+      }
+    };
+    // softmax element v of a tile into the bf16 operands pn / dn
+    auto smx = [&](int v, const f32v16& sc, const f32v16& dc, const float (&lq)[16], const float (&nd)[16],
+                   bfv8 (&pn)[2], bfv8 (&dn)[2]) {
+      const float p = fexp2(fmaf(sc[v], sl2, lq[v]));
+      pn[v >> 3][v & 7] = (__bf16)p;
+      dn[v >> 3][v & 7] = (__bf16)(p * (dc[v] + nd[v]));
+    };
+    // dV / dK of the previous tile (operands po / dso, fragments tf) || softmax of this tile into pn / dsn;
+    // with `ns` the first two k-steps of the next tile's rows are read at the end
+    auto phase_b = [&](auto smax, const bfv8 (&po)[2], const bfv8 (&dso)[2], const bfv8 (&tf)[NB],
+                       const f32v16& sc, const f32v16& dc, const float (&lq)[16], const float (&nd)[16],
+                       bfv8 (&pn)[2], bfv8 (&dsn)[2], const char* ns, bfv8 (&qa)[2], bfv8 (&da)[2]) {
+      constexpr bool SMAX = decltype(smax)::value;  // softmax of a next tile (and its rows) to interleave
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int s2 = (i / NDT) & 1, dt = i % NDT;
+        if (i < 2 * NDT)
+          dvt[dt] = mfma32(tf[i], po[s2], dvt[dt]);
+        else
+          dkt[dt] = mfma32(tf[i], dso[s2], dkt[dt]);
+        if constexpr (SMAX) {
+#pragma unroll
+          for (int v = i * 16 / NB; v < (i + 1) * 16 / NB; ++v) smx(v, sc, dc, lq, nd, pn, dsn);
+        }
+        if (SMAX && i == NB - 3) {
+          qa[0] = lds_b128(ns + ro[0]);
+          da[0] = lds_b128(ns + ro[0] + IMG);
+          qa[1] = lds_b128(ns + ro[1]);
+          da[1] = lds_b128(ns + ro[1] + IMG);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+
+    int sl_m2 = (NS - 1) * SLOT, sl_m1 = 0, sl_0 = SLOT, sl_p1 = 2 * SLOT;
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t) issue(smem + t * SLOT);
+    wait_vm<NDMA * (NS - 4)>();
+    ring_barrier();
+
+    bfv8 qa[2], da[2], pb[2], db[2];
+    bfv8 tf[NB];
+    float lq[16], nd[16];
+    {  // tile 0: S / dP and its softmax
+      qa[0] = lds_b128(smem + ro[0]);
+      da[0] = lds_b128(smem + ro[0] + IMG);
+      qa[1] = lds_b128(smem + ro[1]);
+      da[1] = lds_b128(smem + ro[1] + IMG);
+      f32v16 sc, dc;
+      const TileMask m0 = tile_mask();
+      phase_a(std::false_type{}, smem, smem, qa, da, sc, dc, tf, lq, nd);
+      if (m0.need) apply_mask(smem, m0, sc);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) smx(v, sc, dc, lq, nd, pb, db);
+      qa[0] = lds_b128(smem + SLOT + ro[0]);
+      da[0] = lds_b128(smem + SLOT + ro[0] + IMG);
+      qa[1] = lds_b128(smem + SLOT + ro[1]);
+      da[1] = lds_b128(smem + SLOT + ro[1] + IMG);
+    }
+    for (int t = 1; t < T; ++t) {
+      issue(smem + sl_m2);
+      const TileMask mcur = tile_mask();
+      f32v16 sc, dc;
+      phase_a(std::true_type{}, smem + sl_0, smem + sl_m1, qa, da, sc, dc, tf, lq, nd);
+      if (mcur.need) apply_mask(smem + sl_0, mcur, sc);
+      bfv8 pn[2], dsn[2];
+      phase_b(std::true_type{}, pb, db, tf, sc, dc, lq, nd, pn, dsn, smem + sl_p1, qa, da);
+      pb[0] = pn[0]; pb[1] = pn[1]; db[0] = dsn[0]; db[1] = dsn[1];
+      sl_m2 = sl_m1;
+      sl_m1 = sl_0;
+      sl_0 = sl_p1;
+      sl_p1 = (sl_p1 + SLOT == NS * SLOT) ? 0 : sl_p1 + SLOT;
+      wait_vm<NDMA * (NS - 4)>();
+      ring_barrier_nodrain();
+    }
+    {  // dV / dK of the last tile
+#pragma unroll
+      for (int i = 0; i < NB; ++i) tf[i] = trf(smem + sl_m1, i);
+      f32v16 z = {};
+      bfv8 pn[2], dsn[2];
+      phase_b(std::false_type{}, pb, db, tf, z, z, lq, nd, pn, dsn, smem, qa, da);
+    }
+    wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+  }
+
+  uint2 wk[4 * NDT], wv[4 * NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int g = 4 * dt + c;
+      wk[g].x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
+      wk[g].y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
+      wv[g].x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
+      wv[g].y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
+    }
+  widen_pairs(wk);
+  widen_pairs(wv);
+  if (kr < S) {
+    store_pairs(a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh + 8 * hh, wk);
+    store_pairs(a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh + 8 * hh, wv);
+  }
+}
+
 // ============================================================================ forward, D = 128, v3
 // grid: ceil(S/128) * Hq * B blocks (1-D, kv-head-major, heaviest query blocks first), 4 waves x 32
 // queries, two workgroups per CU. Differences from fa_fwd_kernel<128>, each aimed at the exposed LDS
@@ -2247,7 +2561,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
       fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      if (dkdv_variant() >= 3)
+      if (dkdv_variant() == 5)
+        fa_bwd_dkdv5_kernel<96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      else if (dkdv_variant() >= 3)
         fa_bwd_dkdv128_kernel<3, 96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
         fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
@@ -2256,7 +2572,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     if (D == 64) {
       fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
       fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      if (dkdv_variant() >= 3)
+      if (dkdv_variant() == 5)
+        fa_bwd_dkdv5_kernel<64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      else if (dkdv_variant() >= 3)
         fa_bwd_dkdv128_kernel<3, 64, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
         fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
@@ -2282,7 +2600,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<128, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     }
     const int variant = dkdv_variant();
-    if (variant == 3)
+    if (variant == 5)
+      fa_bwd_dkdv5_kernel<128><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 3)
       fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 4)
       fa_bwd_dkdv128_kernel<3, 128, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);

@@ -137,9 +137,9 @@ class BaseDataModule:
         for k, d in self.datasets.items():
             d.save_to_disk(f"{path}/{k}")
 
-    def train_dataloader(self, dp_rank=0, dp_size=1, seed=0, skip_batches=0, epoch=0) -> DataLoader:
+    def train_dataloader(self, dp_rank=0, dp_size=1, seed=0, skip_batches=0, epoch=0, shuffle=True) -> DataLoader:
         ds = self.datasets["train"]
-        sampler = ResumableDistributedSampler(len(ds), self.config.batch_size, dp_rank, dp_size, True, seed)
+        sampler = ResumableDistributedSampler(len(ds), self.config.batch_size, dp_rank, dp_size, shuffle, seed)
         sampler.set_epoch(epoch)
         sampler.set_skip(skip_batches)
         kw = {}

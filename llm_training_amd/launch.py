@@ -95,6 +95,33 @@ def resolve_devices(devices, accelerator="auto") -> int:
     return max(1, int(devices))
 
 
+def device_list(devices) -> list[int] | None:
+    """The explicit GPU indices of ``trainer.devices`` (a list or "2,3"), or None for a count / auto."""
+    if isinstance(devices, (list, tuple)):
+        return [int(d) for d in devices]
+    if isinstance(devices, str) and "," in devices:
+        return [int(d) for d in devices.split(",") if d.strip()]
+    return None
+
+
+def visible_devices_env(ids: list[int], env: dict | None = None) -> dict:
+    """HIP_VISIBLE_DEVICES for ranks pinned to the listed GPUs (Lightning semantics: indices into the
+    GPUs this process sees). Every child sees exactly the listed GPUs, in order, so LOCAL_RANK r runs on
+    ``ids[r]``; an existing HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES selection is composed with it."""
+    env = os.environ if env is None else env
+    base = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
+    if base:
+        vis = [x.strip() for x in base.split(",") if x.strip()]
+        if max(ids) >= len(vis):
+            raise SystemExit(f"trainer.devices {ids}: only {len(vis)} GPUs are visible ({base})")
+        sel = [vis[i] for i in ids]
+    else:
+        sel = [str(i) for i in ids]
+    if len(set(sel)) != len(sel):
+        raise SystemExit(f"trainer.devices {ids} lists a GPU twice")
+    return {"HIP_VISIBLE_DEVICES": ",".join(sel)}
+
+
 def _kill_group(p: subprocess.Popen, sig) -> None:
     try:
         os.killpg(p.pid, sig)
@@ -186,6 +213,16 @@ def launch_for_trainer(trainer_cfg: dict, cmd: list[str]) -> int | None:
     if num_nodes > 1:
         raise SystemExit("trainer.num_nodes > 1 needs one task per GPU from srun or torchrun "
                          "(see scripts/train.sh)")
+    ids = device_list(devices) if accelerator != "cpu" else None
+    if ids is not None and ids != list(range(len(ids))):
+        # GPUs other than the first n: every rank sees exactly the listed ones (a single rank too)
+        extra = visible_devices_env(ids)
+        if len(ids) == 1:
+            os.environ.update(extra)  # this process becomes the rank: no HIP call has happened yet
+            apply_rccl_env()
+            return None
+        apply_rccl_env()
+        return spawn(len(ids), cmd, extra_env=extra)
     return maybe_launch(resolve_devices(devices, accelerator), cmd)
 
 

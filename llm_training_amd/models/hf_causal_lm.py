@@ -252,24 +252,87 @@ def _is_silu(act) -> bool:
     return isinstance(act, nn.SiLU) or type(act).__name__ in ("SiLUActivation", "SiLU")
 
 
+_SLICE_CLASSES: dict[type, type] = {}
+
+
+def _slice_linear(cls: type) -> type:
+    """A subclass of ``cls`` (an nn.Linear) whose ``weight`` is a row slice of the owning MLP's fused
+    ``gate_up_weight`` parameter instead of a parameter of its own."""
+    sub = _SLICE_CLASSES.get(cls)
+    if sub is None:
+        def weight(self):
+            lo, hi = self._fused_rows
+            return self._fused_owner.gate_up_weight[lo:hi]
+        sub = type(f"Fused{cls.__name__}", (cls,), {"weight": property(weight)})
+        _SLICE_CLASSES[cls] = sub
+    return sub
+
+
+def _state_dict_split(module, state_dict, prefix, local_metadata):
+    """Checkpoints / HF export keep transformers' names: gate_up_weight -> gate_proj.weight, up_proj.weight."""
+    w = state_dict.pop(prefix + "gate_up_weight", None)
+    if w is not None:
+        i = module.gate_proj._fused_rows[1]
+        state_dict[prefix + "gate_proj.weight"] = w[:i]
+        state_dict[prefix + "up_proj.weight"] = w[i:]
+
+
+def _load_fuse(module, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys, error_msgs):
+    g, u = prefix + "gate_proj.weight", prefix + "up_proj.weight"
+    if g in state_dict and u in state_dict:
+        state_dict[prefix + "gate_up_weight"] = torch.cat([state_dict.pop(g), state_dict.pop(u)], 0)
+
+
+def _fuse_gate_up(m: nn.Module) -> bool:
+    """Re-home gate_proj / up_proj weights into one [2I, h] parameter ``gate_up_weight`` (gate rows first):
+    the patched forward multiplies by it directly (no per-call torch.cat of 2 x I x h weights and no cat
+    backward), its gradient is written by the main-grad-aware linear kernel. ``gate_proj.weight`` /
+    ``up_proj.weight`` stay readable as views; state dicts keep the transformers key names."""
+    g, u = m.gate_proj, m.up_proj
+    if g.bias is not None or u.bias is not None or g.weight.shape[1] != u.weight.shape[1]:
+        return False
+    if "weight" not in g._parameters or "weight" not in u._parameters:
+        return False
+    I = g.weight.shape[0]
+    fused = nn.Parameter(torch.cat([g.weight.detach(), u.weight.detach()], 0),
+                         requires_grad=g.weight.requires_grad or u.weight.requires_grad)
+    del g._parameters["weight"]
+    del u._parameters["weight"]
+    m.register_parameter("gate_up_weight", fused)
+    for mod, rows in ((g, (0, I)), (u, (I, I + u.out_features))):
+        mod.__class__ = _slice_linear(type(mod))
+        object.__setattr__(mod, "_fused_owner", m)  # plain attribute: not a child module
+        object.__setattr__(mod, "_fused_rows", rows)
+    m._register_state_dict_hook(_state_dict_split)
+    m._register_load_state_dict_pre_hook(_load_fuse, with_module=True)
+    return True
+
+
 def _patch_mlp(m: nn.Module) -> bool:
     act = getattr(m, "act_fn", getattr(m, "activation_fn", None))
     if act is None or not _is_silu(act):
         return False
     if all(hasattr(m, n) for n in ("gate_proj", "up_proj", "down_proj")):
-        # one GEMM for gate and up (the weights concatenated per call), the SwiGLU kernel on the fused
-        # [.., 2I] buffer, then down_proj (Liger's LigerSwiGLUMLP)
-        def forward(x, _m=m):
-            from ..ops.fused import swiglu
-            w = torch.cat([_m.gate_proj.weight, _m.up_proj.weight], 0)
-            b = None
-            if _m.gate_proj.bias is not None:
-                b = torch.cat([_m.gate_proj.bias, _m.up_proj.bias], 0)
-            return _m.down_proj(swiglu(torch.nn.functional.linear(x, w, b)))
+        # one GEMM for gate and up, the SwiGLU kernel on the fused [.., 2I] buffer, then down_proj
+        # (Liger's LigerSwiGLUMLP); gate / up weights live in one fused parameter (no per-call concat)
+        if _fuse_gate_up(m):
+            def forward(x, _m=m):
+                from ..ops.fused import linear, swiglu
+                c = swiglu(linear(x, _m.gate_up_weight), dy_t_consumer=True)
+                return linear(c, _m.down_proj.weight, _m.down_proj.bias)
+        else:  # biased projections: concatenated per call
+            def forward(x, _m=m):
+                from ..ops.fused import swiglu
+                w = torch.cat([_m.gate_proj.weight, _m.up_proj.weight], 0)
+                b = None
+                if _m.gate_proj.bias is not None:
+                    b = torch.cat([_m.gate_proj.bias, _m.up_proj.bias], 0)
+                return _m.down_proj(swiglu(torch.nn.functional.linear(x, w, b)))
     elif hasattr(m, "gate_up_proj") and hasattr(m, "down_proj"):  # Phi-3: fused [gate | up] projection
         def forward(x, _m=m):
-            from ..ops.fused import swiglu
-            return _m.down_proj(swiglu(_m.gate_up_proj(x)))
+            from ..ops.fused import linear, swiglu
+            gu = linear(x, _m.gate_up_proj.weight, _m.gate_up_proj.bias)
+            return linear(swiglu(gu, dy_t_consumer=True), _m.down_proj.weight, _m.down_proj.bias)
     else:
         return False
     m.forward = forward

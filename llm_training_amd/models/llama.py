@@ -143,7 +143,8 @@ class LlamaMLP(nn.Module):
         if sp_group is not None:
             gu = tpl.ag_linear(h, self.gate_up_proj.weight, self.gate_up_proj.bias, sp_group)
             return tpl.linear_rs(F_.swiglu(gu), self.down_proj.weight, self.down_proj.bias, sp_group)
-        return self.down_proj(F_.swiglu(self.gate_up_proj(h)))
+        gu = self.gate_up_proj(h)
+        return self.down_proj(F_.swiglu(gu, dy_t_consumer=isinstance(self.gate_up_proj, Linear)))
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -267,7 +268,12 @@ class Llama(BaseModel):
             position_ids = torch.arange(S, device=device).unsqueeze(0).expand(B, S)
         else:
             position_ids = position_ids.to(device).long().expand(B, S)
-        cos, sin = self.rope.get(device, S)
+        n_pos = S
+        if self.rope.dynamic:
+            # dynamic NTK: the reference sizes the rescale by max(position_ids) + 1 (packed rows restart
+            # their positions), llama_model.py:367-371; one host read, for this rope type only
+            n_pos = int(position_ids.max()) + 1
+        cos, sin = self.rope.get(device, max(S, n_pos), ntk_positions=n_pos)
         impl = self.config.resolved_attn_implementation(device.type)
         selective = self.gradient_checkpointing and self.config.recompute_granularity == "selective"
         seg_info = None

@@ -488,9 +488,10 @@ def drop_dy_t():
 
 class _SwiGLUFn(Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, dy_t_consumer):
         gu = gu.contiguous()
         ctx.save_for_backward(gu)
+        ctx.dy_t_consumer = dy_t_consumer
         return lib().swiglu_fwd(gu)
 
     @staticmethod
@@ -501,19 +502,23 @@ class _SwiGLUFn(Function):
         I2 = gu.shape[-1]
         T = gu.numel() // I2
         on = FUSED_DY_T[0] if FUSED_DY_T[0] is not None else I2 // 2 >= DY_T_MIN_I
-        if (on and TRANSPOSE_LAYOUTS[0] and T % 64 == 0 and (I2 // 2) % 64 == 0
+        # only when the caller guarantees that gate_up's weight gradient runs through _LinearFn, which
+        # pops the transposed copy (HF modules / torch linears would leave a T x 2I buffer behind)
+        if (on and ctx.dy_t_consumer and TRANSPOSE_LAYOUTS[0] and T % 64 == 0 and (I2 // 2) % 64 == 0
                 and T >= _TR_WGRAD_MIN_M and GEMM_MODES.get("wgrad") == "lt"):
             # dgu plus dgu^T in one pass: the gate_up weight gradient then runs hipBLASLt's TN kernel
             dgu, dgu_t = lib().swiglu_bwd_tr(gu, dc)
             _DY_T[dgu.data_ptr()] = dgu_t
-            return dgu
-        return lib().swiglu_bwd(gu, dc)
+            return dgu, None
+        return lib().swiglu_bwd(gu, dc), None
 
 
-def swiglu(gate_up: torch.Tensor) -> torch.Tensor:
-    """silu(gate) * up for a fused [..., 2I] buffer laid out [gate | up]."""
+def swiglu(gate_up: torch.Tensor, dy_t_consumer: bool = False) -> torch.Tensor:
+    """silu(gate) * up for a fused [..., 2I] buffer laid out [gate | up]. ``dy_t_consumer``: gate_up came
+    from this module's ``linear`` (so its backward can take the transposed input gradient the SwiGLU
+    backward writes for wide MLPs)."""
     if use_native(gate_up):
-        return _SwiGLUFn.apply(gate_up)
+        return _SwiGLUFn.apply(gate_up, bool(dy_t_consumer))
     return ref.swiglu_fused(gate_up)
 
 

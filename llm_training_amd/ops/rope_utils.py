@@ -147,16 +147,31 @@ class RopeTables:
 
     def __post_init__(self):
         self._cache: dict[str, tuple[torch.Tensor, torch.Tensor, int]] = {}
+        self._dyn_cached = self.max_position_embeddings  # the reference's max_seq_len_cached (dynamic NTK)
 
-    def get(self, device, min_positions: int):
+    @property
+    def dynamic(self) -> bool:
+        return rope_type(self.scaling) == "dynamic"
+
+    def get(self, device, min_positions: int, ntk_positions: int | None = None):
+        """cos / sin tables covering ``min_positions``. Dynamic NTK follows the reference's stateful rule
+        (models/llama/llama_model.py:328-341, 367-371): the rescale length is ``ntk_positions`` (max
+        position + 1, default ``min_positions``) rounded up to a multiple of 4096; it only grows while
+        lengths stay at or above max_position_embeddings, and falls back to the original frequencies once a
+        shorter batch comes."""
         n = max(min_positions, self.max_position_embeddings)
         n = (n + 8191) // 8192 * 8192
         ntk = None
-        if rope_type(self.scaling) == "dynamic":
-            # the reference's rule (models/llama/llama_model.py:367-371, 328-341): the NTK rescale sees the
-            # sequence length rounded up to a multiple of 4096, and only once it exceeds
-            # max_position_embeddings (the original frequencies below that)
-            ntk = max(reference_rope_seq_len(min_positions), self.max_position_embeddings)
+        if self.dynamic:
+            L = min_positions if ntk_positions is None else int(ntk_positions)
+            orig = self.max_position_embeddings
+            if not (orig <= L <= self._dyn_cached):
+                R = reference_rope_seq_len(L)
+                if R > self._dyn_cached:
+                    self._dyn_cached = R  # growth
+                if R < orig and self._dyn_cached > orig:
+                    self._dyn_cached = orig  # reset to the original frequencies
+            ntk = self._dyn_cached
         key = (str(device), ntk)
         hit = self._cache.get(key)
         if hit is not None and hit[2] >= min_positions:

@@ -100,6 +100,20 @@ def _in_backward() -> bool:
     return torch._C._current_graph_task_id() != -1
 
 
+def _grad_to_main(p: torch.Tensor) -> None:
+    """Post-accumulate-grad hook: move an autograd-produced .grad into the parameter's flat-buffer slice."""
+    g = p.grad
+    mg = getattr(p, "main_grad", None)
+    if g is None or mg is None or mg.numel() != g.numel():
+        return  # no buffer bound right now: finish_backward absorbs the .grad
+    if getattr(p, "grad_added", False):
+        mg.add_(g.view_as(mg))
+    else:
+        mg.copy_(g.view_as(mg))
+    p.grad_added = True
+    p.grad = None
+
+
 @dataclass
 class _Unit:
     idx: int
@@ -119,6 +133,7 @@ class _Unit:
     gshard_valid: bool = False      # gshard holds this step's first reduced micro-batch
     gathered: bool = True
     ag_event: object = None
+    ag_kind: str = "opt"  # the stream ag_event comes from: "comm" (all-gather) or "opt" (AdamW)
     hook_handles: list = field(default_factory=list)
     opt_event: object = None        # async AdamW of this unit done (stage 3 shard update)
     replicated: bool = False
@@ -225,9 +240,18 @@ class DataParallelEngine:
                            else None)
         self.copy_stream = (torch.cuda.Stream(device=dev) if (self.cuda and (self.offload or self.offload_params))
                             else None)
+        # exposed-wait meter (bench.py): when a dict, every point where the compute stream waits on the
+        # comm / optimizer stream is bracketed by two timing events on the compute stream; their
+        # distance is how long the compute stream stalled there (no host synchronisation)
+        self.wait_meter: dict | None = None
         # models built from our fused ops write weight grads straight into the flat buffers; others
-        # (transformers modules) leave ordinary .grad tensors that are absorbed after backward
-        self.autograd_grads = not getattr(model, "writes_main_grad", True)
+        # (transformers modules) produce ordinary .grad tensors: a post-accumulate-grad hook per parameter
+        # moves each one into the flat buffer as soon as autograd has it (FSDP2's mechanism), so those
+        # models get the same transient gradient ring and per-unit overlapped reduction
+        # (LLMT_GRAD_HOOKS=0: absorb the .grad tensors after backward instead)
+        self.grad_hooks = (not getattr(model, "writes_main_grad", True)
+                           and os.environ.get("LLMT_GRAD_HOOKS", "1") != "0")
+        self.autograd_grads = not getattr(model, "writes_main_grad", True) and not self.grad_hooks
         if shard_gradients is None:
             shard_gradients = os.environ.get("LLMT_SHARD_GRADS", "1") != "0"
         self.shard_gradients = (bool(shard_gradients) and self.stage >= 2 and self.sharded
@@ -238,6 +262,10 @@ class DataParallelEngine:
         self.units: list[_Unit] = []
         self._build_units()
         self._install_hooks()
+        if self.grad_hooks:
+            for u in self.units:
+                for p in u.params:
+                    u.hook_handles.append(p.register_post_accumulate_grad_hook(_grad_to_main))
         # units whose module is never called in forward cannot wait for their own parameter
         # all-gather in a pre-forward hook: then the whole comm stream is awaited at step start
         self.global_wait = any(u.module is not None and not _hookable(u.module) for u in self.units)
@@ -339,6 +367,8 @@ class DataParallelEngine:
             else:
                 u.master = u.master.cpu().pin_memory() if pin else u.master.cpu()
             gdt = self.reduce_dtype if (stage >= 1 and sharded) else self.grad_dtype
+            if gdt == torch.float16:  # the host AdamW reads bf16 / fp32: fp16 gradients land upcast
+                gdt = torch.float32
             u.g_host = torch.empty(u.master.numel(), dtype=gdt, pin_memory=pin)
             # bf16 models: the host kernel also writes the bf16 copy that is uploaded; fp32 models
             # upload the master itself
@@ -448,6 +478,34 @@ class DataParallelEngine:
         u.pslot = slot
         self._bind_params(u, slot["buf"][:u.numel])
 
+    # ------------------------------------------------------------------ exposed-wait meter
+    def _xwait(self, what, kind: str):
+        """The current (compute) stream waits for ``what`` (an event or a stream) of kind "comm" (RCCL on
+        the comm stream) or "opt" (the optimizer stream); metered when ``wait_meter`` is set."""
+        cur = torch.cuda.current_stream()
+        m = self.wait_meter
+        if m is not None:
+            a = torch.cuda.Event(enable_timing=True)
+            a.record(cur)
+        if isinstance(what, torch.cuda.Event):
+            cur.wait_event(what)
+        else:
+            cur.wait_stream(what)
+        if m is not None:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record(cur)
+            m.setdefault(kind, []).append((a, b))
+
+    @staticmethod
+    def wait_meter_ms(meter: dict) -> dict[str, float]:
+        """Total stall (ms) per kind of a finished meter (call after a device synchronize)."""
+        return {k: float(sum(a.elapsed_time(b) for a, b in v)) for k, v in meter.items()}
+
+    def _ag_wait(self, u: _Unit):
+        if u.ag_event is not None:
+            self._xwait(u.ag_event, u.ag_kind)
+            u.ag_event = None
+
     # ------------------------------------------------------------------ transient gradient buffers
     def _grad_allocated(self, u: _Unit) -> bool:
         return u.gslot is not None
@@ -464,7 +522,7 @@ class DataParallelEngine:
         self._gpool_next = (self._gpool_next + 1) % len(self._gpool)
         assert slot["owner"] is None, "gradient ring exhausted: a slot's owner never reduced it"
         if slot["event"] is not None:  # its previous reduce-scatter must have read it
-            torch.cuda.current_stream().wait_event(slot["event"])
+            self._xwait(slot["event"], "comm")
             slot["event"] = None
         slot["owner"] = u.idx
         u.gslot = slot
@@ -502,9 +560,8 @@ class DataParallelEngine:
                 nxt = self.units[u.idx + 1] if u.idx + 1 < len(self.units) else None
                 if nxt is not None and not recompute and self._zero3(nxt):
                     self._gather_unit(nxt, async_=True)
-            elif u.ag_event is not None:
-                torch.cuda.current_stream().wait_event(u.ag_event)
-                u.ag_event = None
+            else:
+                self._ag_wait(u)
             if (torch.is_grad_enabled() and not recompute and (self.sharded or self.pc.tp)
                     and not self.autograd_grads):
                 for a in args:
@@ -555,13 +612,12 @@ class DataParallelEngine:
     # ------------------------------------------------------------------ stage-3 gather / release
     def _gather_unit(self, u: _Unit, async_: bool = False):
         if u.gathered:
-            if u.ag_event is not None and not async_:
-                torch.cuda.current_stream().wait_event(u.ag_event)
-                u.ag_event = None
+            if not async_:
+                self._ag_wait(u)
             return
         self._alloc_full(u)
         if self.cuda and u.opt_event is not None:
-            torch.cuda.current_stream().wait_event(u.opt_event)  # updated shard (async AdamW)
+            self._xwait(u.opt_event, "opt")  # updated shard (async AdamW)
             u.opt_event = None
         if self.cuda and self.comm_stream is not None:
             ev = torch.cuda.Event()
@@ -571,10 +627,9 @@ class DataParallelEngine:
                 self._all_gather_params(u)
                 done = torch.cuda.Event()
                 done.record(self.comm_stream)
-            u.ag_event = done
+            u.ag_event, u.ag_kind = done, "comm"
             if not async_:
-                torch.cuda.current_stream().wait_event(done)
-                u.ag_event = None
+                self._ag_wait(u)
         else:
             self._all_gather_params(u)
         u.gathered = True
@@ -692,9 +747,8 @@ class DataParallelEngine:
             self.wait_params()
         elif self.cuda:
             for u in self.units:  # units without a forward hook (TP-replicated norms): wait here
-                if u.module is None and u.ag_event is not None:
-                    torch.cuda.current_stream().wait_event(u.ag_event)
-                    u.ag_event = None
+                if u.module is None:
+                    self._ag_wait(u)
 
     def begin_micro(self, i: int):
         if i > 0:
@@ -714,6 +768,9 @@ class DataParallelEngine:
 
     def finish_backward(self):
         """Called after the last micro-batch's backward: reduce units whose hook did not fire."""
+        if self.cuda:
+            from ..ops.fused import drop_dy_t
+            drop_dy_t()  # no transposed input gradient outlives the backward that produced it
         for u in self.units:
             if u.transient_grad:
                 if not u.reduced and (self._grad_allocated(u) or not u.gshard_valid):
@@ -735,7 +792,7 @@ class DataParallelEngine:
                         p.grad_added = True
                 self._reduce_unit(u)
         if self.comm_stream is not None:
-            torch.cuda.current_stream().wait_stream(self.comm_stream)
+            self._xwait(self.comm_stream, "comm")
 
     def _grad_shard(self, u: _Unit) -> torch.Tensor:
         if self._ustage(u) >= 1 and self._usharded(u):
@@ -760,7 +817,7 @@ class DataParallelEngine:
         """Global grad norm computed on device; returns the device scalar scale used by the optimizer.
         ``loss_scale``: the fp16 loss scale the gradients carry (divided out of the norm and the update)."""
         if self.opt_stream is not None:
-            torch.cuda.current_stream().wait_stream(self.opt_stream)
+            self._xwait(self.opt_stream, "opt")
         denom = float(self.dp * self.accum) * float(loss_scale)
         need_norm = max_norm is not None and max_norm > 0
         sumsq = torch.zeros(1, device=self.device, dtype=torch.float32)
@@ -879,6 +936,8 @@ class DataParallelEngine:
                 g = u.g_host
             else:
                 g = grads[i].contiguous()
+                if g.dtype == torch.float16:
+                    g = g.float()
             lib().adamw_cpu_(u.master, u.exp_avg, u.exp_avg_sq, g, u.p_host, lr, b1, b2, self.eps,
                              self.weight_decay, self.step_count, scale)
             done = None
@@ -927,6 +986,8 @@ class DataParallelEngine:
             u.sec = None  # an hpZ secondary copy holds last step's parameters
         else:
             u.ag_event = done
+            u.ag_kind = "comm" if (self.stage in (1, 2) and self._usharded(u) and self.comm_stream is not None) \
+                else "opt"
 
     def wait_params(self):
         """Make the current stream wait for every pending update / parameter all-gather."""

@@ -4,11 +4,17 @@ Reference: ``loss_parallel()`` around F.cross_entropy on vocab-sharded DTensor l
 (src/llm_training/lms/clm/clm.py:113-134) and the manual vocab-window gather + all_reduce of DPO/ORPO
 log-probs (lms/dpo/dpo.py:89-108, lms/orpo/orpo.py:68-87) — SURVEY K10/P7.
 
-Here each TP rank multiplies the (sequence-gathered) hidden states by its lm_head vocab shard, the
-HIP CE kernel produces the LOCAL log-sum-exp and target logit per row, ONE all-gather of the
-[tp, N] lse rows and ONE all-reduce of the target logits (N fp32 each) combine them, and a second
-kernel pass writes the local dlogits in place. dh is returned as a per-rank partial: the
+Cross-entropy runs in ONE pass over the local logits, chunk by chunk: each TP rank multiplies its
+(sequence-gathered) hidden-state chunk by its lm_head vocab shard, the HIP CE kernel produces the LOCAL
+log-sum-exp and target logit per row, ONE small all-gather of the packed (lse, target) pairs of that chunk
+(2 x rows fp32 per rank) gives the global values, and the same kernel then turns the chunk's logits into
+d loss / d logits in place, which feed the chunk's dh rows and dW contribution right away: three GEMMs
+per chunk (logits, dh, dW) and no second lm_head GEMM. dh is returned as a per-rank partial: the
 sequence-gather that produced h reduce-scatters (sums) it on the way back.
+
+Token log-probs (DPO / ORPO) need the upstream gradient, so their logits are either kept for the backward
+(when the local logits of all rows fit ``keep_budget`` bytes) or recomputed there; the local (lse, target,
+row sum) triples of all chunks meet in one all-gather.
 
 When the vocabulary does not divide by the TP degree the last shard carries zero padding rows
 (``ceil(V / tp)`` rows per rank); only the first ``n_valid`` rows of a shard are multiplied, so the
@@ -24,11 +30,12 @@ from ..ops.fused import _apply_weight_grad, dw_accumulator, dw_add_chunk, mm_nn,
 from ..ops.native import lib, use_native
 
 
-def _combine_lse(lse_local: torch.Tensor, group) -> torch.Tensor:
+def _combine(stats: torch.Tensor, group) -> torch.Tensor:
+    """All-gather the [k, n] local row statistics of every TP rank -> [tp, k, n] (one collective)."""
     n = dist.get_world_size(group)
-    allv = torch.empty(n * lse_local.numel(), dtype=lse_local.dtype, device=lse_local.device)
-    dist.all_gather_into_tensor(allv, lse_local.contiguous(), group=group)
-    return torch.logsumexp(allv.view(n, -1), dim=0)
+    allv = torch.empty(n * stats.numel(), dtype=stats.dtype, device=stats.device)
+    dist.all_gather_into_tensor(allv, stats.contiguous().view(-1), group=group)
+    return allv.view(n, *stats.shape)
 
 
 def _local_stats(lg, lab, v0, ignore_index, native, rowsum=None):
@@ -65,30 +72,16 @@ def _local_grad(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, native):
 
 
 class _VPFusedCE(Function):
-    """Vocab-parallel fused linear + CE, memory bounded by one local logits chunk: pass 1 computes the
-    local (lse, target logit) per chunk and drops the logits; after the TP combine, pass 2 recomputes
-    each chunk's logits, turns them into d loss / d logits in place and produces that chunk's dh rows
-    and dW contribution immediately (one extra GEMM instead of O(N * V/tp) saved logits)."""
+    """Vocab-parallel fused linear + CE in one pass, memory bounded by one local logits chunk: per chunk
+    the local logits, one all-gather of their (lse, target) rows, d loss / d logits in place, dh and dW."""
 
     @staticmethod
     def forward(ctx, h, w_full, labels, v0, ignore_index, group, chunk, n_valid):
         native = use_native(h)
         N = h.shape[0]
         w = w_full[:n_valid]
-        inv_n = (1.0 / (labels != ignore_index).sum().clamp(min=1).float()).reshape(1)
-        lses, tgts = [], []
-        for s0 in range(0, N, chunk):
-            s1 = min(N, s0 + chunk)
-            lg = mm_nt(h[s0:s1], w)
-            lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
-            lses.append(lse)
-            tgts.append(tgt)
-            del lg
-        lse = _combine_lse(torch.cat(lses), group)
-        tgt = torch.cat(tgts)
-        dist.all_reduce(tgt, group=group)
         valid = labels != ignore_index
-        loss = ((lse - tgt) * valid).sum() * inv_n[0]
+        inv_n = (1.0 / valid.sum().clamp(min=1).float()).reshape(1)
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dh = torch.empty_like(h) if need_h else None
         dw_full = dw_accumulator(w_full, N, chunk) if need_w else None
@@ -96,19 +89,27 @@ class _VPFusedCE(Function):
         if need_w and n_valid < w_full.shape[0]:
             dw_full[n_valid:].zero_()
         wt = weight_t(w, N) if need_h and native and N > chunk else None
+        loss = torch.zeros((), device=h.device, dtype=torch.float32)
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
+            lab = labels[s0:s1]
             lg = mm_nt(h[s0:s1], w)
-            _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), None, inv_n, native)
-            if need_h:
-                mm_nn(lg, w, out=dh[s0:s1], wt=wt)
-            if need_w:
-                dw_add_chunk(dw, lg, h[s0:s1], s0 == 0)
+            lse_l, tgt_l = _local_stats(lg, lab, v0, ignore_index, native)
+            allv = _combine(torch.stack([lse_l.float(), tgt_l.float()]), group)
+            lse = torch.logsumexp(allv[:, 0], dim=0)
+            tgt = allv[:, 1].sum(0)  # the target logit lives in exactly one rank's vocabulary window
+            loss += ((lse - tgt) * valid[s0:s1]).sum()
+            if need_h or need_w:
+                _local_grad(lg, lab, v0, ignore_index, lse.contiguous(), None, inv_n, native)
+                if need_h:
+                    mm_nn(lg, w, out=dh[s0:s1], wt=wt)
+                if need_w:
+                    dw_add_chunk(dw, lg, h[s0:s1], s0 == 0)
             del lg
         ctx.save_for_backward(*(t for t in (dh, dw_full) if t is not None))
         ctx.has = (need_h, need_w)
         ctx.w = w_full
-        return loss
+        return loss * inv_n[0]
 
     @staticmethod
     def backward(ctx, g):
@@ -123,26 +124,31 @@ class _VPFusedCE(Function):
 
 
 class _VPLogps(Function):
+    """Vocab-parallel token log-probs: local stats per chunk, one all-gather of every row's (lse, target,
+    logit row sum), logits kept for the backward when they fit ``keep_budget`` bytes (else recomputed)."""
+
     @staticmethod
-    def forward(ctx, h, w_full, labels, v0, ignore_index, group, chunk, n_valid):
+    def forward(ctx, h, w_full, labels, v0, ignore_index, group, chunk, n_valid, keep_budget):
         native = use_native(h)
         N = h.shape[0]
         w = w_full[:n_valid]
-        lses, tgts = [], []
-        rowsum = torch.zeros(N, device=h.device, dtype=torch.float32)
+        keep = ctx.needs_input_grad[0] and N * n_valid * h.element_size() <= keep_budget
+        stats = torch.zeros(3, N, device=h.device, dtype=torch.float32)
+        kept = []
         for s0 in range(0, N, chunk):
             s1 = min(N, s0 + chunk)
             lg = mm_nt(h[s0:s1], w)
-            lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native, rowsum[s0:s1])
-            lses.append(lse)
-            tgts.append(tgt)
-        lse = _combine_lse(torch.cat(lses), group)
-        # target logits and the per-row logit sums (ORPO metrics) in one all-reduce
-        both = torch.stack([torch.cat(tgts), rowsum])
-        dist.all_reduce(both, group=group)
-        tgt, rowsum = both[0], both[1].contiguous()
+            lse, tgt = _local_stats(lg, labels[s0:s1], v0, ignore_index, native, stats[2, s0:s1])
+            stats[0, s0:s1] = lse
+            stats[1, s0:s1] = tgt
+            if keep:
+                kept.append(lg)
+        allv = _combine(stats, group)
+        lse = torch.logsumexp(allv[:, 0], dim=0)
+        tgt, rowsum = allv[:, 1].sum(0), allv[:, 2].sum(0).contiguous()
         valid = labels != ignore_index
         ctx.save_for_backward(h, labels, lse)
+        ctx.kept = kept if keep else None
         ctx.w = w_full
         ctx.cfg = (v0, ignore_index, chunk, n_valid)
         ctx.mark_non_differentiable(rowsum)
@@ -153,6 +159,7 @@ class _VPLogps(Function):
         h, labels, lse = ctx.saved_tensors
         w_full = ctx.w
         v0, ignore_index, chunk, n_valid = ctx.cfg
+        kept, ctx.kept = ctx.kept, None
         w = w_full[:n_valid]
         native = use_native(h)
         N = h.shape[0]
@@ -162,14 +169,17 @@ class _VPLogps(Function):
         if n_valid < w_full.shape[0]:
             dw[n_valid:].zero_()
         wt = weight_t(w, N) if native and N > chunk else None
-        for s0 in range(0, N, chunk):
+        for i, s0 in enumerate(range(0, N, chunk)):
             s1 = min(N, s0 + chunk)
-            lg = mm_nt(h[s0:s1], w)
+            lg = kept[i] if kept is not None else mm_nt(h[s0:s1], w)
             _local_grad(lg, labels[s0:s1], v0, ignore_index, lse[s0:s1].contiguous(), coef[s0:s1], None, native)
             mm_nn(lg, w, out=dh[s0:s1], wt=wt)
             dw_add_chunk(dw[:n_valid], lg, h[s0:s1], s0 == 0)
+            if kept is not None:
+                kept[i] = None
+            del lg
         one = torch.ones((), device=dw.device, dtype=torch.float32)
-        return dh, _apply_weight_grad(w_full, dw, one), None, None, None, None, None, None
+        return dh, _apply_weight_grad(w_full, dw, one), None, None, None, None, None, None, None
 
 
 def _n_valid(w_local, vocab_start, vocab_size):
@@ -185,10 +195,14 @@ def vocab_parallel_cross_entropy(h, w_local, labels, vocab_start, group, ignore_
                             chunk_size, _n_valid(w_local, vocab_start, vocab_size))
 
 
+# local logits kept from the log-prob forward for its backward (no lm_head recompute) up to this many bytes
+LOGPS_KEEP_BYTES = [8 << 30]
+
+
 def vocab_parallel_token_logps(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192,
                                vocab_size: int | None = None, logit_sums: bool = False):
     shape = labels.shape
     h = h.reshape(-1, h.shape[-1]).contiguous()
     out, rs = _VPLogps.apply(h, w_local, labels.reshape(-1).contiguous(), int(vocab_start), ignore_index, group,
-                             chunk_size, _n_valid(w_local, vocab_start, vocab_size))
+                             chunk_size, _n_valid(w_local, vocab_start, vocab_size), LOGPS_KEEP_BYTES[0])
     return (out.view(shape), rs.view(shape)) if logit_sums else out.view(shape)

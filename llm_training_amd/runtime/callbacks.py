@@ -12,6 +12,7 @@ from __future__ import annotations
 import io
 import json
 import logging
+import math
 import os
 import re
 import shutil
@@ -133,10 +134,23 @@ class ModelCheckpoint(Callback):
         if path is None:
             return
         from ..ckpt.checkpoint import is_complete, wait_for_pending_saves
-        wait_for_pending_saves()
-        if dist.is_available() and dist.is_initialized():
-            dist.barrier()
+        err = None
+        try:
+            wait_for_pending_saves()
+        except Exception as e:  # noqa: BLE001 - re-raised below on every rank
+            err = e
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            # a background write that failed on one rank fails the save on every rank (instead of the
+            # others waiting in the barrier for a rank that has already raised)
+            dev = getattr(trainer, "device", None)
+            flag = torch.tensor([1.0 if err is not None else 0.0],
+                                device=dev if dev is not None and dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(flag)
+            if err is None and float(flag.item()) > 0:
+                err = RuntimeError(f"checkpoint {path}: a background write failed on another rank")
         self._pending = None
+        if err is not None:
+            raise err
         if not is_complete(path):
             logger.error("checkpoint %s is incomplete; keeping the previous checkpoints", path)
             return
@@ -179,6 +193,81 @@ class ModelCheckpoint(Callback):
 
     def on_fit_end(self, trainer, lm):
         self.finalize(trainer)
+
+
+class EarlyStopping(Callback):
+    """Lightning's EarlyStopping: stop when ``monitor`` has not improved by more than ``min_delta`` for
+    ``patience`` consecutive checks (validation ends, or training epoch ends with
+    ``check_on_train_epoch_end``). ``check_finite`` stops on a NaN / inf value, ``stopping_threshold``
+    once the value is good enough, ``divergence_threshold`` once it is hopeless. The stop is a request
+    (``trainer.should_stop``) that ``min_steps`` / ``min_epochs`` can defer; the counters are saved in
+    checkpoints. Every rank reads the same DP-averaged metric, so every rank decides alike."""
+
+    def __init__(self, monitor: str, min_delta: float = 0.0, patience: int = 3, verbose: bool = False,
+                 mode: str = "min", strict: bool = True, check_finite: bool = True,
+                 stopping_threshold: float | None = None, divergence_threshold: float | None = None,
+                 check_on_train_epoch_end: bool | None = None, log_rank_zero_only: bool = False):
+        if mode not in ("min", "max"):
+            raise ValueError(f"EarlyStopping mode must be 'min' or 'max', got {mode!r}")
+        self.monitor, self.patience, self.verbose, self.mode, self.strict = monitor, int(patience), verbose, mode, strict
+        self.min_delta = abs(float(min_delta)) * (-1.0 if mode == "min" else 1.0)
+        self.check_finite = check_finite
+        self.stopping_threshold, self.divergence_threshold = stopping_threshold, divergence_threshold
+        self.check_on_train_epoch_end = check_on_train_epoch_end
+        self.wait_count = 0
+        self.best_score = float("inf") if mode == "min" else -float("inf")
+        self.stopped_epoch = 0
+        self.stopping_reason: str | None = None
+
+    def _better(self, a: float, b: float) -> bool:
+        return a < b if self.mode == "min" else a > b
+
+    def _check(self, trainer, metrics: dict):
+        if self.monitor not in metrics:
+            if self.strict:
+                raise RuntimeError(f"EarlyStopping: monitored metric {self.monitor!r} is not available; have "
+                                   f"{sorted(metrics)} (set strict=False to skip)")
+            return
+        cur = float(metrics[self.monitor])
+        reason = None
+        if self.check_finite and not math.isfinite(cur):
+            reason = f"{self.monitor} = {cur} is not finite"
+        elif self.stopping_threshold is not None and self._better(cur, self.stopping_threshold):
+            reason = f"{self.monitor} = {cur:.6g} reached the stopping threshold {self.stopping_threshold}"
+        elif self.divergence_threshold is not None and self._better(self.divergence_threshold, cur):
+            reason = f"{self.monitor} = {cur:.6g} is past the divergence threshold {self.divergence_threshold}"
+        elif self._better(cur - self.min_delta, self.best_score):
+            self.best_score, self.wait_count = cur, 0
+            if self.verbose:
+                logger.info("EarlyStopping: %s improved to %.6g", self.monitor, cur)
+        else:
+            self.wait_count += 1
+            if self.wait_count >= self.patience:
+                reason = (f"{self.monitor} did not improve by more than {abs(self.min_delta)} in the last "
+                          f"{self.wait_count} checks; best {self.best_score:.6g}")
+        if reason is not None:
+            self.stopping_reason = reason
+            self.stopped_epoch = trainer.state.epoch
+            trainer.should_stop = True
+            logger.info("EarlyStopping at step %d: %s", trainer.global_step, reason)
+
+    def on_validation_end(self, trainer, lm, metrics: dict):
+        if not self.check_on_train_epoch_end:
+            self._check(trainer, metrics)
+
+    def on_train_epoch_end(self, trainer, lm):
+        if self.check_on_train_epoch_end:
+            trainer._flush_logs(force=True)
+            self._check(trainer, trainer.last_metrics)
+
+    def state_dict(self) -> dict:
+        return {"wait_count": self.wait_count, "best_score": self.best_score, "stopped_epoch": self.stopped_epoch,
+                "patience": self.patience}
+
+    def load_state_dict(self, st: dict):
+        self.wait_count = int(st["wait_count"])
+        self.best_score = float(st["best_score"])
+        self.stopped_epoch = int(st.get("stopped_epoch", 0))
 
 
 def _remove_checkpoint(path: str):

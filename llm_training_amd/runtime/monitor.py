@@ -27,6 +27,7 @@ import logging
 import os
 import re
 import sys
+import threading
 import time
 import traceback
 from pathlib import Path
@@ -198,6 +199,64 @@ class StallWatchdog:
         if self._f is not None:
             self._f.close()
             self._f = None
+
+
+class StepWatchdog:
+    """Fail fast instead of hanging: if the phase armed by ``arm(label)`` does not end (next ``arm`` or
+    ``disarm``) within its time limit, write ``[rank r] watchdog: <label> exceeded T s`` and every
+    thread's stack to stderr and end the process with ``exit_code`` (``os._exit``: a rank blocked in a
+    collective cannot unwind). The launcher (``launch.py``) then stops the other ranks and returns that
+    code, so a stuck RCCL collective ends a multi-GPU run in seconds with every rank's stacks instead of
+    running into the job's outer time limit. A Python timer thread does the labelled dump; a
+    ``faulthandler`` timer 30 s later is the backstop for a rank whose interpreter lock is held.
+    Reference: Lightning / NCCL rely on the 30-minute process-group timeout
+    (src/llm_training/lightning/strategy/fsdp2/fsdp2_strategy.py:411-420)."""
+
+    def __init__(self, rank: int = 0, timeout: float = 120.0, exit_code: int = 3, stream=None):
+        self.rank = rank
+        self.timeout = float(timeout)
+        self.exit_code = exit_code
+        self.stream = stream if stream is not None else sys.stderr
+        self._gen = 0
+        self._lock = threading.Lock()
+
+    def arm(self, label: str, timeout: float | None = None):
+        t = self.timeout if timeout is None else float(timeout)
+        with self._lock:
+            self._gen += 1
+            gen = self._gen
+        faulthandler.cancel_dump_traceback_later()
+        if t <= 0:
+            return
+        faulthandler.dump_traceback_later(t + 30.0, repeat=False, file=self.stream, exit=True)
+        th = threading.Thread(target=self._watch, args=(gen, label, t), daemon=True, name="llmt-step-watchdog")
+        th.start()
+
+    def disarm(self):
+        with self._lock:
+            self._gen += 1
+        faulthandler.cancel_dump_traceback_later()
+
+    def _watch(self, gen: int, label: str, t: float):
+        deadline = time.monotonic() + t
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                break
+            time.sleep(min(left, 0.5))
+            with self._lock:
+                if self._gen != gen:
+                    return
+        with self._lock:
+            if self._gen != gen:
+                return
+        try:
+            self.stream.write(f"[rank {self.rank}] watchdog: {label} exceeded {t:.0f} s; stacks of every thread:\n")
+            self.stream.flush()
+            faulthandler.dump_traceback(file=self.stream, all_threads=True)
+            self.stream.flush()
+        finally:
+            os._exit(self.exit_code)
 
 
 _STEP_RE = re.compile(r"step=(\d+)")

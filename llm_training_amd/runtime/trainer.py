@@ -33,6 +33,7 @@ from .monitor import (StallWatchdog, StepProfiler, ThroughputMeter, find_last_ch
 from .strategies import Strategy, resolve_strategy
 
 logger = logging.getLogger("llm_training")
+_log = logger  # for Trainer.__init__, whose `logger` argument shadows the module logger
 
 # precision -> (parameter / compute dtype, gradient accumulation + reduction dtype)
 #  * bf16-true : bf16 params, bf16 gradients, fp32 master weights + Adam state (reference bf16-true with
@@ -80,13 +81,14 @@ class LossScaler:
 
     def load_state_dict(self, st):
         self.scale, self.good_steps, self.skipped = float(st["scale"]), int(st["good_steps"]), int(st["skipped"])
-# Lightning Trainer arguments that exist upstream but have no effect here: accepted (with a warning)
-# so reference configs load; anything else is a typo and raises, as jsonargparse would
-IGNORED_TRAINER_ARGS = {"benchmark", "fast_dev_run",
-                        "overfit_batches", "profiler", "detect_anomaly", "barebones", "plugins",
-                        "sync_batchnorm", "reload_dataloaders_every_n_epochs", "enable_model_summary",
-                        "inference_mode", "use_distributed_sampler", "min_epochs", "min_steps",
-                        "limit_test_batches", "limit_predict_batches", "move_metrics_to_cpu"}
+# Lightning Trainer arguments that have nothing to act on in this framework, so accepting them is exactly
+# Lightning's behaviour here: cuDNN autotuning (no convolutions), BatchNorm sync (none in these models),
+# the model-summary printout flag (a summary is logged at setup), inference vs no-grad validation (same
+# numbers), dataloader reloading (the loaders are rebuilt every epoch), metric placement, and the
+# test / predict loops (not part of `fit`). Everything else Lightning offers is implemented below or
+# raises; a misspelled argument raises with a suggestion, as jsonargparse would.
+IGNORED_TRAINER_ARGS = {"benchmark", "sync_batchnorm", "reload_dataloaders_every_n_epochs", "enable_model_summary",
+                        "inference_mode", "limit_test_batches", "limit_predict_batches", "move_metrics_to_cpu"}
 
 
 def parse_max_time(v: Any) -> float | None:
@@ -135,7 +137,10 @@ class Trainer:
                  limit_val_batches: Any = None, enable_checkpointing: bool = True, enable_progress_bar: bool = True,
                  default_root_dir: str = "logs", num_sanity_val_steps: int = 2, seed: int | None = None,
                  deterministic: bool = False, benchmark: Any = None, gemm_tuning: str | None = None,
-                 max_time: Any = None, **unused):
+                 max_time: Any = None, fast_dev_run: Any = False, overfit_batches: Any = 0.0,
+                 min_epochs: int | None = None, min_steps: int | None = None, profiler: Any = None,
+                 detect_anomaly: bool = False, barebones: bool = False, plugins: Any = None,
+                 use_distributed_sampler: bool = True, enable_model_summary: bool = True, **unused):
         self.strategy: Strategy = resolve_strategy(strategy)
         # devices / num_nodes decide how many ranks llm_training_amd.launch starts; inside a rank the
         # accelerator picks the device type (cpu -> gloo ranks)
@@ -177,7 +182,40 @@ class Trainer:
             raise TypeError("Trainer got unknown argument(s): " + ", ".join(
                 f"{k!r}" + (f" (did you mean {h[0]!r}?)" if h else "") for k, h in hint.items()))
         if unused:
-            logger.info("Trainer: arguments without effect in this framework: %s", sorted(unused))
+            _log.info("Trainer: arguments with nothing to act on in this framework: %s", sorted(unused))
+        if plugins:
+            raise ValueError("Trainer(plugins=...) is not supported: precision and cluster environments are "
+                             "built in (precision=..., the launcher / torchrun / srun environment)")
+        self.min_epochs = int(min_epochs) if min_epochs is not None else None
+        self.min_steps = int(min_steps) if min_steps is not None else None
+        self.detect_anomaly = bool(detect_anomaly)
+        self.use_distributed_sampler = bool(use_distributed_sampler)
+        self.enable_model_summary = bool(enable_model_summary) and not barebones
+        self.fit_profiler = make_fit_profiler(profiler)
+        # Lightning debugging flags (trainer/connectors: _init_debugging_flags)
+        if fast_dev_run is True:
+            fast_dev_run = 1
+        self.fast_dev_run = int(fast_dev_run or 0)
+        if self.fast_dev_run < 0:
+            raise ValueError(f"fast_dev_run must be a bool or a non-negative int, got {fast_dev_run!r}")
+        self.overfit_batches = overfit_batches if overfit_batches else 0
+        if self.fast_dev_run:
+            # N training batches, then N validation batches; no sanity check, loggers, checkpoints or time limit
+            n = self.fast_dev_run
+            self.max_steps, self.max_epochs, self.max_time = n, 1, None
+            self.limit_train_batches, self.limit_val_batches = n * self.accumulate_grad_batches, n
+            self.val_check_interval, self.check_val_every_n_epoch, self.num_sanity_val_steps = 1.0, 1, 0
+            self.loggers, self.enable_checkpointing = [], False
+            _log.info("fast_dev_run=%d: %d training + %d validation batch(es); loggers and checkpoints off", n, n, n)
+        elif self.overfit_batches:
+            # the same first batches every epoch (no shuffling), validation limited alike
+            self.limit_train_batches = self.overfit_batches
+            self.limit_val_batches = self.overfit_batches
+        if barebones:
+            # Lightning barebones: no logging, progress bar, checkpointing, summary or profiler
+            if self.fit_profiler is not None:
+                raise ValueError("barebones=True cannot be combined with a profiler")
+            self.loggers, self.enable_checkpointing, self.enable_progress_bar = [], False, False
         if precision not in PRECISIONS:
             raise ValueError(f"unknown precision {precision!r}; use one of bf16-true, bf16-mixed, 32-true")
         if PRECISIONS[precision] is None:
@@ -255,6 +293,13 @@ class Trainer:
         torch.manual_seed(seed + self.pc.dp_rank + 1_000_003 * self.pc.tp_rank)
         if ckpt_path == "last":
             ckpt_path = self.resolve_last_checkpoint()
+        if not self.enable_checkpointing:
+            from .callbacks import ModelCheckpoint
+            dropped = [cb for cb in self.callbacks if isinstance(cb, ModelCheckpoint)]
+            if dropped:
+                logger.info("checkpointing off (%s): %d ModelCheckpoint callback(s) inactive",
+                            "fast_dev_run" if self.fast_dev_run else "enable_checkpointing=False", len(dropped))
+                self.callbacks = [cb for cb in self.callbacks if not isinstance(cb, ModelCheckpoint)]
         self.lm, self.datamodule = lm, datamodule
         for cb in self.callbacks:
             _call(cb, "setup", self, lm, "fit")
@@ -282,6 +327,8 @@ class Trainer:
                                          reshard_after_forward=st.reshard_after_forward,
                                          overlap_comm=st.overlap_comm, **st.engine_kwargs())
         _call(lm, "on_engine_ready", self.engine)  # e.g. DPO shards its frozen reference model (ZeRO-3)
+        if self.enable_model_summary and self.pc.rank == 0:
+            log_model_summary(lm.model)
         self.scheduler = lm.build_lr_scheduler(self.base_lr, self.estimated_stepping_batches())
         if ckpt_path:
             from ..ckpt.checkpoint import load_checkpoint
@@ -319,13 +366,18 @@ class Trainer:
         logger.info("ckpt_path=last: resuming from %s", best)
         return best
 
+    def _dp(self) -> tuple[int, int]:
+        """(rank, size) the loaders shard over: the data-parallel group, or (0, 1) with
+        use_distributed_sampler=False (every rank iterates the whole dataset, as in Lightning)."""
+        return (self.pc.dp_rank, self.pc.dp_size) if self.use_distributed_sampler else (0, 1)
+
     def train_loader(self):
-        return self.datamodule.train_dataloader(self.pc.dp_rank, self.pc.dp_size,
-                                                seed=(self.seed if self.seed is not None else 42),
-                                                skip_batches=self.state.batch_idx, epoch=self.state.epoch)
+        kw = {"shuffle": False} if self.overfit_batches else {}
+        return self.datamodule.train_dataloader(*self._dp(), seed=(self.seed if self.seed is not None else 42),
+                                                skip_batches=self.state.batch_idx, epoch=self.state.epoch, **kw)
 
     def num_batches_per_epoch(self) -> int:
-        n = len(self.datamodule.train_dataloader(self.pc.dp_rank, self.pc.dp_size).batch_sampler)
+        n = len(self.datamodule.train_dataloader(*self._dp()).batch_sampler)
         lim = self.limit_train_batches
         if lim is not None:
             n = min(n, int(lim) if (isinstance(lim, int) or float(lim) > 1) else int(n * float(lim)))
@@ -341,6 +393,9 @@ class Trainer:
     # ------------------------------------------------------------------ loop
     def fit(self, lm, datamodule=None, ckpt_path: str | None = None):
         try:
+            if self.fit_profiler is not None:
+                with self.fit_profiler.session(self):
+                    return self._fit(lm, datamodule, ckpt_path)
             return self._fit(lm, datamodule, ckpt_path)
         except Exception as e:
             rank = self.pc.rank if self.pc is not None else int(os.environ.get("RANK", "0"))
@@ -363,23 +418,28 @@ class Trainer:
             # nothing is logged or kept
             self.validate(sanity=True)
         max_epochs = self.max_epochs if self.max_epochs is not None else (1 if self.max_steps <= 0 else 10 ** 9)
+        if self.min_epochs is not None and self.max_epochs is None:
+            max_epochs = max(max_epochs, self.min_epochs)
         lm.train()
         nbe = self.num_batches_per_epoch()
-        while self.state.epoch < max_epochs and not self.should_stop:
+        self._hard_stop = False
+        while self.state.epoch < max_epochs and not self._stopping():
             loader = self.train_loader()
             it = iter(loader)
             accum = self.accumulate_grad_batches
-            while self.state.batch_idx + accum <= nbe and not self.should_stop:
-                batches = [next(it) for _ in range(accum)]
+            while self.state.batch_idx + accum <= nbe and not self._stopping():
+                with self._prof("get_train_batch"):
+                    batches = [next(it) for _ in range(accum)]
                 self.train_step(batches)  # advances batch_idx before the batch-end callbacks run
                 if self.max_steps > 0 and self.state.global_step >= self.max_steps:
-                    self.should_stop = True
+                    self.should_stop = self._hard_stop = True
                 if self.max_time is not None and self._time_is_up():
                     self.should_stop = True
                 if self._should_validate(nbe):
-                    self.validate()
+                    with self._prof("validation"):
+                        self.validate()
             epoch_done = self.state.batch_idx + accum > nbe
-            if epoch_done or self.should_stop:
+            if epoch_done or self._stopping():
                 # Lightning ends the epoch loop also when max_steps / max_time stop it early, so the
                 # epoch-end hooks (ModelCheckpoint(save_on_train_epoch_end) among them) run; the counters
                 # only advance for a completed epoch, so a resume continues mid-epoch
@@ -396,6 +456,26 @@ class Trainer:
         for lg in self.loggers:
             _call(lg, "finalize", "success")
         return self
+
+    def _stopping(self) -> bool:
+        """max_steps ends the run at once; any other stop request (max_time, EarlyStopping, a callback
+        setting ``should_stop``) waits until ``min_steps`` / ``min_epochs`` are met (Lightning's
+        ``_can_stop_early``)."""
+        if not self.should_stop:
+            return False
+        if self._hard_stop:
+            return True
+        ok = ((self.min_steps is None or self.state.global_step >= self.min_steps)
+              and (self.min_epochs is None or self.state.epoch >= self.min_epochs))
+        if not ok and not getattr(self, "_min_note", False):
+            self._min_note = True
+            logger.info("stop requested at step %d but min_steps=%s / min_epochs=%s not met: training continues",
+                        self.state.global_step, self.min_steps, self.min_epochs)
+        return ok
+
+    def _prof(self, action: str):
+        p = self.fit_profiler
+        return p.profile(action) if p is not None else _NULLCTX
 
     def _time_is_up(self) -> bool:
         """max_time reached? Rank 0's clock decides for every rank (Lightning's Timer broadcasts its
@@ -440,6 +520,8 @@ class Trainer:
         if self.meter is not None and self.meter.t0 is None:
             self.meter.start()  # the first logged rate covers the first step's own time
         self.profiler.before_step(self.state.global_step + 1)
+        if self.fit_profiler is not None:
+            self.fit_profiler.before_step(self, self.state.global_step + 1)
         self.watchdog.arm()
         for cb in self.callbacks:
             _call(cb, "on_train_batch_start", self, lm, batches[0], self.state.batch_idx)
@@ -447,18 +529,20 @@ class Trainer:
         eng.zero_grad()
         metrics_acc: dict[str, torch.Tensor] = {}
         counters: dict[str, Any] = {}
+        anomaly = torch.autograd.detect_anomaly(check_nan=True) if self.detect_anomaly else _NULLCTX
         for i, b in enumerate(batches):
             eng.begin_micro(i)
             b = self.to_device(b)
-            with trace_range("forward"):
-                loss, metrics, cnt = lm.training_step(b, self.state.batch_idx + i)
-            with trace_range("backward"):
-                (loss * self.scaler.scale if self.scaler is not None else loss).backward()
+            with anomaly:
+                with trace_range("forward"), self._prof("training_step"):
+                    loss, metrics, cnt = lm.training_step(b, self.state.batch_idx + i)
+                with trace_range("backward"), self._prof("backward"):
+                    (loss * self.scaler.scale if self.scaler is not None else loss).backward()
             for k, v in metrics.items():
                 metrics_acc[k] = metrics_acc.get(k, 0) + v.detach().float().to(self.device) / len(batches)
             for k, v in cnt.items():
                 counters[k] = counters.get(k, 0) + v
-        with trace_range("optimizer"):
+        with trace_range("optimizer"), self._prof("optimizer_step"):
             eng.finish_backward()
             if self.scaler is None:
                 eng.clip_and_scale(self.gradient_clip_val)
@@ -489,6 +573,8 @@ class Trainer:
         self.step_times.append(time.perf_counter() - t0)
         self._count_tokens(batches)
         self.profiler.after_step(self.state.global_step)
+        if self.fit_profiler is not None:
+            self.fit_profiler.after_step(self, self.state.global_step)
         self.watchdog.disarm()
         if self.collectives is not None and self.state.global_step % collective_debug.check_every() == 0:
             self.collectives.verify()
@@ -586,7 +672,7 @@ class Trainer:
     def validate(self, sanity: bool = False):
         if self.datamodule.datasets.get("validation") is None:
             return {}
-        dl = self.datamodule.val_dataloader(self.pc.dp_rank, self.pc.dp_size)
+        dl = self.datamodule.val_dataloader(*self._dp())
         if dl is None:
             return {}
         limit = self._val_batch_limit(dl, sanity)
@@ -634,3 +720,50 @@ def _call(obj, name, *args):
     if fn is not None:
         return fn(*args)
     return None
+
+
+class _NullCtx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+_NULLCTX = _NullCtx()
+
+
+def log_model_summary(model) -> None:
+    """Lightning's model summary, condensed: parameters per top-level module (this rank's shard under TP)."""
+    rows, total, trainable = [], 0, 0
+    for name, mod in model.named_children():
+        n = sum(p.numel() for p in mod.parameters())
+        rows.append(f"  {name:<24} {type(mod).__name__:<28} {n / 1e6:>10.2f} M")
+        total += n
+        trainable += sum(p.numel() for p in mod.parameters() if p.requires_grad)
+    total += sum(p.numel() for p in model.parameters(recurse=False))
+    logger.info("model summary (%s):\n%s\n  total %.2f M parameters, %.2f M trainable", type(model).__name__,
+                "\n".join(rows), total / 1e6, trainable / 1e6)
+
+
+def make_fit_profiler(spec):
+    """Lightning ``Trainer(profiler=...)``: "simple", "advanced", "pytorch", a profiler object, or a
+    ``class_path`` dict naming Lightning's SimpleProfiler / AdvancedProfiler / PyTorchProfiler."""
+    from .profilers import AdvancedProfiler, PyTorchProfiler, SimpleProfiler
+    if spec in (None, False, "", "none"):
+        return None
+    if isinstance(spec, str):
+        table = {"simple": SimpleProfiler, "advanced": AdvancedProfiler, "pytorch": PyTorchProfiler}
+        if spec.lower() not in table:
+            raise ValueError(f"profiler {spec!r}: use 'simple', 'advanced' or 'pytorch'")
+        return table[spec.lower()]()
+    if isinstance(spec, dict) and "class_path" in spec:
+        name = spec["class_path"].rsplit(".", 1)[-1]
+        table = {"SimpleProfiler": SimpleProfiler, "AdvancedProfiler": AdvancedProfiler,
+                 "PyTorchProfiler": PyTorchProfiler}
+        if name not in table:
+            raise ValueError(f"profiler class {spec['class_path']!r} is not supported")
+        return table[name](**(spec.get("init_args") or {}))
+    if hasattr(spec, "profile") and hasattr(spec, "session"):
+        return spec
+    raise TypeError(f"unsupported profiler {spec!r}")

@@ -15,12 +15,19 @@ ALIASES = {
     "deepspeed.ops.adam.DeepSpeedCPUAdam": "llm_training_amd.optim.FusedAdamW",
     "lightning.pytorch.callbacks.LearningRateMonitor": "llm_training_amd.runtime.callbacks.LearningRateMonitor",
     "lightning.pytorch.callbacks.ModelCheckpoint": "llm_training_amd.runtime.callbacks.ModelCheckpoint",
+    "lightning.pytorch.callbacks.EarlyStopping": "llm_training_amd.runtime.callbacks.EarlyStopping",
+    "lightning.pytorch.callbacks.early_stopping.EarlyStopping": "llm_training_amd.runtime.callbacks.EarlyStopping",
+    "lightning.pytorch.callbacks.TQDMProgressBar": "llm_training_amd.runtime.callbacks.TQDMProgressBar",
+    "lightning.pytorch.profilers.SimpleProfiler": "llm_training_amd.runtime.profilers.SimpleProfiler",
+    "lightning.pytorch.profilers.AdvancedProfiler": "llm_training_amd.runtime.profilers.AdvancedProfiler",
+    "lightning.pytorch.profilers.PyTorchProfiler": "llm_training_amd.runtime.profilers.PyTorchProfiler",
 }
 
 SHORT_NAMES = {
     "HFTokenizer": "llm_training_amd.data.tokenizer.HFTokenizer",
     "LearningRateMonitor": "llm_training_amd.runtime.callbacks.LearningRateMonitor",
     "ModelCheckpoint": "llm_training_amd.runtime.callbacks.ModelCheckpoint",
+    "EarlyStopping": "llm_training_amd.runtime.callbacks.EarlyStopping",
     "TrainingTimeEstimator": "llm_training_amd.runtime.callbacks.TrainingTimeEstimator",
     "OutputRedirection": "llm_training_amd.runtime.callbacks.OutputRedirection",
     "CSVLogger": "llm_training_amd.runtime.loggers.CSVLogger",

@@ -237,3 +237,17 @@ def test_fp16_precisions_with_dynamic_loss_scaler(tmp_path, precision):
     assert all(x == x for x in losses)
     t.save_checkpoint(str(tmp_path / "ck"))
     assert ckpt.read_meta(str(tmp_path / "ck"))["loss_scaler"]["scale"] == t.scaler.scale
+
+
+def test_fp16_with_optimizer_offload(tmp_path):
+    """fp16 gradients reach the host AdamW (which reads bf16 / fp32) upcast to fp32: 16-mixed / 16-true
+    with offload_optimizer train instead of failing in the first step."""
+    from llm_training_amd.runtime.strategies import DeepSpeedStrategy
+    for precision in ("16-true", "16-mixed"):
+        t = Trainer(strategy=DeepSpeedStrategy(stage=2, offload_optimizer=True), precision=precision, max_steps=3,
+                    seed=1, default_root_dir=str(tmp_path))
+        lm = _lm()
+        t.fit(lm, _dm())
+        assert t.global_step == 3
+        assert all(u.g_host.dtype == torch.float32 for u in t.engine.units)
+        assert all(torch.isfinite(p).all() for p in lm.model.parameters())

@@ -219,39 +219,68 @@ def test_tensor_sequence_parallel_matches_single_process(world, tp, overlap):
             assert torch.allclose(out[r]["params"][k], v, atol=atol, rtol=1e-4), (r, k)
 
 
-def _vp_worker(rank, world, h, w, labels):
+def _vp_worker(rank, world, h, w, labels, chunk, vocab, keep):
     import torch.distributed as dist
 
-    from llm_training_amd.parallel.vocab_parallel import vocab_parallel_cross_entropy, vocab_parallel_token_logps
+    from llm_training_amd.parallel import vocab_parallel as vp
     V = w.shape[0]
-    per = V // world
-    wl = w[rank * per:(rank + 1) * per].clone().requires_grad_(True)
+    per = -(-vocab // world)  # ceil: the last shard carries zero padding rows past the vocabulary
+    wl = torch.zeros(per, w.shape[1])
+    lo, hi = rank * per, min(vocab, (rank + 1) * per)
+    wl[:max(0, hi - lo)] = w[lo:hi]
+    wl.requires_grad_(True)
+    calls = {"nt": 0}
+    orig_nt = vp.mm_nt
+
+    def counting_nt(*a, **k):
+        calls["nt"] += 1
+        return orig_nt(*a, **k)
+    vp.mm_nt = counting_nt
+    vp.LOGPS_KEEP_BYTES[0] = (1 << 40) if keep else 0
     hh = h.clone().requires_grad_(True)
-    loss = vocab_parallel_cross_entropy(hh, wl, labels, rank * per, dist.group.WORLD)
+    loss = vp.vocab_parallel_cross_entropy(hh, wl, labels, lo, dist.group.WORLD, chunk_size=chunk, vocab_size=vocab)
     loss.backward()
+    ce_nt = calls["nt"]
+    calls["nt"] = 0
     hh2 = h.clone().requires_grad_(True)
-    lp = vocab_parallel_token_logps(hh2, wl, labels, rank * per, dist.group.WORLD)
-    return {"loss": loss.item(), "dh": hh.grad, "dw": wl.grad, "lp": lp.detach()}
+    wl2 = wl.detach().clone().requires_grad_(True)
+    lp = vp.vocab_parallel_token_logps(hh2, wl2, labels, lo, dist.group.WORLD, chunk_size=chunk, vocab_size=vocab)
+    (lp * torch.linspace(0.5, 1.5, lp.numel())).sum().backward()
+    return {"loss": loss.item(), "dh": hh.grad, "dw": wl.grad[:max(0, hi - lo)], "lp": lp.detach(),
+            "dh2": hh2.grad, "dw2": wl2.grad[:max(0, hi - lo)], "ce_nt": ce_nt, "lp_nt": calls["nt"]}
 
 
-def test_vocab_parallel_losses():
+@pytest.mark.parametrize("world,chunk,vocab,keep", [(2, 8192, 64, True), (2, 6, 64, False), (4, 7, 62, True),
+                                                     (4, 5, 61, False)])
+def test_vocab_parallel_losses(world, chunk, vocab, keep):
+    """The single-pass vocab-parallel CE (one lm_head GEMM per chunk in the forward, one small all-gather
+    per chunk) and the token log-probs (logits kept or recomputed) equal the full-vocabulary losses and
+    gradients, with several chunks and a vocabulary that does not divide by tp."""
     torch.manual_seed(0)
-    h = torch.randn(20, 16)
-    w = torch.randn(64, 16)
-    labels = torch.randint(0, 64, (20,))
+    N = 20
+    h = torch.randn(N, 16)
+    w = torch.randn(vocab, 16)
+    labels = torch.randint(0, vocab, (N,))
     labels[::4] = -100
-    out = run_gloo(_vp_worker, 2, (h, w, labels))
+    out = run_gloo(_vp_worker, world, (h, w, labels, chunk, vocab, keep))
     hr, wr = h.clone().requires_grad_(True), w.clone().requires_grad_(True)
     ref = torch.nn.functional.cross_entropy(hr @ wr.t(), labels, ignore_index=-100)
     ref.backward()
     from llm_training_amd.ops.reference import token_logps
-    lp_ref = token_logps(h @ w.t(), labels)
-    for r in (0, 1):
+    hr2, wr2 = h.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    lp_ref = token_logps(hr2 @ wr2.t(), labels)
+    (lp_ref * torch.linspace(0.5, 1.5, lp_ref.numel())).sum().backward()
+    n_chunks = -(-N // min(chunk, N))
+    for r in range(world):
         assert abs(out[r]["loss"] - ref.item()) < 1e-5
-        assert torch.allclose(out[r]["lp"], lp_ref, atol=1e-5)
-    dh = out[0]["dh"] + out[1]["dh"]  # partials: summed by the sequence gather's backward in the model
+        assert torch.allclose(out[r]["lp"], lp_ref.detach(), atol=1e-5)
+        assert out[r]["ce_nt"] == n_chunks  # logits computed once per chunk: no recompute pass
+        assert out[r]["lp_nt"] == (n_chunks if keep else 2 * n_chunks)
+    dh = sum(out[r]["dh"] for r in range(world))  # partials: summed by the sequence gather's backward
     assert torch.allclose(dh, hr.grad, atol=1e-5)
-    assert torch.allclose(torch.cat([out[0]["dw"], out[1]["dw"]]), wr.grad, atol=1e-5)
+    assert torch.allclose(torch.cat([out[r]["dw"] for r in range(world)]), wr.grad, atol=1e-5)
+    assert torch.allclose(sum(out[r]["dh2"] for r in range(world)), hr2.grad, atol=1e-5)
+    assert torch.allclose(torch.cat([out[r]["dw2"] for r in range(world)]), wr2.grad, atol=1e-5)
 
 
 def _ckpt_worker(rank, world, tp, stage, path, mode, offload=False):
@@ -494,3 +523,78 @@ def test_dpo_reference_model_zero3_sharded_matches_single_process():
     avg = [(a + b) / 2 for a, b in zip(out[0]["losses"], out[1]["losses"])]
     for a, b in zip(avg, ref["losses"]):
         assert abs(a - b) < 1e-5
+
+
+def _failed_background_write(rank, world, tmp):
+    """ModelCheckpoint.finalize with a background shard write that failed on rank 1 only: every rank
+    raises (rank 1 its own error, rank 0 'failed on another rank') instead of rank 0 waiting in a barrier."""
+    from llm_training_amd.ckpt import checkpoint as ck
+    from llm_training_amd.runtime.callbacks import ModelCheckpoint
+
+    class _T:
+        device = torch.device("cpu")
+        is_global_zero = rank == 0
+    cb = ModelCheckpoint(dirpath=tmp)
+    cb._pending = os.path.join(tmp, "x.ckpt")
+    if rank == 1:
+        ck._errors.append(OSError("disk full"))
+    try:
+        cb.finalize(_T())
+    except RuntimeError as e:
+        return str(e)
+    return "no error"
+
+
+def test_async_checkpoint_failure_fails_every_rank(tmp_path):
+    out = run_gloo(_failed_background_write, 2, (str(tmp_path),), timeout=60)
+    assert "another rank" in out[0]
+    assert "disk full" in out[1]
+
+
+_HF_KW = {"model_type": "llama", "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 2,
+          "hidden_size": 32, "intermediate_size": 64, "vocab_size": 96, "max_position_embeddings": 64}
+
+
+def _hf_model(liger):
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    m = HFCausalLM(HFCausalLMConfig(hf_config=dict(_HF_KW), enable_liger_kernel=liger,
+                                    attn_implementation="eager"))
+    m.init_weights(3)
+    return m
+
+
+def _hf_dp_worker(rank, world, stage, liger, global_batches):
+    from llm_training_amd.parallel.context import ParallelContext
+    pc = ParallelContext.create("auto", 1, "cpu")
+    m = _hf_model(liger)
+    B = global_batches[0].shape[0] // world
+    seen = {"transient": 0, "grads_left": 0}
+
+    def probe(eng):
+        seen["transient"] = sum(u.transient_grad for u in eng.units)
+        seen["grads_left"] += sum(p.grad is not None for p in m.parameters())
+
+    eng, losses = _train(m, pc, stage, [b[rank * B:(rank + 1) * B] for b in global_batches], probe=probe)
+    with eng.full_params_context():
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    return {"params": sd, "losses": losses, **seen}
+
+
+@pytest.mark.parametrize("liger", [False, True])
+def test_hf_model_zero2_gradient_hooks_match_single_process(liger):
+    """A transformers model (HFCausalLM, with and without the fused-kernel patch) on the ZeRO-2 engine:
+    its autograd gradients move into the flat buffers through post-accumulate-grad hooks as they appear
+    (no .grad left after backward), so its decoder layers use the transient gradient ring and per-unit
+    reduction like the native models, and dp2 training equals one process on the full batch."""
+    from llm_training_amd.parallel.context import ParallelContext
+    batches = _batches(96, STEPS, B=4)
+    m = _hf_model(liger)
+    eng, ref_losses = _train(m, ParallelContext.single(), 0, batches)
+    ref = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    out = run_gloo(_hf_dp_worker, 2, (2, liger, batches))
+    for r in range(2):
+        assert out[r]["transient"] == 1 and out[r]["grads_left"] == 0  # layer 0 (the last unit keeps its buffer)
+        for k, v in ref.items():
+            assert torch.allclose(out[r]["params"][k], v, atol=5e-5, rtol=1e-4), (r, k)
+    avg = [(a + b) / 2 for a, b in zip(out[0]["losses"], out[1]["losses"])]
+    assert max(abs(a - b) for a, b in zip(avg, ref_losses)) < 1e-5

@@ -357,6 +357,40 @@ def test_flash_attention_d128_segments_gqa():
     _attn_case(B, S, 8, 1, 128, seg=seg)
 
 
+_DKDV_CASES = [
+    dict(B=2, S=300, Hq=4, Hkv=4, D=64),
+    dict(B=2, S=300, Hq=8, Hkv=2, D=96),
+    dict(B=2, S=300, Hq=8, Hkv=2, D=128),
+    dict(B=1, S=200, Hq=4, Hkv=2, D=128, causal=False),
+    dict(B=1, S=512, Hq=4, Hkv=4, D=96, window=100),
+    dict(B=2, S=1100, Hq=8, Hkv=2, D=128, window=100),
+    dict(B=2, S=1100, Hq=8, Hkv=2, D=128, causal=False),
+]
+
+
+@pytest.mark.parametrize("variant", ["5"])
+@pytest.mark.parametrize("case", range(len(_DKDV_CASES) + 2))
+def test_flash_attention_dkdv_variant(monkeypatch, variant, case):
+    """The dK/dV kernel variants selected by LLMT_FA_BWD_VARIANT against the fp32 oracle: causal / not,
+    windows, GQA, D 64 / 96 / 128, several ring wraps, packed segments."""
+    monkeypatch.setenv("LLMT_FA_BWD_VARIANT", variant)
+    if case < len(_DKDV_CASES):
+        _attn_case(**_DKDV_CASES[case])
+        return
+    if case == len(_DKDV_CASES):
+        B, S = 2, 384
+        seg = torch.ones(B, S, dtype=torch.int32, device=DEV)
+        seg[0, 100:250] = 2
+        seg[0, 250:] = 3
+        seg[1, 300:] = 0
+        _attn_case(B, S, 4, 2, 128, seg=seg)
+    else:
+        seg = torch.zeros(1, 777, dtype=torch.int32, device=DEV)
+        seg[0, 200:500] = 1
+        seg[0, 500:] = 2
+        _attn_case(1, 777, 8, 1, 128, seg=seg)
+
+
 def test_rope_attention_fused_matches_reference():
     torch.manual_seed(0)
     S, B, nq, nkv, D = 256, 2, 8, 2, 128

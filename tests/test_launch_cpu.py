@@ -154,3 +154,26 @@ def test_bench_gpus_mismatch_under_torchrun_env_fails():
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "WORLD_SIZE" in (r.stderr + r.stdout)
+
+
+def test_device_list_pins_ranks_to_the_listed_gpus(tmp_path, monkeypatch):
+    """trainer.devices [2, 3] (Lightning: those GPU indices) runs the ranks on GPUs 2 and 3: every child
+    sees exactly the listed GPUs (HIP_VISIBLE_DEVICES), so LOCAL_RANK r is GPU devices[r]; an existing
+    visibility mask is composed with the list."""
+    import json
+
+    from llm_training_amd.launch import launch_for_trainer, visible_devices_env
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LLMT_LAUNCHED", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(k, raising=False)
+    prog = tmp_path / "p.py"
+    prog.write_text("import os, json\n"
+                    f"json.dump(dict(os.environ), open(os.path.join({str(tmp_path)!r}, 'env' + os.environ['RANK']), 'w'))\n")
+    assert launch_for_trainer({"devices": [2, 3]}, [sys.executable, str(prog)]) == 0
+    envs = [json.load(open(tmp_path / f"env{r}")) for r in range(2)]
+    assert [e["HIP_VISIBLE_DEVICES"] for e in envs] == ["2,3", "2,3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1"]
+    assert visible_devices_env([1, 3], {"HIP_VISIBLE_DEVICES": "4,5,6,7"}) == {"HIP_VISIBLE_DEVICES": "5,7"}
+    with pytest.raises(SystemExit):
+        visible_devices_env([0, 0], {})
+    with pytest.raises(SystemExit):
+        visible_devices_env([5], {"HIP_VISIBLE_DEVICES": "0,1"})

@@ -328,8 +328,15 @@ def test_hf_enable_liger_kernel_on_hip(model_type):
         y1.backward(g)
         assert rel(y1, y0) < 1e-2, name
         assert rel(x2.grad, x.grad) < 2e-2, name
-        for (n0, p0), (_, p1) in zip(orig.named_parameters(), patched.named_parameters()):
-            assert rel(p1.grad, p0.grad) < 2e-2, (name, n0)
+        g1 = {}
+        for n1, p1 in patched.named_parameters():
+            if n1 == "gate_up_weight":  # the fused gate / up parameter of the patch, split back
+                i = patched.gate_proj._fused_rows[1]
+                g1["gate_proj.weight"], g1["up_proj.weight"] = p1.grad[:i], p1.grad[i:]
+            else:
+                g1[n1] = p1.grad
+        for n0, p0 in orig.named_parameters():
+            assert rel(g1[n0], p0.grad) < 2e-2, (name, n0)
     ids = torch.randint(0, 1000, (2, 256), device="cuda", generator=torch.Generator("cuda").manual_seed(1))
     from llm_training_amd.lms.clm import CLM
     losses = []
@@ -522,3 +529,33 @@ def test_it_trainer_validation_accumulation_best_checkpoint(tmp_path, arch):
     # step 2 saves before its validation runs (Lightning's order) and is unranked; step 4 is ranked by the
     # step-2 validation loss, which stays visible after the later train rows, and is the one kept
     assert len(kept) == 1 and kept[0].endswith("step=4.ckpt"), kept
+
+
+def test_hf_fused_mlp_no_concat_and_no_leftover_transposed_gradient():
+    """The patched HF MLP of a wide model (I >= 12288, Llama-3-8B-like) runs gate/up as one GEMM on the
+    fused parameter (no cat kernel in forward or backward), takes the SwiGLU backward's transposed
+    gradient for its TN weight gradient, and leaves no transposed buffer behind after backward."""
+    from llm_training_amd.models.hf_causal_lm import apply_fused_kernels
+    from llm_training_amd.ops import fused as F_
+    from transformers import LlamaConfig as HFC
+    from transformers.models.llama.modeling_llama import LlamaMLP
+    mlp = LlamaMLP(HFC(hidden_size=1024, intermediate_size=12288)).to("cuda", torch.bfloat16)
+    ref = LlamaMLP(HFC(hidden_size=1024, intermediate_size=12288)).to("cuda", torch.bfloat16)
+    ref.load_state_dict(mlp.state_dict())
+    assert apply_fused_kernels(mlp)
+    x = torch.randn(4096, 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+        y = mlp(x)
+        y.float().pow(2).mean().backward()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    assert not any("cat" in n.lower() for n in names), [n for n in names if "cat" in n.lower()]
+    assert not F_._DY_T  # consumed by the gate_up weight gradient
+    x2 = x.detach().clone().requires_grad_(True)
+    y2 = ref(x2)
+    y2.float().pow(2).mean().backward()
+    rel = lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
+    assert rel(y, y2) < 1e-2 and rel(x.grad, x2.grad) < 2e-2
+    i = 12288
+    assert rel(mlp.gate_up_weight.grad[:i], ref.gate_proj.weight.grad) < 2e-2
+    assert rel(mlp.gate_up_weight.grad[i:], ref.up_proj.weight.grad) < 2e-2

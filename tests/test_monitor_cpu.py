@@ -258,3 +258,34 @@ def test_sanity_check_and_fractional_val_limit(monkeypatch):
     assert calls == [0, 1] and out == {"Loss/Val": 1.0} and "Loss/Val" not in t2.last_metrics
     t2.validate()
     assert len(calls) == 9 and t2.last_metrics["Loss/Val"] == 1.0
+
+
+def test_step_watchdog_dumps_stacks_and_exits(tmp_path):
+    """StepWatchdog (bench.py's hang guard): a phase that overruns its limit writes the rank, the phase and
+    every thread's stack to stderr and ends the process with exit code 3; re-arming / disarming in time
+    keeps it alive."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prog = ("import time\n"
+            "from llm_training_amd.runtime.monitor import StepWatchdog\n"
+            "wd = StepWatchdog(rank=5, timeout=1.0)\n"
+            "for i in range(3):\n"
+            "    wd.arm(f'step {i}')\n"
+            "    time.sleep(0.3)\n"
+            "wd.disarm()\n"
+            "time.sleep(1.5)\n"
+            "print('alive', flush=True)\n"
+            "def stuck_in_a_collective():\n"
+            "    time.sleep(60)\n"
+            "wd.arm('step 3')\n"
+            "stuck_in_a_collective()\n")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, PYTHONPATH=root))
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert r.stdout.strip() == "alive"
+    assert "[rank 5] watchdog: step 3 exceeded 1 s" in r.stderr
+    assert "stuck_in_a_collective" in r.stderr  # the main thread's stack
+    assert time.time() - t0 < 30

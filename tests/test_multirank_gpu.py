@@ -87,6 +87,35 @@ def test_bench_two_ranks_through_the_launcher(tmp_path):
     out = lines[0]
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["zero_stage"] == 2
     assert out["value"] > 0 and out["config"]["global_batch"] == 2
+    assert out["config"]["force_sharded"] is False
+    # the self-verification block: the process group that ran, the untimed collective probe, and the
+    # compute stream's stalls on the comm / optimizer streams during the timed steps
+    rc = out["rccl"]
+    assert rc["backend"] == "gloo" and rc["world"] == 2 and rc["probe_group"] == 2
+    assert rc["ag_busbw_gbs"] > 0 and rc["rs_busbw_gbs"] > 0
+    assert rc["exposed_comm_ms_per_step"] >= 0 and rc["exposed_optimizer_wait_ms_per_step"] >= 0
+
+
+def test_bench_hung_rank_ends_the_job_with_stacks(tmp_path):
+    """A rank that stops inside step 2 (LLMT_BENCH_HANG) leaves the other blocked in a collective: the
+    per-step watchdog dumps the ranks' stacks and the job exits non-zero within the limit instead of
+    waiting for the driver's time-out."""
+    import time
+    env = dict(os.environ, LLMT_DIST_BACKEND="gloo", LLMT_SHARED_DEVICE="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="4",
+               LLMT_BENCH_HANG="1:2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LLMT_LAUNCHED"):
+        env.pop(k, None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--layers", "2", "--seq", "1024", "--micro-batch", "1", "--step-timeout", "15",
+                        "--probe-mb", "8"],
+                       env=env, capture_output=True, text=True, timeout=150, cwd=str(tmp_path))
+    took = time.time() - t0
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "watchdog: timed step 1 exceeded 15 s" in r.stderr, r.stderr[-4000:]
+    assert "File " in r.stderr and "bench.py" in r.stderr  # the Python stacks
+    assert not any(x.startswith('{"metric"') for x in r.stdout.splitlines())
+    assert took < 120
 
 
 def test_dpo_zero3_sharded_reference_two_ranks_on_one_gpu(tmp_path):

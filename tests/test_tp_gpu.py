@@ -53,7 +53,7 @@ def test_overlapped_tp_linears(group, fn):
     assert _rel(b.grad, br.grad) < 1e-2
 
 
-@pytest.mark.parametrize("head", ["ce", "logps"])
+@pytest.mark.parametrize("head", ["ce", "logps", "logps-recompute"])
 def test_vocab_parallel_heads(group, head):
     torch.manual_seed(0)
     N, H, V = 1024, 256, 5000
@@ -68,7 +68,8 @@ def test_vocab_parallel_heads(group, head):
         torch.nn.functional.cross_entropy(hr @ wr.t(), lab, ignore_index=-100).backward()
         assert abs(out.item() - torch.nn.functional.cross_entropy(hr @ wr.t(), lab).item()) < 2e-2
     else:
-        out, rs = vp._VPLogps.apply(h, w, lab, 0, -100, group, 256, V)
+        keep = 0 if head == "logps-recompute" else 1 << 40  # logits recomputed in backward / kept
+        out, rs = vp._VPLogps.apply(h, w, lab, 0, -100, group, 256, V, keep)
         assert _rel(rs, (hr @ wr.t()).sum(-1)) < 1e-2  # logit row sums (ORPO metrics)
         gg = torch.randn_like(out)
         (out * gg).sum().backward()
