@@ -1356,7 +1356,7 @@ __device__ __forceinline__ void mfma_vv(f32v16& c, const bfv8& x, const bfv8& y)
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(x), "a"(y));
 }
 
-template <int D>
+template <int D, int PAD = 0>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const float* ld) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
@@ -1388,6 +1388,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
   }
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
+  // move K / V into the accumulator file here, with the VALU-write -> MFMA-read wait states behind them
+  // (the asm MFMAs that read them are invisible to the hazard recognizer)
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+a"(kf[kk]), "+a"(vf[kk]));
+  asm volatile("s_nop 7");
   f32v16 dkt[NDT], dvt[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
@@ -1516,13 +1521,20 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
         }
         if (kk == 0) {
           mfma_v0(sc, qf[0], kf[0]);
+          if constexpr (PAD) asm volatile("s_nop 7\n\ts_nop 7");
           mfma_v0(dc, df[0], vf[0]);
         } else {
           mfma_vv(sc, qf[kk], kf[kk]);
+          if constexpr (PAD) asm volatile("s_nop 7\n\ts_nop 7");
           mfma_vv(dc, df[kk], vf[kk]);
         }
+        if constexpr (PAD) asm volatile("s_nop 7\n\ts_nop 7");
         __builtin_amdgcn_sched_barrier(0);
       }
+      // hipcc's hazard recognizer does not see the asm MFMAs: the XDL-write -> VALU read / write wait states
+      // (8-pass 32x32x16: 11, +1 on gfx950) before the mask / softmax touch the scores, with margin
+      asm volatile("s_nop 7\n\ts_nop 7");
+      __builtin_amdgcn_sched_barrier(0);
     };
     // masked elements (diagonal / window / packed tiles only) get S = -inf, so P = exp2(-inf) = 0 (the row
     // constant is never +inf: rows past S or without keys carry -inf)
@@ -2602,6 +2614,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     const int variant = dkdv_variant();
     if (variant == 5)
       fa_bwd_dkdv5_kernel<128><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 6)  // hazard-padding probe
+      fa_bwd_dkdv5_kernel<128, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 3)
       fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 4)

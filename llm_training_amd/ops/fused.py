@@ -243,7 +243,10 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
         def nn():  # dy^T materialised
             lib().gemm_lt(x, transpose(dy), o2, False, False, K, N, M, _ld(x), M, K, accumulate, sk)
 
-        variants = {"nt": nt, "tt": tt, "nn": nn}
+        def tn():  # both transposed: token-contiguous operands (the layout hipBLASLt runs fastest)
+            lib().gemm_lt(transpose(x), transpose(dy), o2, True, False, K, N, M, M, M, K, accumulate, sk)
+
+        variants = {"nt": nt, "tt": tt, "nn": nn, "tn": tn}
         if N * K <= _SPLITK_MAX_OUT and M % 256 == 0:
             # split-K along the token (contraction) dimension into 2 or 4 slices, run as one strided-batch
             # GEMM into fp32 slabs + one reduction pass: 2-4x the output tiles for outputs that fill the
@@ -260,6 +263,7 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
                 variants[f"nt{ns}"] = _split(x, dy, False, True, _ld(x), _ld(dy), ns)
                 variants[f"tt{ns}"] = _split(lambda: transpose(x), dy, True, True, M, _ld(dy), ns)
                 variants[f"nn{ns}"] = _split(x, lambda: transpose(dy), False, False, _ld(x), M, ns)
+                variants[f"tn{ns}"] = _split(lambda: transpose(x), lambda: transpose(dy), True, False, M, M, ns)
         if _OWN_WGRAD and M % 32 == 0 and N % 4 == 0:
             # the hand-written ping-pong GEMM (csrc/gemm.hip) reads both token-major operands directly
             # (transposed LDS reads, no materialised transposes); split into 2 / 4 contraction slices for

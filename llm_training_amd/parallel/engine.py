@@ -893,8 +893,11 @@ class DataParallelEngine:
                 del g32
                 pout.copy_(u.master)
             elif self.native:
-                lib().adamw_(u.master, u.exp_avg, u.exp_avg_sq, g, pout, lr, b1, b2, self.eps,
+                bf = pout.dtype == torch.bfloat16  # the kernel writes a bf16 copy; fp32 params copy the master
+                lib().adamw_(u.master, u.exp_avg, u.exp_avg_sq, g, pout if bf else None, lr, b1, b2, self.eps,
                              self.weight_decay, self.step_count, self._gscale)
+                if not bf:
+                    pout.copy_(u.master)
             else:
                 _adamw_ref(u.master, u.exp_avg, u.exp_avg_sq, g.float() * self._gscale, lr, b1, b2, self.eps,
                            self.weight_decay, self.step_count)

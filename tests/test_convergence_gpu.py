@@ -25,6 +25,7 @@ DEV = torch.device("cuda", 0)
 V, S, B = 4096, 512, 4
 STEPS = 300
 LR = 2e-3
+DPO_LR = 1e-4
 
 
 def cfg():
@@ -218,7 +219,7 @@ def train_dpo(dtype, batches, init):
     ref.eval()
     lm = DPO({"model": None, "beta": 0.1})
     lm.model, lm.ref_model = m, ref
-    eng = DataParallelEngine(m, pc, 0, lr=5e-4, weight_decay=0.0)
+    eng = DataParallelEngine(m, pc, 0, lr=DPO_LR, weight_decay=0.0)
     lm.train()
     losses = []
     for b in batches:
@@ -230,7 +231,7 @@ def train_dpo(dtype, batches, init):
         loss.backward()
         eng.finish_backward()
         eng.clip_and_scale(1.0)
-        eng.step(5e-4)
+        eng.step(DPO_LR)
         losses.append(loss.detach().float())
     return torch.stack(losses).cpu()
 
@@ -241,6 +242,8 @@ def test_dpo_bf16_hip_trains_like_the_fp32_reference():
     batches = dpo_batches(150)
     hip = train_dpo(torch.bfloat16, batches, init)
     ref = train_dpo(torch.float32, batches, init)
+    print("dpo hip", [round(x, 4) for x in hip.tolist()])
+    print("dpo ref", [round(x, 4) for x in ref.tolist()])
     assert abs(hip[0].item() - math.log(2)) < 1e-2  # policy == reference at step 0
     assert hip[-30:].mean() <= 0.5 * math.log(2), hip[-30:].mean()  # it learned the preference
     assert abs(hip[-30:].mean() - ref[-30:].mean()) < 0.02 * math.log(2) + 0.02 * ref[-30:].mean(), \
