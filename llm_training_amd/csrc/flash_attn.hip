@@ -2397,7 +2397,9 @@ static int dkdv_variant() {
   const char* e = getenv("LLMT_FA_BWD_VARIANT");
   // 4 = 3 with the widened dK / dV store tail: B32 S1024 1.496 -> 1.476 ms, B64 S512 1.058 -> 1.029 ms,
   // S8192 unchanged, bitwise-equal gradients (profiles/r3_attention_wide_store_ab.jsonl)
-  return e ? atoi(e) : 4;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
+  // 5 = the software-pipelined loop (fa_bwd_dkdv5_kernel): B4 S8192 Hq32 Hkv8 backward 8.150 -> 8.017 ms in
+  // one process, bitwise-equal gradients on every checked shape (benchmarks/attn_variant_check.py)
+  return e ? atoi(e) : 5;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
 }
 
 static void set_dropout(AttnArgs& a, float p, uint32_t seed) {

@@ -368,7 +368,7 @@ _DKDV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", ["5"])
+@pytest.mark.parametrize("variant", ["4", "5"])
 @pytest.mark.parametrize("case", range(len(_DKDV_CASES) + 2))
 def test_flash_attention_dkdv_variant(monkeypatch, variant, case):
     """The dK/dV kernel variants selected by LLMT_FA_BWD_VARIANT against the fp32 oracle: causal / not,
