@@ -170,6 +170,9 @@ def main():
     ap.add_argument("--zero-stage", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--attn", default="flash", choices=["flash", "sdpa", "eager"])
+    ap.add_argument("--impl", default="native", choices=["native", "hf"],
+                    help="pt / pt-packed: the native Llama, or transformers' LlamaForCausalLM through HFCausalLM "
+                         "(HIP attention, fused RMSNorm / SwiGLU patch, fused loss head)")
     ap.add_argument("--ckpt", action="store_true", help="full activation checkpointing")
     ap.add_argument("--ckpt-keep-attn", action="store_true",
                     help="with --ckpt: keep the flash-attention outputs (recompute_granularity full_keep_attention)")
@@ -247,7 +250,17 @@ def main():
     else:
         from llm_training_amd.models.llama import Llama as Model
         from llm_training_amd.models.llama import LlamaConfig as MCfg
-    mcfg = MCfg(**cfg, **common)
+    if args.impl == "hf":
+        if phi3 or args.workload in ("dpo", "orpo") or args.tp > 1:
+            raise SystemExit("--impl hf: the pt / pt-packed workloads without tensor parallelism")
+        from llm_training_amd.models.hf_causal_lm import HFCausalLM as Model
+        from llm_training_amd.models.hf_causal_lm import HFCausalLMConfig
+        hf = {k: v for k, v in cfg.items()}
+        hf.update(model_type="llama", torch_dtype="bfloat16")
+        mcfg = HFCausalLMConfig(hf_config=hf, attn_implementation=args.attn, enable_liger_kernel=True,
+                                enable_gradient_checkpointing=args.ckpt, loss_chunk_size=args.loss_chunk)
+    else:
+        mcfg = MCfg(**cfg, **common)
     torch.manual_seed(1234)
     model = Model(mcfg, pc, dtype=torch.bfloat16, device=device)
     model.init_weights(seed=1234)
@@ -403,6 +416,8 @@ def main():
                    "grad_clip": 1.0, "gemm_tuning": gemm_mode}
         if args.workload != "pt":
             cfg_out["workload"] = args.workload
+        if args.impl != "native":
+            cfg_out["impl"] = "transformers LlamaForCausalLM (HFCausalLM, fused-kernel patch)"
         if args.workload in ("pt-packed", "it"):
             cfg_out.update(packed_docs_per_row=args.packed_docs, attn_work_vs_causal=round(frac, 4))
         if phi3:

@@ -1,6 +1,6 @@
 """In-process A/B of flash-attention forward variants (LLMT_FA_FWD_VARIANT is read on every launch):
 alternating windows of each variant on the same operands.
-    python benchmarks/ab_attention_fwd.py [B S Hq Hkv D] [variants, comma-separated]"""
+    python benchmarks/ab_attention_fwd.py [B S Hq Hkv D] [variants, comma-separated] [env var]"""
 import json
 import os
 import sys
@@ -12,6 +12,7 @@ from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D = (int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (4, 8192, 32, 8, 128)))
 variants = (sys.argv[6] if len(sys.argv) > 6 else "2,3").split(",")
+ENV = sys.argv[7] if len(sys.argv) > 7 else "LLMT_FA_FWD_VARIANT"  # or e.g. LLMT_FA_BMAJOR
 q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16)
 k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
 v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
@@ -19,7 +20,7 @@ outs, times = {}, {x: [] for x in variants}
 with torch.no_grad():
     for rnd in range(5):
         for var in variants:
-            os.environ["LLMT_FA_FWD_VARIANT"] = var
+            os.environ[ENV] = var
             for _ in range(2):
                 o = F_.flash_attention(q, k, v, causal=True)
             torch.cuda.synchronize()
@@ -31,7 +32,7 @@ with torch.no_grad():
             torch.cuda.synchronize()
             times[var].append(a.elapsed_time(b) / 10)
             outs[var] = o
-res = {"shape": [B, S, Hq, Hkv, D]}
+res = {"shape": [B, S, Hq, Hkv, D], "env": ENV}
 for var in variants:
     ms = sorted(times[var])[len(times[var]) // 2]
     res[f"v{var}_ms"] = round(ms, 4)

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--docs", default="1,2,4,8,16,32")
     ap.add_argument("--equal", action="store_true")
+    ap.add_argument("--ab", default="", help="in-process A/B of a per-launch env knob, e.g. LLMT_FA_RANGE_MASK:0,1")
     a = ap.parse_args()
     dev = "cuda"
     B, S = a.B, a.S
@@ -92,6 +93,20 @@ def main():
 
         def fwd():
             return F_.flash_attention(q, k, v, causal=True, segment_ids=seg, seg_info=info)
+
+        if a.ab:
+            name, vals = a.ab.split(":")
+            vals = vals.split(",")
+            tf_ab, tb_ab = {x: [] for x in vals}, {x: [] for x in vals}
+            for _ in range(3):
+                for x in vals:
+                    os.environ[name] = x
+                    tf_ab[x].append(timeit(fwd))
+                    tb_ab[x].append(timeit(lambda: fwd().backward(do)))
+            os.environ.pop(name)
+            print(json.dumps({"docs": n, "B": B, "S": S, "D": a.D, "Hq": a.Hq, "Hkv": a.Hkv, "ab": name,
+                              **{f"fwd_ms_{x}": round(min(tf_ab[x]), 4) for x in vals},
+                              **{f"fwd_bwd_ms_{x}": round(min(tb_ab[x]), 4) for x in vals}}), flush=True)
 
         def fb():
             fwd().backward(do)

@@ -190,6 +190,12 @@ struct AttnArgs {
   // backward regenerates the same mask from the same counters. drop_thresh = 0: no dropout.
   uint32_t drop_seed, drop_thresh;
   float drop_scale;
+  // dense rows: 1 = a batch row's blocks back to back in the 1-D grids (block_of), so the workgroups
+  // co-resident on an XCD share one row's K / V (or Q / dO) stream in L2; 0 = batch-interleaved
+  int bmajor;
+  // 1: masks from per-row index ranges (the run of a packed row, causal, window, sequence end) instead of
+  // per-element segment-id compares; needs run bounds (rs / re) whenever `seg` is set
+  int rmask;
 };
 
 __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q, uint32_t k) {
@@ -224,6 +230,50 @@ __device__ __forceinline__ RunInfo block_run(const AttnArgs& a, int b, int lo, i
   }
   return ri;
 }
+// Range masks (AttnArgs::rmask). Every mask of a row is an index interval: the keys of query row q are
+// [max(rs[q], q - window), causal ? q : re[q]] within [0, S) (documents are contiguous runs: the
+// reference's varlen cu_seqlens), and the queries of key row k are [causal ? k : rs[k], min(re[k], k + window)].
+// A tile then tests element o (a compile-time offset from the lane's first index i0) with one unsigned
+// compare, (i0 - lo + o) <= hi - lo, instead of up to five compares and a segment-id load per element.
+struct IdxRange {
+  unsigned base, span;  // element o is inside iff base + o <= span (unsigned)
+};
+__device__ __forceinline__ IdxRange idx_range(int lo, int hi, int i0) {
+  if (hi < lo) return {1u, 0u};  // empty: base + o >= 1 > span for every o in [0, 2^31)
+  return {(unsigned)(i0 - lo), (unsigned)(hi - lo)};
+}
+__device__ __forceinline__ bool in_range(const IdxRange& r, int o) { return r.base + (unsigned)o <= r.span; }
+// [lo, hi] of the keys of query row q (q >= S: empty)
+__device__ __forceinline__ void key_interval(const AttnArgs& a, int b, int q, int& lo, int& hi) {
+  lo = 0;
+  hi = a.S - 1;
+  if (q >= a.S) {
+    hi = -1;
+    return;
+  }
+  if (a.rs) {
+    lo = a.rs[(int64_t)b * a.S + q];
+    hi = a.re[(int64_t)b * a.S + q];
+  }
+  if (a.causal) hi = min(hi, q);
+  if (a.window >= 0) lo = max(lo, q - a.window);
+}
+// [lo, hi] of the queries of key row k (k >= S: empty)
+__device__ __forceinline__ void query_interval(const AttnArgs& a, int b, int k, int& lo, int& hi) {
+  lo = 0;
+  hi = a.S - 1;
+  if (k >= a.S) {
+    hi = -1;
+    return;
+  }
+  if (a.rs) {
+    lo = a.rs[(int64_t)b * a.S + k];
+    hi = a.re[(int64_t)b * a.S + k];
+  }
+  if (a.causal) lo = max(lo, k);
+  if (a.window >= 0) hi = min(hi, k + a.window);
+}
+
 // does the segment compare matter for the tile [t0, t1] against a block described by ri?
 __device__ __forceinline__ bool seg_mask(const AttnArgs& a, const RunInfo& ri, int t0, int t1) {
   return a.seg && !(ri.uni && t0 >= ri.rs && t1 <= ri.re);
@@ -238,6 +288,10 @@ __device__ __forceinline__ void block_of(const AttnArgs& a, int i, int nblk, boo
     const int bm = ord[i];
     b = bm / nblk;
     blk = bm - b * nblk;
+  } else if (a.bmajor) {
+    b = i / nblk;
+    blk = i - b * nblk;
+    if (query) blk = nblk - 1 - blk;
   } else {
     b = i % a.B;
     blk = query ? nblk - 1 - i / a.B : i / a.B;
@@ -1356,7 +1410,7 @@ __device__ __forceinline__ void mfma_vv(f32v16& c, const bfv8& x, const bfv8& y)
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(x), "a"(y));
 }
 
-template <int D, int PAD = 0>
+template <int D, bool OM = false>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const float* ld) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
@@ -1377,7 +1431,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
   const int nT = (S + 31) / 32;
   const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
   const bf16* vp = a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh;
-  const int sk = (a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;
+  const int sk = (OM && a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;  // OM: see fa_fwd3_kernel
+  int qlo = 0, qhi = -1;
+  if (!OM) query_interval(a, b, kr, qlo, qhi);
   const float sl2 = a.scale * kLog2e;
 
   bfv8 kf[NKK], vf[NKK];
@@ -1429,10 +1485,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
     const int step_q = BM * a.q_ss * 2, step_d = BM * a.d_ss * 2;
     Rsrc qrs = make_rsrc4(qh0, nrec_q), drs = make_rsrc4(dh0, nrec_d), lrs = make_rsrc4(lh0, nrec_l);
     int iss_g = 0, iss_q = 0, iss_n = 0, toff_q = 0, toff_d = 0, toff_l = 0;
-    auto issue = [&](const char* slot) {
-      const char* q0 = slot + 8 * wid * 256;
-      dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, slot + 2 * IMG + (wid & 1) * 256,
-                dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
+    auto advance = [&]() {  // offsets (and head descriptors) of the next tile in load order
       if (++iss_n < T) {
         toff_q += step_q;
         toff_d += step_d;
@@ -1446,6 +1499,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
           lrs = make_rsrc4(lh0 + (int64_t)iss_g * nT * kLdTile, nrec_l);
         }
       }
+    };
+    auto issue = [&](const char* slot) {
+      const char* q0 = slot + 8 * wid * 256;
+      dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, slot + 2 * IMG + (wid & 1) * 256,
+                dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
+      advance();
     };
     int cur_q = 0;
     const bool seg_or_window = a.seg != nullptr || a.window >= 0;
@@ -1521,14 +1580,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
         }
         if (kk == 0) {
           mfma_v0(sc, qf[0], kf[0]);
-          if constexpr (PAD) asm volatile("s_nop 7\n\ts_nop 7");
           mfma_v0(dc, df[0], vf[0]);
         } else {
           mfma_vv(sc, qf[kk], kf[kk]);
-          if constexpr (PAD) asm volatile("s_nop 7\n\ts_nop 7");
           mfma_vv(dc, df[kk], vf[kk]);
         }
-        if constexpr (PAD) asm volatile("s_nop 7\n\ts_nop 7");
         __builtin_amdgcn_sched_barrier(0);
       }
       // hipcc's hazard recognizer does not see the asm MFMAs: the XDL-write -> VALU read / write wait states
@@ -1539,6 +1595,13 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
     // masked elements (diagonal / window / packed tiles only) get S = -inf, so P = exp2(-inf) = 0 (the row
     // constant is never +inf: rows past S or without keys carry -inf)
     auto apply_mask = [&](const char* cs, const TileMask& m, f32v16& sc) {
+      if constexpr (!OM) {
+        const IdxRange rg = idx_range(qlo, qhi, m.q0 + 4 * hh);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (!in_range(rg, 8 * (i >> 2) + (i & 3))) sc[i] = -INFINITY;
+        return;
+      }
       const int* Sg = reinterpret_cast<const int*>(cs + 2 * IMG) + 64;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -1716,7 +1779,7 @@ __device__ __forceinline__ void kv_tile_dma(const char* slot, int n0, int wid, i
 // NW = 8: two query heads of one kv group per workgroup, side by side (waves 0-3 head h, waves 4-7 head
 // h + 1, 32 queries each): every K/V tile of the LDS-DMA ring then serves 256 query rows instead of 128,
 // crossing L2 -> LDS half as often, and each wave issues half the DMA pieces (2 K + 2 V rows groups).
-template <int D, int RS = 0, int WS = 0, int NW = 4>
+template <int D, int RS = 0, int WS = 0, int NW = 4, bool OM = false>
 __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;  // k-steps of a D-deep product, 32-wide output tiles
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
@@ -1738,13 +1801,16 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   const int qs = mb * 128, qw = qs + wq * 32, qrow = qw + r;
   const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
   const float sl2 = a.scale * kLog2e;
-  int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
+  // OM: the per-element segment-id compares (A/B reference; rows without run bounds); else range masks
+  int sq = (OM && a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
+  int klo = 0, khi = -1;
+  if (!OM) key_interval(a, b, qrow, klo, khi);
 
   bfv8 qf[NKK];
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
   // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
-  asm volatile("" : "+v"(sq));
+  asm volatile("" : "+v"(sq), "+v"(klo), "+v"(khi));
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
   f32v16 ot[NDT];
@@ -1821,7 +1887,16 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
       const bool m_window = a.window >= 0 && (n0 < qw + 31 - a.window);
       const bool m_end = n0 + BN > S;
       const bool m_seg = seg_mask(a, qr, n0, n0 + BN - 1);
-      if (m_causal || m_window || m_end || m_seg || qw + 31 >= S) {
+      if ((m_causal || m_window || m_end || m_seg || qw + 31 >= S) && !OM) {
+        const IdxRange rg = idx_range(klo, khi, n0 + 4 * hh);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (!in_range(rg, 32 * tt + 8 * c + j)) st[tt][4 * c + j] = -INFINITY;
+      } else if (OM && (m_causal || m_window || m_end || m_seg || qw + 31 >= S)) {
         const int* Ss = reinterpret_cast<const int*>(slot + 2 * IMG);
         const int lim = qrow - n0 - 4 * hh, lo = qrow - a.window - n0 - 4 * hh, hi = S - 1 - n0 - 4 * hh;
 #pragma unroll
@@ -1848,7 +1923,12 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
         mx1 = vmax3(mx1, st[1][i], st[1][i + 1]);
       }
       float smax = vmax3(mx0, st[0][15], vmax3(mx1, st[1][15], mx1));
-      smax = fmaxf(smax, __shfl_xor(smax, 32, 64)) * sl2;
+      if constexpr (RS == 2) {  // the two half-waves' maxima through one permlane32 swap (no LDS round trip)
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(smax), __float_as_uint(smax), false, false);
+        smax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
+      } else {
+        smax = fmaxf(smax, __shfl_xor(smax, 32, 64)) * sl2;
+      }
       // deferred rescale: keep the running max unless some row grew by more than kThr
       if (__any(smax > m + kThr)) {
         const float mnew = fmaxf(m, smax);
@@ -1866,6 +1946,19 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {
+          if constexpr (RS == 2) {
+            // exp pair + row-sum adds in one asm block: each add sits one instruction behind the exp it reads
+            // (the trans-use wait state, by placement instead of an s_nop), and hipcc cannot pair the adds
+            // into v_pk_add_f32 (an anti-lever beside MFMAs, cdna guide cycle constants)
+            const float x0 = fmaf(st[tt][i], sl2, nm), x1 = fmaf(st[tt][i + 1], sl2, nm);
+            float e0, e1;
+            asm("v_exp_f32 %0, %4\n\tv_exp_f32 %1, %5\n\tv_add_f32 %2, %2, %0\n\tv_add_f32 %3, %3, %1"
+                : "=&v"(e0), "=&v"(e1), "+v"(rs0), "+v"(rs1)
+                : "v"(x0), "v"(x1));
+            st[tt][i] = e0;
+            st[tt][i + 1] = e1;
+            continue;
+          }
           st[tt][i] = fexp2(fmaf(st[tt][i], sl2, nm));
           st[tt][i + 1] = fexp2(fmaf(st[tt][i + 1], sl2, nm));
           if constexpr (RS == 0) {
@@ -2193,7 +2286,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3c_kernel(AttnArgs a) {
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
 // dQ = scale * sum; the row constants come straight from lse / delta (delta written by the prep kernel).
 // NW = 8: two query heads of one kv group per workgroup sharing the K/V ring (as fa_fwd3_kernel)
-template <int D, bool IL = true, bool WS = false, int NW = 4>
+template <int D, bool IL = true, bool WS = false, int NW = 4, bool OM = false>
 __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
@@ -2219,7 +2312,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   const int64_t lrow = ((int64_t)b * a.Hq + h) * S + min(qrow, S - 1);
   float lse2 = qrow < S ? a.lse[lrow] * kLog2e : INFINITY;
   float dlt = qrow < S ? a.delta[lrow] : 0.f;
-  int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
+  int sq = (OM && a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;  // OM: see fa_fwd3_kernel
+  int klo = 0, khi = -1;
+  if (!OM) key_interval(a, b, qrow, klo, khi);
 
   bfv8 qf[NKK], df[NKK];
 #pragma unroll
@@ -2228,7 +2323,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
     df[kk] = gload8(dop + (int64_t)min(qrow, S - 1) * a.d_ss + kk * 16 + hh * 8, qrow < S);
   }
   // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
-  asm volatile("" : "+v"(sq), "+v"(lse2), "+v"(dlt));
+  asm volatile("" : "+v"(sq), "+v"(lse2), "+v"(dlt), "+v"(klo), "+v"(khi));
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(df[kk]));
   f32v16 dqt[NDT];
@@ -2314,7 +2409,14 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
             fr[4 * s2 + dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
           }
         __builtin_amdgcn_sched_barrier(0);
-        if (need_mask) {
+        if (need_mask && !OM) {
+          const IdxRange rg = idx_range(klo, khi, n0 + 32 * tt + 4 * hh);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float pr = in_range(rg, 8 * (i >> 2) + (i & 3)) ? fexp2(fmaf(st[i], sl2, -lse2)) : 0.f;
+            st[i] = pr * (dpt[i] - dlt);
+          }
+        } else if (OM && need_mask) {
           const int* Ss = reinterpret_cast<const int*>(slot + 2 * IMG);
           const int k0 = n0 + 32 * tt + 4 * hh;
 #pragma unroll
@@ -2402,6 +2504,18 @@ static int dkdv_variant() {
   return e ? atoi(e) : 5;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
 }
 
+// range masks (AttnArgs::rmask; LLMT_FA_RANGE_MASK=0: per-element compares, the A/B reference)
+static int range_masks() {
+  const char* e = getenv("LLMT_FA_RANGE_MASK");
+  return e ? atoi(e) : 1;
+}
+
+// block order of the 1-D attention grids (AttnArgs::bmajor), read per launch for A/B (LLMT_FA_BMAJOR)
+static int bmajor_order() {
+  const char* e = getenv("LLMT_FA_BMAJOR");
+  return e ? atoi(e) : 0;
+}
+
 static void set_dropout(AttnArgs& a, float p, uint32_t seed) {
   if (p <= 0.f) {
     a.drop_thresh = 0;
@@ -2454,6 +2568,8 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   a.v_sb = v_sb; a.v_ss = v_ss; a.v_sh = v_sh; a.o_sb = o_sb; a.o_ss = o_ss; a.o_sh = o_sh;
   a.scale = scale; a.causal = causal; a.window = window;
   set_dropout(a, drop_p, drop_seed);
+  a.bmajor = bmajor_order();
+  a.rmask = range_masks() && (seg == nullptr || a.rs != nullptr);
   dim3 grid((S + 127) / 128, Hq, B);
   // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907 (variant 0), the
   // removed one-wave-per-SIMD ring forward 1.043; 3 = fwd3 with compiler-placed row-sum adds, 2 = with the
@@ -2479,8 +2595,10 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
         fa_fwd3c_kernel<64, 4><<<nb1 / 4, 256, 0, stream>>>(a);
       else if (chain == 2)
         fa_fwd3c_kernel<64, 2><<<nb1 / 2, 256, 0, stream>>>(a);
-      else
+      else if (a.rmask)
         fa_fwd3_kernel<64, 1, 1><<<nb1, 256, 0, stream>>>(a);
+      else
+        fa_fwd3_kernel<64, 1, 1, 4, true><<<nb1, 256, 0, stream>>>(a);
       break;
     case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
       if (a.drop_thresh || variant == 0)
@@ -2489,8 +2607,10 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
         fa_fwd3c_kernel<96, 4><<<nb1 / 4, 256, 0, stream>>>(a);
       else if (chain == 2)
         fa_fwd3c_kernel<96, 2><<<nb1 / 2, 256, 0, stream>>>(a);
-      else
+      else if (a.rmask)
         fa_fwd3_kernel<96, 1, 1><<<nb1, 256, 0, stream>>>(a);
+      else
+        fa_fwd3_kernel<96, 1, 1, 4, true><<<nb1, 256, 0, stream>>>(a);
       break;
     case 128: {
       if (a.drop_thresh)  // dropout lives in the generic kernels
@@ -2505,8 +2625,12 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
         fa_fwd3c_kernel<128, 2><<<nb1 / 2, 256, 0, stream>>>(a);
       else if (grp % 2 == 0 && (variant == 7 || (variant == 4 && pairs_pay(seg, S))))  // GQA head pairs
         fa_fwd3_kernel<128, 1, 1, 8><<<nb1 / 2, 512, 0, stream>>>(a);
-      else if (variant >= 4)
+      else if (variant == 9 && a.rmask)  // permlane row max, asm exp + row-sum pairs
+        fa_fwd3_kernel<128, 2, 1><<<nb1, 256, 0, stream>>>(a);
+      else if (variant >= 4 && a.rmask)
         fa_fwd3_kernel<128, 1, 1><<<nb1, 256, 0, stream>>>(a);
+      else if (variant >= 4)
+        fa_fwd3_kernel<128, 1, 1, 4, true><<<nb1, 256, 0, stream>>>(a);
       else
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
     } break;
@@ -2563,6 +2687,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   a.dv_sb = dv_sb; a.dv_ss = dv_ss; a.dv_sh = dv_sh;
   a.scale = scale; a.causal = causal; a.window = window;
   set_dropout(a, drop_p, drop_seed);
+  a.bmajor = bmajor_order();
+  a.rmask = range_masks() && (seg == nullptr || a.rs != nullptr);
   const bool gqa = Hq != Hkv;
   const int64_t nrows = (int64_t)B * S * Hq;
   dim3 grid((S + 127) / 128, Hq, B);
@@ -2574,9 +2700,14 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     const int64_t nT = (S + 31) / 32;
     if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
       fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
-      fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      if (dkdv_variant() == 5)
+      if (a.rmask)
+        fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else
+        fa_bwd_dq3_kernel<96, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      if (dkdv_variant() == 5 && a.rmask)
         fa_bwd_dkdv5_kernel<96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      else if (dkdv_variant() == 5)
+        fa_bwd_dkdv5_kernel<96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else if (dkdv_variant() >= 3)
         fa_bwd_dkdv128_kernel<3, 96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
@@ -2585,9 +2716,14 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     }
     if (D == 64) {
       fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
-      fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      if (dkdv_variant() == 5)
+      if (a.rmask)
+        fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else
+        fa_bwd_dq3_kernel<64, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      if (dkdv_variant() == 5 && a.rmask)
         fa_bwd_dkdv5_kernel<64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      else if (dkdv_variant() == 5)
+        fa_bwd_dkdv5_kernel<64, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else if (dkdv_variant() >= 3)
         fa_bwd_dkdv128_kernel<3, 64, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
@@ -2610,14 +2746,16 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<128, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (dqv == 1)
         fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else
+      else if (a.rmask)
         fa_bwd_dq3_kernel<128, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else
+        fa_bwd_dq3_kernel<128, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     }
     const int variant = dkdv_variant();
-    if (variant == 5)
+    if (variant == 5 && a.rmask)
       fa_bwd_dkdv5_kernel<128><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 6)  // hazard-padding probe
-      fa_bwd_dkdv5_kernel<128, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 5)
+      fa_bwd_dkdv5_kernel<128, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 3)
       fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 4)

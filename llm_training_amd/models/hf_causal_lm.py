@@ -128,9 +128,14 @@ class HFCausalLM(BaseModel):
         self.uses_hip_attention = impl == HF_ATTN_IMPL
         if dtype is None:
             dtype = config.torch_dtype if isinstance(config.torch_dtype, torch.dtype) else torch.float32
-        self.hf_model = AutoModelForCausalLM.from_config(hf_cfg, torch_dtype=dtype)
-        if device is not None:
-            self.hf_model.to(device)
+        if device is not None and torch.device(device).type == "cuda":
+            # built on the GPU directly (an 8 B model's CPU construction + copy takes minutes)
+            with torch.device(device):
+                self.hf_model = AutoModelForCausalLM.from_config(hf_cfg, torch_dtype=dtype)
+        else:
+            self.hf_model = AutoModelForCausalLM.from_config(hf_cfg, torch_dtype=dtype)
+            if device is not None:
+                self.hf_model.to(device)
         if config.enable_gradient_checkpointing:
             self.hf_model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
         self.fused_modules: dict[str, int] = {}
