@@ -1410,10 +1410,11 @@ __device__ __forceinline__ void mfma_vv(f32v16& c, const bfv8& x, const bfv8& y)
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(x), "a"(y));
 }
 
-template <int D, bool OM = false>
+template <int D, bool OM = false, int NSL = 6>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const float* ld) {
   constexpr int NKK = D / 16, NDT = D / 32;
-  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
+  // NSL ring slots: tiles issued NSL - 2 ahead, each given NSL - 4 iterations to land
+  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = NSL;
   constexpr int NDMA = 5;
   constexpr int NB = 4 * NDT;  // phase-B MFMAs (dV then dK, s2-major)
   using QI = Img<128>;
@@ -2753,7 +2754,11 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<128, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     }
     const int variant = dkdv_variant();
-    if (variant == 5 && a.rmask)
+    // dense rows: an 8-slot Q / dO ring (tiles 6 ahead; B4 S8192 backward 7.605 -> 7.544 ms in one process,
+    // 7 slots 7.572); packed rows keep 6 (their key blocks often visit only a few tiles)
+    if (variant == 5 && a.rmask && !seg)
+      fa_bwd_dkdv5_kernel<128, false, 8><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 5 && a.rmask)
       fa_bwd_dkdv5_kernel<128><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 5)
       fa_bwd_dkdv5_kernel<128, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
