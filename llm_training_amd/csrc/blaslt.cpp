@@ -115,11 +115,12 @@ void set_batch(Desc& d, bool ta, bool tb, int64_t m, int64_t n, int64_t kc, int6
 }
 
 std::string key_of(bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
-                   hipDataType ctype, bool beta, bool streamk, int batch = 1) {
+                   hipDataType ctype, bool beta, bool streamk, int batch = 1, bool bias = false) {
   std::ostringstream o;
   o << (ta ? 't' : 'n') << (tb ? 't' : 'n') << "_" << m << "_" << n << "_" << k << "_ld" << lda << "_" << ldb << "_"
     << ldc << (ctype == HIP_R_32F ? "_f32" : "_bf16") << (beta ? "_acc" : "") << (streamk ? "" : "_nosk");
   if (batch > 1) o << "_b" << batch;
+  if (bias) o << "_bias";
   return o.str();
 }
 
@@ -136,8 +137,12 @@ bool is_streamk(hipblasLtHandle_t h, hipblasLtMatmulAlgo_t& algo) {
 
 // C (m x n, column-major) = op(A) . op(B) (+ C when accumulate); batch > 1: split-K into `batch` fp32 slabs
 // of C (C is then [batch, n, m] fp32 with ldc = m, k divisible by batch)
+// bias (optional, length m, bf16 or fp32): the BIAS epilogue, D = op(A) op(B) + bias broadcast over the n
+// columns — for a linear layer's forward (column-major y^T = W . x^T) the bias of every output feature, added
+// inside the GEMM instead of by a separate pass over y
 void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bool tb, int64_t m, int64_t n,
-                  int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool accumulate, bool streamk, int batch) {
+                  int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool accumulate, bool streamk, int batch,
+                  const c10::optional<at::Tensor>& bias = c10::nullopt) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm_lt: GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_lt: bf16 A/B");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "gemm_lt: C bf16/fp32");
@@ -155,9 +160,22 @@ void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool t
     TORCH_CHECK(ctype == HIP_R_32F && ldc == m && C.numel() >= batch * m * n, "gemm_lt: split-K slabs are fp32 [batch, n, m]");
     set_batch(d, ta, tb, m, n, k / batch, lda, ldb, batch);
   }
+  const bool has_bias = bias.has_value() && bias->defined();
+  if (has_bias) {
+    TORCH_CHECK(batch == 1 && bias->is_cuda() && bias->is_contiguous() && bias->numel() == m &&
+                    (bias->scalar_type() == at::kBFloat16 || bias->scalar_type() == at::kFloat),
+                "gemm_lt: bias must be a contiguous bf16 / fp32 vector of length m");
+    const hipblasLtEpilogue_t ep = HIPBLASLT_EPILOGUE_BIAS;
+    const void* bp = bias->data_ptr();
+    const hipDataType bt = bias->scalar_type() == at::kFloat ? HIP_R_32F : HIP_R_16BF;
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(d.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(d.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(d.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  }
   const float alpha = 1.f, beta = accumulate ? 1.f : 0.f;
   auto ws = at::empty({(int64_t)kWorkspace}, C.options().dtype(at::kByte));
-  const std::string key = key_of(ta, tb, m, n, k, lda, ldb, ldc, ctype, accumulate, streamk, batch);
+  const std::string key = key_of(ta, tb, m, n, k, lda, ldb, ldc, ctype, accumulate, streamk, batch, has_bias) +
+                          (has_bias && bias->scalar_type() == at::kFloat ? "32" : "");
   auto it = s.cache.find(key);
   if (it == s.cache.end()) {
     hipblasLtMatmulPreference_t pref;
@@ -224,6 +242,11 @@ void gemm_lt(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bo
   gemm_lt_impl(A, B, C, ta, tb, m, n, k, lda, ldb, ldc, accumulate, streamk, 1);
 }
 
+void gemm_lt_bias(const at::Tensor& A, const at::Tensor& B, at::Tensor C, const at::Tensor& bias, bool ta, bool tb,
+                  int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc, bool streamk) {
+  gemm_lt_impl(A, B, C, ta, tb, m, n, k, lda, ldb, ldc, false, streamk, 1, bias);
+}
+
 // split-K form: C fp32 [batch, n, m] slabs, no accumulation (the caller reduces them)
 void gemm_lt_splitk(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool ta, bool tb, int64_t m, int64_t n,
                     int64_t k, int64_t lda, int64_t ldb, int64_t batch, bool streamk) {
@@ -271,6 +294,9 @@ TORCH_LIBRARY_FRAGMENT(llmt, m) {
   m.def(
       "gemm_lt_splitk(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, int m, int n, int k, int lda, int ldb, "
       "int batch, bool streamk=True) -> ()");
+  m.def(
+      "gemm_lt_bias(Tensor a, Tensor b, Tensor(a!) c, Tensor bias, bool ta, bool tb, int m, int n, int k, int lda, "
+      "int ldb, int ldc, bool streamk=True) -> ()");
   m.def("gemm_lt_export() -> str", &gemm_lt_export);
   m.def("gemm_lt_import(str text, bool tune_unknown) -> int", &gemm_lt_import);
 }
@@ -278,4 +304,5 @@ TORCH_LIBRARY_FRAGMENT(llmt, m) {
 TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("gemm_lt", &gemm_lt);
   m.impl("gemm_lt_splitk", &gemm_lt_splitk);
+  m.impl("gemm_lt_bias", &gemm_lt_bias);
 }

@@ -152,21 +152,27 @@ def _path(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> str:
     return mode
 
 
-def mm_nt(x2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """x2 [M, K] @ w[N, K]^T -> [M, N] (forward of a linear layer); ``out``: contiguous [M, N] target."""
+def mm_nt(x2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+          bias: torch.Tensor | None = None) -> torch.Tensor:
+    """x2 [M, K] @ w[N, K]^T (+ bias[N]) -> [M, N] (forward of a linear layer); ``out``: contiguous [M, N]
+    target. On the hipBLASLt path the bias is the GEMM's BIAS epilogue (no separate pass over y)."""
     path = _path("fwd", x2.shape[1], w.shape[0], x2, w)
     if out is not None and path != "blas" and not _gemm_operand_ok(out):
         path = "blas"
     if path == "blas":
-        return torch.matmul(x2, w.t()) if out is None else torch.matmul(x2, w.t(), out=out)
+        y = torch.matmul(x2, w.t()) if out is None else torch.matmul(x2, w.t(), out=out)
+        return y if bias is None else y.add_(bias)
     M, K = x2.shape
     N = w.shape[0]
     y = out if out is not None else torch.empty(M, N, device=x2.device, dtype=x2.dtype)
     if path == "lt":  # column-major: y^T (N x M) = w^T (from K x N) . x^T (K x M)
+        if bias is not None and bias.is_contiguous() and bias.dtype in (torch.bfloat16, torch.float32):
+            lib().gemm_lt_bias(w, x2, y, bias, True, False, N, M, K, _ld(w), _ld(x2), N, ALLOW_STREAMK[0])
+            return y
         lib().gemm_lt(w, x2, y, True, False, N, M, K, _ld(w), _ld(x2), N, False, ALLOW_STREAMK[0])
     else:
         lib().gemm_(x2, w, y, False, False, False)
-    return y
+    return y if bias is None else y.add_(bias)
 
 
 def weight_t(w: torch.Tensor, rows: int) -> torch.Tensor | None:
@@ -344,10 +350,8 @@ class _LinearFn(Function):
         ctx.save_for_backward(x)
         ctx.w = w
         ctx.has_bias = b is not None
-        y = mm_nt(x.reshape(-1, x.shape[-1]), w).view(*x.shape[:-1], w.shape[0])
-        if b is not None:
-            y = y + b
-        return y
+        # the bias rides in the GEMM's epilogue on the hipBLASLt path (mm_nt)
+        return mm_nt(x.reshape(-1, x.shape[-1]), w, bias=b).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):

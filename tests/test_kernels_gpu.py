@@ -531,6 +531,41 @@ def test_linear_gemm_paths_grads_into_grad_buffer(monkeypatch, mode):
         assert _rel(x.grad, dy.float() @ w.float()) < 1e-2
 
 
+@pytest.mark.parametrize("bias_dtype", [torch.bfloat16, torch.float32])
+def test_linear_bias_in_the_gemm_epilogue(monkeypatch, bias_dtype):
+    """A biased linear on the hipBLASLt path adds the bias in the GEMM's BIAS epilogue (no elementwise add
+    kernel after it) and matches x W^T + b; the bias gradient is the column sum of dy."""
+    import llm_training_amd.ops.fused as fused
+    monkeypatch.setattr(fused, "GEMM_MODES", {"fwd": "lt", "dgrad": "lt", "wgrad": "lt"})
+    torch.manual_seed(0)
+    T, K, N = 512, 256, 384
+    x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16().requires_grad_(True)
+    b = torch.randn(N, device=DEV).to(bias_dtype).requires_grad_(True)
+    calls = []
+    monkeypatch.setattr(fused, "lib", lambda: _Spy(torch.ops.llmt, calls))
+    y = F_.linear(x, w, b)
+    assert calls == ["gemm_lt_bias"]
+    assert y.dtype == torch.bfloat16
+    assert _rel(y, x.float() @ w.float().t() + b.float()) < 1e-2
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    assert _rel(b.grad, dy.float().sum(0)) < 1e-2
+    assert _rel(x.grad, dy.float() @ w.float()) < 1e-2
+
+
+class _Spy:
+    """Records which torch.ops.llmt GEMM entry points a call goes through."""
+
+    def __init__(self, ops, calls):
+        self._ops, self._calls = ops, calls
+
+    def __getattr__(self, name):
+        if name.startswith("gemm_lt"):
+            self._calls.append(name)
+        return getattr(self._ops, name)
+
+
 # ----------------------------------------------------------------------------- int8 blockwise quant (ZeRO++)
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_int8_quant_dequant_matches_torch(dtype):
