@@ -140,7 +140,7 @@ class HFCausalLM(BaseModel):
             self.hf_model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
         self.fused_modules: dict[str, int] = {}
         if config.enable_liger_kernel:
-            self.fused_modules = apply_fused_kernels(self.hf_model)
+            self.fused_modules = apply_fused_kernels(self.hf_model, attention=self.uses_hip_attention)
             logger.info("HFCausalLM: fused kernels patched into %s", self.fused_modules or "no module")
 
     @property
@@ -257,59 +257,125 @@ def _is_silu(act) -> bool:
     return isinstance(act, nn.SiLU) or type(act).__name__ in ("SiLUActivation", "SiLU")
 
 
-_SLICE_CLASSES: dict[type, type] = {}
+_SLICE_CLASSES: dict[tuple[type, bool], type] = {}
 
 
-def _slice_linear(cls: type) -> type:
-    """A subclass of ``cls`` (an nn.Linear) whose ``weight`` is a row slice of the owning MLP's fused
-    ``gate_up_weight`` parameter instead of a parameter of its own."""
-    sub = _SLICE_CLASSES.get(cls)
+def _slice_linear(cls: type, with_bias: bool = False) -> type:
+    """A subclass of ``cls`` (an nn.Linear) whose ``weight`` (and ``bias``) are row slices of a fused
+    parameter of the owning module instead of parameters of its own."""
+    sub = _SLICE_CLASSES.get((cls, with_bias))
     if sub is None:
         def weight(self):
             lo, hi = self._fused_rows
-            return self._fused_owner.gate_up_weight[lo:hi]
-        sub = type(f"Fused{cls.__name__}", (cls,), {"weight": property(weight)})
-        _SLICE_CLASSES[cls] = sub
+            return getattr(self._fused_owner, self._fused_w)[lo:hi]
+        attrs = {"weight": property(weight)}
+        if with_bias:
+            def bias(self):
+                lo, hi = self._fused_rows
+                return getattr(self._fused_owner, self._fused_b)[lo:hi]
+            attrs["bias"] = property(bias)
+        sub = type(f"Fused{cls.__name__}", (cls,), attrs)
+        _SLICE_CLASSES[(cls, with_bias)] = sub
     return sub
 
 
-def _state_dict_split(module, state_dict, prefix, local_metadata):
-    """Checkpoints / HF export keep transformers' names: gate_up_weight -> gate_proj.weight, up_proj.weight."""
-    w = state_dict.pop(prefix + "gate_up_weight", None)
-    if w is not None:
-        i = module.gate_proj._fused_rows[1]
-        state_dict[prefix + "gate_proj.weight"] = w[:i]
-        state_dict[prefix + "up_proj.weight"] = w[i:]
+def _fuse_linears(owner: nn.Module, names: list[str], wname: str, bname: str | None = None) -> bool:
+    """Re-home the weights (and biases, when every projection has one and ``bname`` is given) of the
+    nn.Linear children ``names`` of ``owner`` into one parameter concatenated along the output rows: the
+    patched forward multiplies by it directly (one GEMM, no per-call torch.cat of weights, no cat backward)
+    and its gradient is written by the main-grad-aware linear kernel. The projections stay readable as
+    views (``q_proj.weight`` ...); state dicts keep the transformers key names."""
+    mods = [getattr(owner, n) for n in names]
+    if any("weight" not in m._parameters for m in mods) or len({m.weight.shape[1] for m in mods}) != 1:
+        return False
+    has_b = [m.bias is not None for m in mods]
+    fb = all(has_b)
+    if any(has_b) and not (fb and bname):
+        return False
+    rows, lo = [], 0
+    for m in mods:
+        rows.append((lo, lo + m.weight.shape[0]))
+        lo += m.weight.shape[0]
+    owner.register_parameter(wname, nn.Parameter(torch.cat([m.weight.detach() for m in mods], 0),
+                                                 requires_grad=any(m.weight.requires_grad for m in mods)))
+    if fb:
+        owner.register_parameter(bname, nn.Parameter(torch.cat([m.bias.detach() for m in mods], 0),
+                                                     requires_grad=any(m.bias.requires_grad for m in mods)))
+    for m, r in zip(mods, rows):
+        del m._parameters["weight"]
+        if fb:
+            del m._parameters["bias"]
+        m.__class__ = _slice_linear(type(m), fb)
+        object.__setattr__(m, "_fused_owner", owner)  # plain attributes: not a child module
+        object.__setattr__(m, "_fused_rows", r)
+        object.__setattr__(m, "_fused_w", wname)
+        if fb:
+            object.__setattr__(m, "_fused_b", bname)
+    groups = [("weight", wname)] + ([("bias", bname)] if fb else [])
 
+    def split(module, state_dict, prefix, local_metadata):
+        for suffix, fname in groups:
+            w = state_dict.pop(prefix + fname, None)
+            if w is not None:
+                for n, (a, b) in zip(names, rows):
+                    state_dict[f"{prefix}{n}.{suffix}"] = w[a:b]
 
-def _load_fuse(module, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys, error_msgs):
-    g, u = prefix + "gate_proj.weight", prefix + "up_proj.weight"
-    if g in state_dict and u in state_dict:
-        state_dict[prefix + "gate_up_weight"] = torch.cat([state_dict.pop(g), state_dict.pop(u)], 0)
+    def fuse(module, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys, error_msgs):
+        for suffix, fname in groups:
+            keys = [f"{prefix}{n}.{suffix}" for n in names]
+            if all(k in state_dict for k in keys):
+                state_dict[prefix + fname] = torch.cat([state_dict.pop(k) for k in keys], 0)
+
+    owner._register_state_dict_hook(split)
+    owner._register_load_state_dict_pre_hook(fuse, with_module=True)
+    return True
 
 
 def _fuse_gate_up(m: nn.Module) -> bool:
-    """Re-home gate_proj / up_proj weights into one [2I, h] parameter ``gate_up_weight`` (gate rows first):
-    the patched forward multiplies by it directly (no per-call torch.cat of 2 x I x h weights and no cat
-    backward), its gradient is written by the main-grad-aware linear kernel. ``gate_proj.weight`` /
-    ``up_proj.weight`` stay readable as views; state dicts keep the transformers key names."""
+    """gate_proj / up_proj weights as one [2I, h] parameter ``gate_up_weight`` (gate rows first)."""
     g, u = m.gate_proj, m.up_proj
-    if g.bias is not None or u.bias is not None or g.weight.shape[1] != u.weight.shape[1]:
+    if g.bias is not None or u.bias is not None:
         return False
-    if "weight" not in g._parameters or "weight" not in u._parameters:
+    return _fuse_linears(m, ["gate_proj", "up_proj"], "gate_up_weight")
+
+
+# attention modules with separate q / k / v projections, full-width rotate-half RoPE and no extra q / k
+# transforms: patched onto one fused QKV GEMM + the in-place RoPE kernel + flash attention (the native
+# Llama layer's path) when the model routes its attention to the HIP kernels
+_ATTN_PATCH = ("LlamaAttention", "MistralAttention", "Qwen2Attention")
+
+
+def _patch_attention(m: nn.Module) -> bool:
+    if type(m).__name__ not in _ATTN_PATCH or not all(hasattr(m, n) for n in ("q_proj", "k_proj", "v_proj", "o_proj")):
         return False
-    I = g.weight.shape[0]
-    fused = nn.Parameter(torch.cat([g.weight.detach(), u.weight.detach()], 0),
-                         requires_grad=g.weight.requires_grad or u.weight.requires_grad)
-    del g._parameters["weight"]
-    del u._parameters["weight"]
-    m.register_parameter("gate_up_weight", fused)
-    for mod, rows in ((g, (0, I)), (u, (I, I + u.out_features))):
-        mod.__class__ = _slice_linear(type(mod))
-        object.__setattr__(mod, "_fused_owner", m)  # plain attribute: not a child module
-        object.__setattr__(mod, "_fused_rows", rows)
-    m._register_state_dict_hook(_state_dict_split)
-    m._register_load_state_dict_pre_hook(_load_fuse, with_module=True)
+    cfg = getattr(m, "config", None)
+    if cfg is None or getattr(m, "q_norm", None) is not None or getattr(cfg, "partial_rotary_factor", 1.0) != 1.0:
+        return False
+    D = int(m.head_dim)
+    nq, nkv = int(cfg.num_attention_heads), int(cfg.num_key_value_heads)
+    if D not in (64, 96, 128) or m.q_proj.out_features != nq * D or m.k_proj.out_features != nkv * D:
+        return False
+    if not _fuse_linears(m, ["q_proj", "k_proj", "v_proj"], "qkv_weight", "qkv_bias"):
+        return False
+    # window as transformers hands it to the attention function (Mistral: the config's, Qwen2: per layer)
+    win = getattr(cfg, "sliding_window", None) if type(m).__name__ == "MistralAttention" else \
+        getattr(m, "sliding_window", None)
+    original = type(m).forward.__get__(m)  # still valid: q / k / v read slices of the fused parameter
+
+    def forward(hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None, _m=m,
+                **kwargs):
+        if past_key_values is not None or attention_mask is not None or position_embeddings is None:
+            return original(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+        from ..ops.fused import linear, rope_attention_bm
+        B, S = hidden_states.shape[:2]
+        qkv = linear(hidden_states, _m.qkv_weight, getattr(_m, "qkv_bias", None)).view(B, S, nq + 2 * nkv, D)
+        cos, sin = position_embeddings
+        o = rope_attention_bm(qkv, cos, sin, nq, nkv, segment_ids=kwargs.get("llmt_segment_ids"),
+                              window=None if win is None else int(win) - 1, scale=_m.scaling,
+                              dropout_p=float(_m.attention_dropout) if _m.training else 0.0)
+        return linear(o.reshape(B, S, nq * D), _m.o_proj.weight, _m.o_proj.bias), None
+
+    m.forward = forward
     return True
 
 
@@ -344,17 +410,21 @@ def _patch_mlp(m: nn.Module) -> bool:
     return True
 
 
-def apply_fused_kernels(model: nn.Module) -> dict[str, int]:
-    """Patch every RMSNorm and SiLU-gated MLP instance of a transformers model onto the HIP kernels;
-    returns {class name: count}. On the CPU the same functions run their torch reference ops."""
+def apply_fused_kernels(model: nn.Module, attention: bool = False) -> dict[str, int]:
+    """Patch every RMSNorm and SiLU-gated MLP instance of a transformers model onto the HIP kernels, and
+    with ``attention`` (the model's attention already routed to the HIP flash kernels) the q / k / v
+    projections, RoPE and attention of the supported attention classes; returns {class name: count}.
+    On the CPU the same functions run their torch reference ops."""
     done: dict[str, int] = {}
-    for m in model.modules():
+    for m in list(model.modules()):
         name = type(m).__name__
         ok = False
         if name.endswith("RMSNorm"):
             ok = _patch_norm(m)
         elif name.endswith("MLP"):
             ok = _patch_mlp(m)
+        elif attention and name.endswith("Attention"):
+            ok = _patch_attention(m)
         if ok:
             done[name] = done.get(name, 0) + 1
     return done

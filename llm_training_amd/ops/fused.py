@@ -545,33 +545,36 @@ class _RopeFlashAttnFn(Function):
     # Activations are sequence-major: qkv is [S, B, Htot, D] contiguous, positions [S, B]. The flash
     # kernels see [B, S, H, D] strided views (transpose(0, 1)) and return O in the same seq-major memory
     # order, so the output projection consumes it without a copy.
+    # bm=True: a batch-major buffer [B, S, Htot, D] (transformers' layout), positions [B * S] in the same
+    # token order; O comes back batch-major [B, S, Hq, D]
     @staticmethod
-    def forward(ctx, qkv, pos, cos, sin, seg, nq, nkv, causal, window, scale, dropout_p=0.0, seed=0):
+    def forward(ctx, qkv, pos, cos, sin, seg, nq, nkv, causal, window, scale, dropout_p=0.0, seed=0, bm=False):
         L = lib()
         L.rope_(qkv, pos, cos, sin, nq + nkv, False)
-        x = qkv.transpose(0, 1)
+        x = qkv if bm else qkv.transpose(0, 1)
         q, k, v = x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:]
         o, lse = L.flash_attn_fwd(q, k, v, seg, scale, causal, window, dropout_p, seed)
         ctx.save_for_backward(qkv, o, lse, pos, cos, sin, seg)
-        ctx.cfg = (nq, nkv, causal, window, scale, dropout_p, seed)
-        return o.transpose(0, 1)
+        ctx.cfg = (nq, nkv, causal, window, scale, dropout_p, seed, bm)
+        return o if bm else o.transpose(0, 1)
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse, pos, cos, sin, seg = ctx.saved_tensors
-        nq, nkv, causal, window, scale, dropout_p, seed = ctx.cfg
+        nq, nkv, causal, window, scale, dropout_p, seed, bm = ctx.cfg
         L = lib()
-        do = do.transpose(0, 1)
+        if not bm:
+            do = do.transpose(0, 1)
         if not _same_layout(do, o):
             do = torch.empty_like(o).copy_(do)
         elif do.stride() != o.stride():
             do = do.as_strided(o.shape, o.stride())  # differs only in the strides of size-1 dims
         dqkv = torch.empty_like(qkv)
-        x, dx = qkv.transpose(0, 1), dqkv.transpose(0, 1)
+        x, dx = (qkv, dqkv) if bm else (qkv.transpose(0, 1), dqkv.transpose(0, 1))
         L.flash_attn_bwd(x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:], o, do, lse, seg, dx[:, :, :nq],
                          dx[:, :, nq:nq + nkv], dx[:, :, nq + nkv:], scale, causal, window, dropout_p, seed)
         L.rope_(dqkv, pos, cos, sin, nq + nkv, True)
-        return dqkv, None, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -701,6 +704,47 @@ def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool =
                                    scale, "sdpa", dropout_p).transpose(0, 1)
     return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale,
                                impl).transpose(0, 1)
+
+
+# transformers-style rotary tables (full-width cos / sin [B or 1, S, D], rotate-half convention, computed once
+# per forward by the model and handed to every layer) as the per-token half-width fp32 tables the RoPE
+# kernel indexes: one conversion per forward (the last pair is cached by identity)
+_HF_ROPE = [None]
+
+
+def _token_tables(cos: torch.Tensor, sin: torch.Tensor, B: int, S: int):
+    hit = _HF_ROPE[0]
+    if hit is not None and hit[0] is cos and hit[1] is sin:
+        return hit[2]
+    Bc, Sc, D = cos.shape
+    if Sc != S or Bc not in (1, B):
+        raise ValueError(f"rotary tables {tuple(cos.shape)} for a [{B}, {S}] batch")
+    h = D // 2
+    ct = cos[..., :h].float().reshape(Bc * S, h).contiguous()
+    st = sin[..., :h].float().reshape(Bc * S, h).contiguous()
+    pos = torch.arange(Bc * S, device=cos.device).view(Bc, S).expand(B, S)
+    _HF_ROPE[0] = (cos, sin, (ct, st, pos))
+    return ct, st, pos
+
+
+def rope_attention_bm(qkv, cos, sin, n_q: int, n_kv: int, segment_ids=None, window: int | None = None,
+                      scale: float | None = None, dropout_p: float = 0.0):
+    """Causal fused RoPE + attention on a BATCH-MAJOR fused QKV buffer [B, S, n_q + 2 n_kv, D] (the HF
+    decoder layer's layout) with transformers' rotary tables ``cos`` / ``sin`` [B or 1, S, D] -> [B, S, n_q, D].
+    The same kernels as :func:`rope_attention` (in-place RoPE on the q / k heads, flash attention on strided
+    views, un-rotation of dQKV in the backward), fed per-token tables so any rope_type / scaling the model's
+    rotary embedding computed applies unchanged."""
+    B, S, _, D = qkv.shape
+    ct, st, pos = _token_tables(cos, sin, B, S)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    win = -1 if window is None else int(window)
+    if use_native(qkv):
+        qkv = qkv.contiguous()
+        seg = _native_seg(segment_ids, None)
+        seed = dropout_seed() if dropout_p > 0 else 0
+        return _RopeFlashAttnFn.apply(qkv, pos.reshape(-1).contiguous(), ct, st, seg, n_q, n_kv, True, win, scale,
+                                      float(dropout_p), seed, True)
+    return _ref_rope_attention(qkv, pos, ct, st, n_q, n_kv, True, segment_ids, win, scale, "sdpa", dropout_p)
 
 
 def _ref_rope_attention(qkv, positions, cos, sin, n_q, n_kv, causal, segment_ids, win, scale, impl,

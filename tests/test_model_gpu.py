@@ -531,6 +531,48 @@ def test_it_trainer_validation_accumulation_best_checkpoint(tmp_path, arch):
     assert len(kept) == 1 and kept[0].endswith("step=4.ckpt"), kept
 
 
+@pytest.mark.parametrize("model_type", ["llama", "qwen2"])
+def test_hf_fused_attention_on_hip(model_type):
+    """The patched transformers attention (one fused QKV GEMM with the bias epilogue for Qwen2, the in-place
+    RoPE kernel on transformers' rotary tables, flash attention, o_proj) against the unpatched module (HF
+    rotary + the HIP flash kernel through the AttentionInterface) on the same input, forward and backward."""
+    import copy as _copy
+
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig, apply_fused_kernels
+    hc = {"model_type": model_type, "num_hidden_layers": 1, "num_attention_heads": 8, "num_key_value_heads": 2,
+          "hidden_size": 1024, "intermediate_size": 1024, "vocab_size": 1000, "max_position_embeddings": 1024}
+    m = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc)), dtype=torch.bfloat16, device="cuda")
+    m.init_weights(0)
+    orig = m.hf_model.model.layers[0].self_attn
+    patched = _copy.deepcopy(orig)
+    assert apply_fused_kernels(patched, attention=True) == {type(orig).__name__: 1}
+    B, S = 2, 384
+    x = torch.randn(B, S, 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    pos = torch.arange(S, device="cuda").expand(B, S)
+    cos, sin = m.hf_model.model.rotary_emb(x, pos)
+    y0, _ = orig(x, position_embeddings=(cos, sin), attention_mask=None)
+    y1, _ = patched(x2, position_embeddings=(cos, sin), attention_mask=None)
+    g = torch.randn_like(y0)
+    y0.backward(g)
+    y1.backward(g)
+
+    def rel(a, b):
+        a, b = a.float(), b.float()
+        return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+    assert rel(y1, y0) < 1e-2
+    assert rel(x2.grad, x.grad) < 2e-2
+    P = dict(patched.named_parameters())
+    qw = P["qkv_weight"].grad
+    assert rel(qw[:1024], orig.q_proj.weight.grad) < 2e-2
+    assert rel(qw[1024:1280], orig.k_proj.weight.grad) < 2e-2
+    assert rel(qw[1280:], orig.v_proj.weight.grad) < 2e-2
+    assert rel(P["o_proj.weight"].grad, orig.o_proj.weight.grad) < 2e-2
+    if model_type == "qwen2":
+        assert rel(P["qkv_bias"].grad[:1024], orig.q_proj.bias.grad) < 2e-2
+
+
 def test_hf_fused_mlp_no_concat_and_no_leftover_transposed_gradient():
     """The patched HF MLP of a wide model (I >= 12288, Llama-3-8B-like) runs gate/up as one GEMM on the
     fused parameter (no cat kernel in forward or backward), takes the SwiGLU backward's transposed

@@ -300,19 +300,75 @@ def test_attention_dropout_applies_in_training_only():
 
 
 def hf_named_grads(m):
-    """Parameter gradients keyed by transformers' names (a fused gate_up_weight split back into gate / up)."""
+    """Parameter gradients keyed by transformers' names (fused gate_up / qkv parameters split back into the
+    projections whose weights / biases they hold)."""
+    slices = {}
+    for mod in m.modules():
+        owner = getattr(mod, "_fused_owner", None)
+        if owner is None:
+            continue
+        oname = next(n for n, x in m.named_modules() if x is owner)
+        mname = next(n for n, x in m.named_modules() if x is mod)
+        for suffix, attr in (("weight", "_fused_w"), ("bias", "_fused_b")):
+            f = getattr(mod, attr, None)
+            if f is not None:
+                slices.setdefault(f"{oname}.{f}", []).append((f"{mname}.{suffix}", mod._fused_rows))
     out = {}
     for n, p in m.named_parameters():
         if p.grad is None:
             continue
-        if n.endswith("gate_up_weight"):
-            mod = m.get_submodule(n.rsplit(".", 1)[0])
-            i = mod.gate_proj._fused_rows[1]
-            out[n.replace("gate_up_weight", "gate_proj.weight")] = p.grad[:i].clone()
-            out[n.replace("gate_up_weight", "up_proj.weight")] = p.grad[i:].clone()
+        if n in slices:
+            for name, (a, b) in slices[n]:
+                out[name] = p.grad[a:b].clone()
         else:
             out[n] = p.grad.clone()
     return out
+
+
+@pytest.mark.parametrize("model_type", ["llama", "qwen2", "mistral"])
+def test_hf_fused_attention_patch_matches(model_type):
+    """With the attention routed to the HIP kernels, the patch also fuses q / k / v into one projection
+    (Qwen2: with the biases) and runs RoPE + attention as the native layer does; outputs and gradients equal
+    transformers' own modules (eager attention, HF rotary), packed rows restart attention per document, and
+    checkpoints keep the HF key names."""
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 2,
+          "hidden_size": 256, "intermediate_size": 128, "vocab_size": 100, "max_position_embeddings": 64,
+          "rope_theta": 10000.0}
+    if model_type == "mistral":
+        hc["sliding_window"] = 7
+    ids = torch.randint(0, 100, (2, 16), generator=torch.Generator().manual_seed(1))
+
+    def run(patch, seg=None):
+        m = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=patch,
+                                        attn_implementation="flash" if patch else "eager"))
+        m.init_weights(0)
+        h = m.hidden_states(ids, segment_ids=seg)
+        h.float().pow(2).mean().backward()
+        return m, h.detach(), hf_named_grads(m)
+
+    _, h0, g0 = run(False)
+    m, h1, g1 = run(True)
+    assert any(n.endswith("Attention") for n in m.fused_modules), m.fused_modules
+    att = m.hf_model.model.layers[0].self_attn
+    assert "qkv_weight" in dict(att.named_parameters())
+    assert ("qkv_bias" in dict(att.named_parameters())) == (model_type == "qwen2")
+    assert torch.equal(att.k_proj.weight, att.qkv_weight[256:384])  # still readable as a view
+    assert torch.allclose(h0, h1, atol=1e-5, rtol=1e-4), (h0 - h1).abs().max()
+    assert g0.keys() == g1.keys()
+    for k in g0:
+        assert torch.allclose(g0[k], g1[k], atol=1e-5, rtol=1e-4), k
+    sd = m.state_dict()
+    assert "hf_model.model.layers.0.self_attn.q_proj.weight" in sd and not any("qkv_" in k for k in sd)
+    m2 = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=True, attn_implementation="flash"))
+    m2.load_state_dict(sd)
+    assert torch.equal(m2.hf_model.model.layers[0].self_attn.qkv_weight, att.qkv_weight)
+    # packed row 0 (documents of 9 and 7 tokens): the first document is the unpacked prefix, the second
+    # attends only to itself; row 1 (one document) is unchanged
+    _, h2, _ = run(True, torch.tensor([[1] * 9 + [2] * 7, [1] * 16]))
+    assert torch.allclose(h2[:, 1], h0[:, 1], atol=1e-5, rtol=1e-4)
+    assert torch.allclose(h2[:9, 0], h0[:9, 0], atol=1e-5, rtol=1e-4)
+    assert not torch.allclose(h2[9:, 0], h0[9:, 0], atol=1e-3)
 
 
 @pytest.mark.parametrize("model_type", ["llama", "qwen2", "mistral", "phi3"])
