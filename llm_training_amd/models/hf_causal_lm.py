@@ -410,6 +410,33 @@ def _patch_mlp(m: nn.Module) -> bool:
     return True
 
 
+_LAYER_PATCH = ("LlamaDecoderLayer", "MistralDecoderLayer", "Qwen2DecoderLayer")
+
+
+def _patch_decoder_layer(m: nn.Module) -> bool:
+    """Pre-norm decoder layer with the attention residual added inside the post-attention RMSNorm kernel
+    (the native layer's fused add + norm: one pass writes both the sum and its norm)."""
+    if type(m).__name__ not in _LAYER_PATCH or not all(hasattr(m, n) for n in
+                                                      ("input_layernorm", "self_attn", "post_attention_layernorm", "mlp")):
+        return False
+    norm = m.post_attention_layernorm
+    eps = getattr(norm, "variance_epsilon", getattr(norm, "eps", None))
+    if eps is None or getattr(norm, "weight", None) is None or type(norm).__name__.startswith(_NORM_SKIP):
+        return False
+
+    def forward(hidden_states, attention_mask=None, position_ids=None, past_key_values=None, use_cache=False,
+                position_embeddings=None, _m=m, _eps=float(eps), **kwargs):
+        from ..ops.fused import rms_norm
+        a, _ = _m.self_attn(hidden_states=_m.input_layernorm(hidden_states), attention_mask=attention_mask,
+                            position_ids=position_ids, past_key_values=past_key_values, use_cache=use_cache,
+                            position_embeddings=position_embeddings, **kwargs)
+        h, res = rms_norm(a, _m.post_attention_layernorm.weight, _eps, residual=hidden_states)
+        return res + _m.mlp(h)
+
+    m.forward = forward
+    return True
+
+
 def apply_fused_kernels(model: nn.Module, attention: bool = False) -> dict[str, int]:
     """Patch every RMSNorm and SiLU-gated MLP instance of a transformers model onto the HIP kernels, and
     with ``attention`` (the model's attention already routed to the HIP flash kernels) the q / k / v
@@ -425,6 +452,8 @@ def apply_fused_kernels(model: nn.Module, attention: bool = False) -> dict[str, 
             ok = _patch_mlp(m)
         elif attention and name.endswith("Attention"):
             ok = _patch_attention(m)
+        elif name.endswith("DecoderLayer"):
+            ok = _patch_decoder_layer(m)
         if ok:
             done[name] = done.get(name, 0) + 1
     return done
