@@ -342,33 +342,45 @@ def _fuse_gate_up(m: nn.Module) -> bool:
 # attention modules with separate q / k / v projections, full-width rotate-half RoPE and no extra q / k
 # transforms: patched onto one fused QKV GEMM + the in-place RoPE kernel + flash attention (the native
 # Llama layer's path) when the model routes its attention to the HIP kernels
-_ATTN_PATCH = ("LlamaAttention", "MistralAttention", "Qwen2Attention")
+_ATTN_PATCH = ("LlamaAttention", "MistralAttention", "Qwen2Attention", "Phi3Attention")
 
 
 def _patch_attention(m: nn.Module) -> bool:
-    if type(m).__name__ not in _ATTN_PATCH or not all(hasattr(m, n) for n in ("q_proj", "k_proj", "v_proj", "o_proj")):
+    name = type(m).__name__
+    fused_proj = name == "Phi3Attention"  # already one [q | k | v] projection
+    proj = ("qkv_proj", "o_proj") if fused_proj else ("q_proj", "k_proj", "v_proj", "o_proj")
+    if name not in _ATTN_PATCH or not all(hasattr(m, n) for n in proj):
         return False
     cfg = getattr(m, "config", None)
     if cfg is None or getattr(m, "q_norm", None) is not None or getattr(cfg, "partial_rotary_factor", 1.0) != 1.0:
         return False
     D = int(m.head_dim)
     nq, nkv = int(cfg.num_attention_heads), int(cfg.num_key_value_heads)
-    if D not in (64, 96, 128) or m.q_proj.out_features != nq * D or m.k_proj.out_features != nkv * D:
+    if D not in (64, 96, 128):
         return False
-    if not _fuse_linears(m, ["q_proj", "k_proj", "v_proj"], "qkv_weight", "qkv_bias"):
+    if fused_proj:
+        if m.qkv_proj.out_features != (nq + 2 * nkv) * D:
+            return False
+    elif (m.q_proj.out_features != nq * D or m.k_proj.out_features != nkv * D
+          or not _fuse_linears(m, ["q_proj", "k_proj", "v_proj"], "qkv_weight", "qkv_bias")):
         return False
-    # window as transformers hands it to the attention function (Mistral: the config's, Qwen2: per layer)
-    win = getattr(cfg, "sliding_window", None) if type(m).__name__ == "MistralAttention" else \
+    # window as transformers hands it to the attention function (Mistral / Phi-3: the config's, Qwen2: per layer)
+    win = getattr(cfg, "sliding_window", None) if name in ("MistralAttention", "Phi3Attention") else \
         getattr(m, "sliding_window", None)
     original = type(m).forward.__get__(m)  # still valid: q / k / v read slices of the fused parameter
 
     def forward(hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None, _m=m,
                 **kwargs):
-        if past_key_values is not None or attention_mask is not None or position_embeddings is None:
+        if (past_key_values is not None or attention_mask is not None or position_embeddings is None
+                or position_embeddings[0].shape[-1] != D):  # (partial rotary: transformers' own path)
             return original(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
         from ..ops.fused import linear, rope_attention_bm
         B, S = hidden_states.shape[:2]
-        qkv = linear(hidden_states, _m.qkv_weight, getattr(_m, "qkv_bias", None)).view(B, S, nq + 2 * nkv, D)
+        if fused_proj:
+            w, b = _m.qkv_proj.weight, _m.qkv_proj.bias
+        else:
+            w, b = _m.qkv_weight, getattr(_m, "qkv_bias", None)
+        qkv = linear(hidden_states, w, b).view(B, S, nq + 2 * nkv, D)
         cos, sin = position_embeddings
         o = rope_attention_bm(qkv, cos, sin, nq, nkv, segment_ids=kwargs.get("llmt_segment_ids"),
                               window=None if win is None else int(win) - 1, scale=_m.scaling,

@@ -325,7 +325,7 @@ def hf_named_grads(m):
     return out
 
 
-@pytest.mark.parametrize("model_type", ["llama", "qwen2", "mistral"])
+@pytest.mark.parametrize("model_type", ["llama", "qwen2", "mistral", "phi3"])
 def test_hf_fused_attention_patch_matches(model_type):
     """With the attention routed to the HIP kernels, the patch also fuses q / k / v into one projection
     (Qwen2: with the biases) and runs RoPE + attention as the native layer does; outputs and gradients equal
@@ -335,8 +335,10 @@ def test_hf_fused_attention_patch_matches(model_type):
     hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 2,
           "hidden_size": 256, "intermediate_size": 128, "vocab_size": 100, "max_position_embeddings": 64,
           "rope_theta": 10000.0}
-    if model_type == "mistral":
+    if model_type in ("mistral", "phi3"):
         hc["sliding_window"] = 7
+    if model_type == "phi3":
+        hc.update(pad_token_id=0, bos_token_id=1, eos_token_id=2)
     ids = torch.randint(0, 100, (2, 16), generator=torch.Generator().manual_seed(1))
 
     def run(patch, seg=None):
@@ -351,18 +353,20 @@ def test_hf_fused_attention_patch_matches(model_type):
     m, h1, g1 = run(True)
     assert any(n.endswith("Attention") for n in m.fused_modules), m.fused_modules
     att = m.hf_model.model.layers[0].self_attn
-    assert "qkv_weight" in dict(att.named_parameters())
-    assert ("qkv_bias" in dict(att.named_parameters())) == (model_type == "qwen2")
-    assert torch.equal(att.k_proj.weight, att.qkv_weight[256:384])  # still readable as a view
+    if model_type != "phi3":  # (Phi-3's projection is fused already)
+        assert "qkv_weight" in dict(att.named_parameters())
+        assert ("qkv_bias" in dict(att.named_parameters())) == (model_type == "qwen2")
+        assert torch.equal(att.k_proj.weight, att.qkv_weight[256:384])  # still readable as a view
     assert torch.allclose(h0, h1, atol=1e-5, rtol=1e-4), (h0 - h1).abs().max()
     assert g0.keys() == g1.keys()
     for k in g0:
         assert torch.allclose(g0[k], g1[k], atol=1e-5, rtol=1e-4), k
-    sd = m.state_dict()
-    assert "hf_model.model.layers.0.self_attn.q_proj.weight" in sd and not any("qkv_" in k for k in sd)
-    m2 = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=True, attn_implementation="flash"))
-    m2.load_state_dict(sd)
-    assert torch.equal(m2.hf_model.model.layers[0].self_attn.qkv_weight, att.qkv_weight)
+    if model_type != "phi3":
+        sd = m.state_dict()
+        assert "hf_model.model.layers.0.self_attn.q_proj.weight" in sd and not any("qkv_" in k for k in sd)
+        m2 = HFCausalLM(HFCausalLMConfig(hf_config=dict(hc), enable_liger_kernel=True, attn_implementation="flash"))
+        m2.load_state_dict(sd)
+        assert torch.equal(m2.hf_model.model.layers[0].self_attn.qkv_weight, att.qkv_weight)
     # packed row 0 (documents of 9 and 7 tokens): the first document is the unpacked prefix, the second
     # attends only to itself; row 1 (one document) is unchanged
     _, h2, _ = run(True, torch.tensor([[1] * 9 + [2] * 7, [1] * 16]))
