@@ -97,6 +97,8 @@ _LAYOUT_CACHE: dict[tuple, str] = {}
 # largest weight-gradient output (elements) offered the split-K candidates (fp32 slabs: 8 bytes / element)
 _SPLITK_MAX_OUT = int(os.environ.get("LLMT_WGRAD_SPLITK_MAX", str(1 << 26)))
 _SPLITK = (2, 4)  # contraction splits offered (slabs: n_split x N x K fp32)
+# offer the both-operands-transposed (TN) weight-gradient layouts among the timed candidates
+_WGRAD_TN = os.environ.get("LLMT_WGRAD_TN", "1").strip().lower() not in ("0", "false", "off")
 # offer the hand-written GEMM (direct and split-K) among the timed weight-gradient candidates
 _OWN_WGRAD = os.environ.get("LLMT_GEMM_OWN", "1").strip().lower() not in ("0", "false", "off")
 
@@ -252,7 +254,9 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
         def tn():  # both transposed: token-contiguous operands (the layout hipBLASLt runs fastest)
             lib().gemm_lt(transpose(x), transpose(dy), o2, True, False, K, N, M, M, M, K, accumulate, sk)
 
-        variants = {"nt": nt, "tt": tt, "nn": nn, "tn": tn}
+        variants = {"nt": nt, "tt": tt, "nn": nn}
+        if _WGRAD_TN:
+            variants["tn"] = tn
         if N * K <= _SPLITK_MAX_OUT and M % 256 == 0:
             # split-K along the token (contraction) dimension into 2 or 4 slices, run as one strided-batch
             # GEMM into fp32 slabs + one reduction pass: 2-4x the output tiles for outputs that fill the
@@ -269,7 +273,8 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
                 variants[f"nt{ns}"] = _split(x, dy, False, True, _ld(x), _ld(dy), ns)
                 variants[f"tt{ns}"] = _split(lambda: transpose(x), dy, True, True, M, _ld(dy), ns)
                 variants[f"nn{ns}"] = _split(x, lambda: transpose(dy), False, False, _ld(x), M, ns)
-                variants[f"tn{ns}"] = _split(lambda: transpose(x), lambda: transpose(dy), True, False, M, M, ns)
+                if _WGRAD_TN:
+                    variants[f"tn{ns}"] = _split(lambda: transpose(x), lambda: transpose(dy), True, False, M, M, ns)
         if _OWN_WGRAD and M % 32 == 0 and N % 4 == 0:
             # the hand-written ping-pong GEMM (csrc/gemm.hip) reads both token-major operands directly
             # (transposed LDS reads, no materialised transposes); split into 2 / 4 contraction slices for
