@@ -1410,6 +1410,11 @@ __device__ __forceinline__ void mfma_vv(f32v16& c, const bfv8& x, const bfv8& y)
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(x), "a"(y));
 }
 
+// P = exp2(x) and dS = P (dP + nd) as single-lane asm (see exp_ds in the dQ kernel)
+__device__ __forceinline__ void exp_pds(float x, float dp, float nd, float& p, float& ds) {
+  asm("v_exp_f32 %0, %2\n\tv_add_f32 %1, %3, %4\n\tv_mul_f32 %1, %0, %1" : "=&v"(p), "=&v"(ds) : "v"(x), "v"(dp), "v"(nd));
+}
+
 template <int D, bool OM = false, int NSL = 6>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const float* ld) {
   constexpr int NKK = D / 16, NDT = D / 32;
@@ -1622,9 +1627,13 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
     // softmax element v of a tile into the bf16 operands pn / dn
     auto smx = [&](int v, const f32v16& sc, const f32v16& dc, const float (&lq)[16], const float (&nd)[16],
                    bfv8 (&pn)[2], bfv8 (&dn)[2]) {
-      const float p = fexp2(fmaf(sc[v], sl2, lq[v]));
+      // single-lane asm: with plain C++ hipcc paired neighbouring elements into v_pk_add_f32 / v_pk_mul_f32
+      // and padded the phase with 16 s_nop; this form took the B4 S8192 backward from 7.996 to 7.545 ms in
+      // one process, bitwise-equal gradients
+      float p, ds;
+      exp_pds(fmaf(sc[v], sl2, lq[v]), dc[v], nd[v], p, ds);
       pn[v >> 3][v & 7] = (__bf16)p;
-      dn[v >> 3][v & 7] = (__bf16)(p * (dc[v] + nd[v]));
+      dn[v >> 3][v & 7] = (__bf16)ds;
     };
     // dV / dK of the previous tile (operands po / dso, fragments tf) || softmax of this tile into pn / dsn;
     // with `ns` the first two k-steps of the next tile's rows are read at the end
@@ -2287,6 +2296,15 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3c_kernel(AttnArgs a) {
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
 // dQ = scale * sum; the row constants come straight from lse / delta (delta written by the prep kernel).
 // NW = 8: two query heads of one kv group per workgroup sharing the K/V ring (as fa_fwd3_kernel)
+// dS = P (dP - delta) with P = exp2(x): the exp, the subtraction and the product as three single-lane VALU
+// instructions in one asm block (the product reads the exp result one instruction later: its trans-use wait
+// state), so hipcc cannot pair neighbouring elements into v_pk_add_f32 / v_pk_mul_f32 beside the MFMAs
+__device__ __forceinline__ float exp_ds(float x, float dp, float dlt) {
+  float p, t;
+  asm("v_exp_f32 %0, %2\n\tv_sub_f32 %1, %3, %4\n\tv_mul_f32 %0, %0, %1" : "=&v"(p), "=&v"(t) : "v"(x), "v"(dp), "v"(dlt));
+  return p;
+}
+
 template <int D, bool IL = true, bool WS = false, int NW = 4, bool OM = false>
 __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;
@@ -2414,8 +2432,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
           const IdxRange rg = idx_range(klo, khi, n0 + 32 * tt + 4 * hh);
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float pr = in_range(rg, 8 * (i >> 2) + (i & 3)) ? fexp2(fmaf(st[i], sl2, -lse2)) : 0.f;
-            st[i] = pr * (dpt[i] - dlt);
+            // masked: x = -inf -> exp2 = 0 -> dS = 0
+            const float x = in_range(rg, 8 * (i >> 2) + (i & 3)) ? fmaf(st[i], sl2, -lse2) : -INFINITY;
+            st[i] = exp_ds(x, dpt[i], dlt);
           }
         } else if (OM && need_mask) {
           const int* Ss = reinterpret_cast<const int*>(slot + 2 * IMG);
@@ -2436,9 +2455,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
               st[i] = pr * (dpt[i] - dlt);
             }
           }
-        } else {
+        } else {  // (single-lane asm: B4 S8192 backward 7.978 -> 7.955 ms against hipcc's packed form)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) st[i] = fexp2(fmaf(st[i], sl2, -lse2)) * (dpt[i] - dlt);
+          for (int i = 0; i < 16; ++i) st[i] = exp_ds(fmaf(st[i], sl2, -lse2), dpt[i], dlt);
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
