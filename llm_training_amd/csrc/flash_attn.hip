@@ -1862,8 +1862,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
     issue(0);
     wait_vm<0>();
     ring_barrier();
-    for (int t = 0; t < T; ++t) {
-      const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
+    // the tile loop unrolled by the ring's two slots: each slot's LDS offsets are compile-time constants
+    // (folded into the ds_read offset fields instead of one v_add per read and tile)
+    auto tile = [&](auto sidx, int t) {
+      const char* slot = smem + decltype(sidx)::value * SLOT;
       const int n0 = kv_beg + t * BN;
       if (t + 1 < T) issue(t + 1);
       bfv8 fr[16];
@@ -1991,6 +1993,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
       __builtin_amdgcn_sched_barrier(0);  // the P.V work stays ahead of the wait: the DMA flies under it
       wait_vm<0>();  // this wave's DMA of tile t + 1
       ring_barrier();
+        };
+    for (int t = 0; t < T; t += 2) {
+      tile(std::integral_constant<int, 0>{}, t);
+      if (t + 1 < T) tile(std::integral_constant<int, 1>{}, t + 1);
     }
   }
 
@@ -2382,8 +2388,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
     issue(0);
     wait_vm<0>();
     ring_barrier();
-    for (int t = 0; t < T; ++t) {
-      const char* slot = smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT);
+    // the tile loop unrolled by the ring's two slots: each slot's LDS offsets are compile-time constants
+    // (folded into the ds_read offset fields instead of one v_add per read and tile)
+    auto tile = [&](auto sidx, int t) {
+      const char* slot = smem + decltype(sidx)::value * SLOT;
       const int n0 = kv_beg + t * BN;
       if (t + 1 < T) issue(t + 1);
       const bool m_seg = seg_mask(a, qr, n0, n0 + BN - 1);
@@ -2469,6 +2477,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       wait_vm<0>();  // this wave's DMA of tile t + 1
       ring_barrier();
+        };
+    for (int t = 0; t < T; t += 2) {
+      tile(std::integral_constant<int, 0>{}, t);
+      if (t + 1 < T) tile(std::integral_constant<int, 1>{}, t + 1);
     }
   }
 
