@@ -2311,7 +2311,7 @@ __device__ __forceinline__ float exp_ds(float x, float dp, float dlt) {
   return p;
 }
 
-template <int D, bool IL = true, bool WS = false, int NW = 4, bool OM = false>
+template <int D, bool IL = true, bool WS = false, int NW = 4, bool OM = false, bool XS = true>
 __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   constexpr int NKK = D / 16, NDT = D / 32;
   constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
@@ -2439,10 +2439,13 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
         if (need_mask && !OM) {
           const IdxRange rg = idx_range(klo, khi, n0 + 32 * tt + 4 * hh);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
+          for (int i = 0; i < 16; i += 2) {
             // masked: x = -inf -> exp2 = 0 -> dS = 0
-            const float x = in_range(rg, 8 * (i >> 2) + (i & 3)) ? fmaf(st[i], sl2, -lse2) : -INFINITY;
-            st[i] = exp_ds(x, dpt[i], dlt);
+            const float x0 = in_range(rg, 8 * (i >> 2) + (i & 3)) ? fmaf(st[i], sl2, -lse2) : -INFINITY;
+            const float x1 = in_range(rg, 8 * (i >> 2) + (i & 3) + 1) ? fmaf(st[i + 1], sl2, -lse2) : -INFINITY;
+            const float t0 = dpt[i] - dlt, t1 = dpt[i + 1] - dlt;
+            asm("v_exp_f32 %0, %2\n\tv_exp_f32 %1, %3\n\tv_mul_f32 %0, %0, %4\n\tv_mul_f32 %1, %1, %5"
+                : "=&v"(st[i]), "=&v"(st[i + 1]) : "v"(x0), "v"(x1), "v"(t0), "v"(t1));
           }
         } else if (OM && need_mask) {
           const int* Ss = reinterpret_cast<const int*>(slot + 2 * IMG);
@@ -2465,7 +2468,20 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
           }
         } else {  // (single-lane asm: B4 S8192 backward 7.978 -> 7.955 ms against hipcc's packed form)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) st[i] = exp_ds(fmaf(st[i], sl2, -lse2), dpt[i], dlt);
+          for (int i = 0; i < 16; i += 2) {
+            if constexpr (!XS) {  // (A/B reference: the asm block reads the MFMA results itself)
+              st[i] = exp_ds(fmaf(st[i], sl2, -lse2), dpt[i], dlt);
+              st[i + 1] = exp_ds(fmaf(st[i + 1], sl2, -lse2), dpt[i + 1], dlt);
+              continue;
+            }
+            // the MFMA results are read by compiler-visible VALU (fma, sub: hipcc places the minimal XDL
+            // wait states instead of padding every asm block that reads them), the exp pair and the products
+            // in one asm block (trans-use wait by placement)
+            const float x0 = fmaf(st[i], sl2, -lse2), x1 = fmaf(st[i + 1], sl2, -lse2);
+            const float t0 = dpt[i] - dlt, t1 = dpt[i + 1] - dlt;
+            asm("v_exp_f32 %0, %2\n\tv_exp_f32 %1, %3\n\tv_mul_f32 %0, %0, %4\n\tv_mul_f32 %1, %1, %5"
+                : "=&v"(st[i]), "=&v"(st[i + 1]) : "v"(x0), "v"(x1), "v"(t0), "v"(t1));
+          }
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -2779,6 +2795,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<128, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (dqv == 1)
         fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      else if (dqv == 4 && a.rmask)  // asm reading the MFMA results (A/B reference)
+        fa_bwd_dq3_kernel<128, true, true, 4, false, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else if (a.rmask)
         fa_bwd_dq3_kernel<128, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
