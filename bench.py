@@ -425,6 +425,10 @@ def main():
         # the schedule actually run: one GPU defaults to ZeRO-0 (no collectives); several GPUs to ZeRO-2
         # (the reference example's DeepSpeed stage); force_sharded runs the dp>1 schedule on one GPU
         cfg_out["force_sharded"] = bool(args.force_sharded)
+        if stage == 2 and pc.dp_size > 1:
+            # the FSDP schedule it matches: parameters gathered once per step (FSDP2
+            # reshard_after_forward=False), gradients reduce-scattered, optimizer state sharded
+            cfg_out["fsdp_equivalent"] = "FSDP2 reshard_after_forward=False"
         out = {
             "metric": metric,
             "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
