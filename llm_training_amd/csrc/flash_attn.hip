@@ -196,6 +196,9 @@ struct AttnArgs {
   // 1: masks from per-row index ranges (the run of a packed row, causal, window, sequence end) instead of
   // per-element segment-id compares; needs run bounds (rs / re) whenever `seg` is set
   int rmask;
+  // backward: non-null -> the dQ kernel computes delta = rowsum(dO * O) itself and writes the packed per-tile
+  // row constants the dK/dV kernel reads here (no separate prep pass); null -> the prep kernel ran
+  float* ldw;
 };
 
 __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q, uint32_t k) {
@@ -2336,7 +2339,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   const float sl2 = a.scale * kLog2e;
   const int64_t lrow = ((int64_t)b * a.Hq + h) * S + min(qrow, S - 1);
   float lse2 = qrow < S ? a.lse[lrow] * kLog2e : INFINITY;
-  float dlt = qrow < S ? a.delta[lrow] : 0.f;
+  float dlt = (qrow < S && !a.ldw) ? a.delta[lrow] : 0.f;
   int sq = (OM && a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;  // OM: see fa_fwd3_kernel
   int klo = 0, khi = -1;
   if (!OM) key_interval(a, b, qrow, klo, khi);
@@ -2346,6 +2349,29 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   for (int kk = 0; kk < NKK; ++kk) {
     qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
     df[kk] = gload8(dop + (int64_t)min(qrow, S - 1) * a.d_ss + kk * 16 + hh * 8, qrow < S);
+  }
+  if (a.ldw) {
+    // the backward prep fused in: delta = rowsum(dO * O) from this lane's half row (64 of D elements, the
+    // other half in lane r + 32), then the row constants of this wave's 32-row tile for the dK/dV kernel
+    // (fa_bwd_prep128_kernel's layout: -lse / scale, -delta, segment id, -lse * log2e)
+    const bf16* opr = a.o + (int64_t)b * a.o_sb + (int64_t)h * a.o_sh + (int64_t)min(qrow, S - 1) * a.o_ss;
+    float dl = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const bfv8 o8 = gload8(opr + kk * 16 + hh * 8, qrow < S);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dl = fmaf((float)o8[i], (float)df[kk][i], dl);
+    }
+    dl += __shfl_xor(dl, 32, 64);
+    dlt = qrow < S ? dl : 0.f;
+    if (hh == 0 && qw < S) {  // (the last block's waves past the sequence end have no tile)
+      float* blk = a.ldw + (((int64_t)b * a.Hq + h) * ((S + 31) / 32) + (qw >> 5)) * kLdTile;
+      const float l = qrow < S ? a.lse[lrow] : -INFINITY;
+      blk[r] = l == -INFINITY ? -INFINITY : -l / a.scale;
+      blk[32 + r] = -dlt;
+      reinterpret_cast<int*>(blk)[64 + r] = qrow < S ? (a.seg ? a.seg[(int64_t)b * S + qrow] : 0) : -1;
+      blk[96 + r] = l == -INFINITY ? -INFINITY : -l * kLog2e;
+    }
   }
   // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
   asm volatile("" : "+v"(sq), "+v"(lse2), "+v"(dlt), "+v"(klo), "+v"(khi));
@@ -2747,8 +2773,18 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws)
     float* ld = delta + nrows;
     const int64_t nT = (S + 31) / 32;
+    // the dQ kernel computes delta and writes the row constants itself (its waves cover every 32-row tile
+    // of every head, and the dK/dV kernel runs after it on this stream); LLMT_FA_PREP=1: the separate prep
+    // pass (A/B reference, read per launch)
+    const char* pe = getenv("LLMT_FA_PREP");
+    const bool fused_prep = !(pe && atoi(pe) == 1);
+    if (fused_prep) a.ldw = ld;
+    auto prep = [&](auto d_c) {
+      if (!fused_prep)
+        fa_bwd_prep128_kernel<decltype(d_c)::value><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
+    };
     if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
-      fa_bwd_prep128_kernel<96><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
+      prep(std::integral_constant<int, 96>{});
       if (a.rmask)
         fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
@@ -2764,7 +2800,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       return hipGetLastError();
     }
     if (D == 64) {
-      fa_bwd_prep128_kernel<64><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
+      prep(std::integral_constant<int, 64>{});
       if (a.rmask)
         fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
@@ -2779,7 +2815,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       return hipGetLastError();
     }
-    fa_bwd_prep128_kernel<128><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
+    prep(std::integral_constant<int, 128>{});
     // dQ: B4 S8192 Hq32 Hkv8 backward 9.16 ms with dq3 vs 9.66 ms with the earlier one-wave-per-SIMD ring
     // kernel (removed, like the 8-wave role-split dK/dV kernel: 10.81 vs 9.89 ms, and the ring forward)
     {
