@@ -345,6 +345,11 @@ def main():
 
     # untimed: bandwidth of one layer-unit all-gather / reduce-scatter over the data-parallel group
     rccl = {"backend": comm_backend, "world": world}
+    # the collective-library knobs this run saw (RCCL / NCCL channel, protocol, MSCCL settings): set by the
+    # user or launcher, never hard-coded here, and recorded with the numbers they produced
+    knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_"))}
+    if knobs:
+        rccl["env"] = knobs
     if dist.is_initialized() and args.probe_mb > 0:
         wd.arm("collective bandwidth probe")
         rccl.update(probe_collectives(pc, device, args.probe_mb))
