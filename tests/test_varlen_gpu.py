@@ -142,3 +142,28 @@ def test_attention_kernel_variants_bitwise(Hq, Hkv, D, packed, monkeypatch):
         monkeypatch.delenv(env)
         for name, x, y in zip(("o", "dq", "dk", "dv"), got, base):
             assert torch.equal(x, y), f"{env}={val}: {name} differs"
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(8, 2, 128), (8, 4, 64), (4, 4, 96)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_backward_prep_inside_dq_matches_separate_pass(Hq, Hkv, D, packed, monkeypatch):
+    """The dQ kernel computes delta = rowsum(O * dO) and writes the per-32-row constants the dK/dV kernel
+    reads (the default), against the separate prep pass (LLMT_FA_PREP=1): same gradients up to the fp32
+    summation order of delta. A ragged length (S = 300: the last 128-row dQ block has waves wholly past
+    the sequence end, which must not write a tile) with several heads and batch rows, where a stray tile
+    write would land in the next head's constants."""
+    torch.manual_seed(0)
+    B, S = 2, 300
+    q = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    do = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    seg = _layout(S, [90, 17, 130], 11).expand(B, S).contiguous() if packed else None
+    fused = _fwd_bwd(q, k, v, do, seg)
+    monkeypatch.setenv("LLMT_FA_PREP", "1")
+    sep = _fwd_bwd(q, k, v, do, seg)
+    monkeypatch.delenv("LLMT_FA_PREP")
+    assert torch.equal(fused[0], sep[0])
+    real = (seg != 0).view(B, S, 1, 1) if packed else torch.ones(B, S, 1, 1, dtype=torch.bool, device=DEV)
+    for name, x, y in zip(("dq", "dk", "dv"), fused[1:], sep[1:]):
+        assert _rel(x * real, y * real) < 5e-3, name
