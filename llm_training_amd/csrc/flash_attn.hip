@@ -877,9 +877,10 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 }
 
 // ============================================================================ backward, D = 128 pipeline
-// The D = 64 / 96 / 128 backward (every Llama-family and Phi-3 model) is: a prep kernel (delta and the
-// packed per-row constants below), the query-parallel dQ kernel (fa_bwd_dq3_kernel, two workgroups per
-// CU) and this key-parallel dK/dV kernel, built for one wave per SIMD (512 registers per lane):
+// The D = 64 / 96 / 128 backward (every Llama-family and Phi-3 model) is: the query-parallel dQ kernel
+// (fa_bwd_dq3_kernel, two workgroups per CU), which also computes delta and writes the packed per-row
+// constants below (fa_bwd_prep128_kernel is the separate-pass form, LLMT_FA_PREP=1), and this key-parallel
+// dK/dV kernel, built for one wave per SIMD (512 registers per lane):
 //  * Q / dO tiles arrive by LDS-DMA (`buffer_load ... lds`, zero-filled past the end) into a ring of NS
 //    slots, several tiles ahead, behind counted `s_waitcnt vmcnt` and a raw barrier.
 //  * one wave per SIMD issues one instruction per issue slot, so the loop is instruction-bound, not
@@ -2303,7 +2304,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd3c_kernel(AttnArgs a) {
 // two workgroups per CU): per 32-key half of a 64-key tile, batched K row reads -> S^T = K.Q^T, batched
 // V row reads -> dP^T = V.dO^T, dS = P (dP - delta) with P = exp2(S * scale * log2e - lse * log2e)
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
-// dQ = scale * sum; the row constants come straight from lse / delta (delta written by the prep kernel).
+// dQ = scale * sum; the row constants come straight from lse / delta. delta = rowsum(O * dO) is computed
+// here from the wave's own O and dO rows (and written, with -lse/scale, the segment ids and -lse*log2e, as
+// the ld tiles the dK/dV kernel reads next); with LLMT_FA_PREP=1 it comes from the prep kernel instead.
 // NW = 8: two query heads of one kv group per workgroup sharing the K/V ring (as fa_fwd3_kernel)
 // dS = P (dP - delta) with P = exp2(x): the exp, the subtraction and the product as three single-lane VALU
 // instructions in one asm block (the product reads the exp result one instruction later: its trans-use wait
