@@ -56,8 +56,10 @@ WORKLOADS = {
                   8192, 4),
     "it": ("tokens/sec (whole node) Phi-3-mini instruction tuning, NEFTune + varlen packing", "Phi-3-mini-128k",
            4096, 16),
-    "dpo": ("tokens/sec (whole node) Llama-3-8B DPO preference tuning", "Llama-3-8B", 4096, 2),
-    "orpo": ("tokens/sec (whole node) Llama-3-8B ORPO preference tuning", "Llama-3-8B", 4096, 2),
+    # DPO / ORPO: pairs per micro-batch (x 2 sides x 4096 tokens); DPO 3 (244 GiB, its frozen reference
+    # model adds 16 GB), ORPO 4
+    "dpo": ("tokens/sec (whole node) Llama-3-8B DPO preference tuning", "Llama-3-8B", 4096, 3),
+    "orpo": ("tokens/sec (whole node) Llama-3-8B ORPO preference tuning", "Llama-3-8B", 4096, 4),
     "gpt2-cpu": ("tokens/sec GPT-2 small CLM pre-train on CPU (plumbing)", "GPT-2-small", 1024, 2),
 }
 # GPT-2 small (124 M) through HFCausalLM: BASELINE.json config #1, a CPU plumbing run
