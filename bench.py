@@ -414,6 +414,7 @@ def main():
     if args.workload == "dpo":
         fpt += flops_per_token(cfg, S, frac) / 3  # frozen reference model: forward only
     peak_mem = torch.cuda.max_memory_allocated(device) / 2 ** 30
+    import llm_training_amd.ops.fused as F_layouts
     if rank == 0:
         par = f"dp{pc.dp_size}" + (f"-tp{pc.tp_size}" if pc.tp_size > 1 else "")
         cfg_out = {"model": model_name if not args.layers else f"{model_name}-{args.layers}L(INVALID-debug)",
@@ -451,7 +452,11 @@ def main():
             "peak_mem_gib": round(peak_mem, 1),
             "final_loss": round(final_loss, 4),
             "rccl": rccl,
+            # how the GEMM layouts were chosen (shipped table / timed / rank 0's) and the hash of the choices
+            "gemm_layouts": F_layouts.layout_summary(),
         }
+        if os.environ.get("LLMT_GEMM_LAYOUT_DUMP"):
+            F_layouts.dump_layouts(os.environ["LLMT_GEMM_LAYOUT_DUMP"])
         print(json.dumps(out), flush=True)
     wd.arm("shutdown")
     if dist.is_initialized():

@@ -1419,7 +1419,11 @@ __device__ __forceinline__ void exp_pds(float x, float dp, float nd, float& p, f
   asm("v_exp_f32 %0, %2\n\tv_add_f32 %1, %3, %4\n\tv_mul_f32 %1, %0, %1" : "=&v"(p), "=&v"(ds) : "v"(x), "v"(dp), "v"(nd));
 }
 
-template <int D, bool OM = false, int NSL = 6>
+// TRJ = 1: the transposed Q^T / dO^T fragments of phase B are read just in time inside phase B (two MFMAs
+// ahead; the first two at the end of phase A) instead of all in phase A. With every wave of the CU in the same
+// phase (one barrier per tile), phase A carried ~40 KB of LDS reads per wave against 16 MFMAs, more than the
+// LDS array serves in their time, while phase B read nothing; split by phase, each fits under its MFMAs.
+template <int D, bool OM = false, int NSL = 6, int TRJ = 0>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const float* ld) {
   constexpr int NKK = D / 16, NDT = D / 32;
   // NSL ring slots: tiles issued NSL - 2 ahead, each given NSL - 4 iterations to land
@@ -1584,9 +1588,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
             nd[4 * c] = d4.x; nd[4 * c + 1] = d4.y; nd[4 * c + 2] = d4.z; nd[4 * c + 3] = d4.w;
           }
         }
-        if constexpr (decltype(with_tr)::value) {
+        if constexpr (decltype(with_tr)::value && TRJ == 0) {
 #pragma unroll
           for (int i = kk * NB / NKK; i < (kk + 1) * NB / NKK; ++i) tf[i] = trf(ps, i);
+        }
+        if constexpr (decltype(with_tr)::value && TRJ == 1) {
+          if (kk >= NKK - 2) tf[kk - (NKK - 2)] = trf(ps, kk - (NKK - 2));
         }
         if (kk == 0) {
           mfma_v0(sc, qf[0], kf[0]);
@@ -1641,12 +1648,15 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
     };
     // dV / dK of the previous tile (operands po / dso, fragments tf) || softmax of this tile into pn / dsn;
     // with `ns` the first two k-steps of the next tile's rows are read at the end
-    auto phase_b = [&](auto smax, const bfv8 (&po)[2], const bfv8 (&dso)[2], const bfv8 (&tf)[NB],
+    auto phase_b = [&](auto smax, const bfv8 (&po)[2], const bfv8 (&dso)[2], bfv8 (&tf)[NB],
                        const f32v16& sc, const f32v16& dc, const float (&lq)[16], const float (&nd)[16],
-                       bfv8 (&pn)[2], bfv8 (&dsn)[2], const char* ns, bfv8 (&qa)[2], bfv8 (&da)[2]) {
+                       bfv8 (&pn)[2], bfv8 (&dsn)[2], const char* ns, bfv8 (&qa)[2], bfv8 (&da)[2], const char* ps) {
       constexpr bool SMAX = decltype(smax)::value;  // softmax of a next tile (and its rows) to interleave
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
+        if constexpr (TRJ == 1) {
+          if (i + 2 < NB) tf[i + 2] = trf(ps, i + 2);
+        }
         const int s2 = (i / NDT) & 1, dt = i % NDT;
         if (i < 2 * NDT)
           dvt[dt] = mfma32(tf[i], po[s2], dvt[dt]);
@@ -1698,7 +1708,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
       phase_a(std::true_type{}, smem + sl_0, smem + sl_m1, qa, da, sc, dc, tf, lq, nd);
       if (mcur.need) apply_mask(smem + sl_0, mcur, sc);
       bfv8 pn[2], dsn[2];
-      phase_b(std::true_type{}, pb, db, tf, sc, dc, lq, nd, pn, dsn, smem + sl_p1, qa, da);
+      phase_b(std::true_type{}, pb, db, tf, sc, dc, lq, nd, pn, dsn, smem + sl_p1, qa, da, smem + sl_m1);
       pb[0] = pn[0]; pb[1] = pn[1]; db[0] = dsn[0]; db[1] = dsn[1];
       sl_m2 = sl_m1;
       sl_m1 = sl_0;
@@ -1709,10 +1719,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
     }
     {  // dV / dK of the last tile
 #pragma unroll
-      for (int i = 0; i < NB; ++i) tf[i] = trf(smem + sl_m1, i);
+      for (int i = 0; i < (TRJ == 1 ? 2 : NB); ++i) tf[i] = trf(smem + sl_m1, i);
       f32v16 z = {};
       bfv8 pn[2], dsn[2];
-      phase_b(std::false_type{}, pb, db, tf, z, z, lq, nd, pn, dsn, smem, qa, da);
+      phase_b(std::false_type{}, pb, db, tf, z, z, lq, nd, pn, dsn, smem, qa, da, smem + sl_m1);
     }
     wait_vm<0>();  // no LDS-DMA may outlive the workgroup
   }
@@ -2844,7 +2854,11 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     const int variant = dkdv_variant();
     // dense rows: an 8-slot Q / dO ring (tiles 6 ahead; B4 S8192 backward 7.605 -> 7.544 ms in one process,
     // 7 slots 7.572); packed rows keep 6 (their key blocks often visit only a few tiles)
-    if (variant == 5 && a.rmask && !seg)
+    if (variant == 6 && a.rmask && !seg)
+      fa_bwd_dkdv5_kernel<128, false, 8, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 6 && a.rmask)
+      fa_bwd_dkdv5_kernel<128, false, 6, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 5 && a.rmask && !seg)
       fa_bwd_dkdv5_kernel<128, false, 8><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 5 && a.rmask)
       fa_bwd_dkdv5_kernel<128><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);

@@ -105,9 +105,12 @@ def device_list(devices) -> list[int] | None:
 
 
 def visible_devices_env(ids: list[int], env: dict | None = None) -> dict:
-    """HIP_VISIBLE_DEVICES for ranks pinned to the listed GPUs (Lightning semantics: indices into the
-    GPUs this process sees). Every child sees exactly the listed GPUs, in order, so LOCAL_RANK r runs on
-    ``ids[r]``; an existing HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES selection is composed with it."""
+    """HIP_VISIBLE_DEVICES (and CUDA_VISIBLE_DEVICES, its alias, set to the same list so that no stale
+    parent value disagrees with it whichever one the runtime reads) for ranks pinned to the listed GPUs
+    (Lightning semantics: indices into the GPUs this process sees). Every child sees exactly the listed
+    GPUs, in order, so LOCAL_RANK r runs on ``ids[r]``; an existing HIP_VISIBLE_DEVICES (else
+    CUDA_VISIBLE_DEVICES) selection is composed with it. ROCR_VISIBLE_DEVICES is applied by the ROCm
+    runtime below HIP (HIP's indices count within it), so it is passed through unchanged."""
     env = os.environ if env is None else env
     base = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
     if base:
@@ -119,7 +122,7 @@ def visible_devices_env(ids: list[int], env: dict | None = None) -> dict:
         sel = [str(i) for i in ids]
     if len(set(sel)) != len(sel):
         raise SystemExit(f"trainer.devices {ids} lists a GPU twice")
-    return {"HIP_VISIBLE_DEVICES": ",".join(sel)}
+    return {"HIP_VISIBLE_DEVICES": ",".join(sel), "CUDA_VISIBLE_DEVICES": ",".join(sel)}
 
 
 def _kill_group(p: subprocess.Popen, sig) -> None:

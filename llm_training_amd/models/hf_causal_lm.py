@@ -18,6 +18,7 @@ checkpoint needed); ``hf_path`` loads a LOCAL checkpoint.
 from __future__ import annotations
 
 import logging
+import types
 from typing import Any
 
 import torch
@@ -92,6 +93,28 @@ def _register_hf_attention():
     AttentionMaskInterface.register(HF_ATTN_IMPL, lambda *a, **k: None)  # masking is by segment ids
 
 
+def _hf_auto_config(config):
+    """The transformers config of an ``HFCausalLMConfig``: from ``hf_config`` or a local ``hf_path``."""
+    from transformers import AutoConfig
+
+    if config.hf_config is not None:
+        d = dict(config.hf_config)
+        mt = d.pop("model_type")
+        return AutoConfig.for_model(mt, **d)
+    if config.hf_path:
+        return AutoConfig.from_pretrained(config.hf_path, local_files_only=True,
+                                          trust_remote_code=config.trust_remote_code)
+    raise ValueError("HFCausalLM needs `hf_config` or a local `hf_path`")
+
+
+def _qkv_rows(hf_cfg) -> tuple[int, int, int]:
+    """Output rows of q_proj, k_proj, v_proj."""
+    nq = int(hf_cfg.num_attention_heads)
+    nkv = int(getattr(hf_cfg, "num_key_value_heads", None) or nq)
+    d = getattr(hf_cfg, "head_dim", None) or hf_cfg.hidden_size // nq
+    return nq * d, nkv * d, nkv * d
+
+
 class HFCausalLMConfig(BaseModelConfig):
     hf_config: dict[str, Any] | None = None
     enable_gradient_checkpointing: bool = False
@@ -109,17 +132,9 @@ class HFCausalLM(BaseModel):
         super().__init__(config, pc)
         if self.pc.tp:
             raise NotImplementedError("HFCausalLM does not support tensor parallelism (as in the reference)")
-        from transformers import AutoConfig, AutoModelForCausalLM
+        from transformers import AutoModelForCausalLM
 
-        if config.hf_config is not None:
-            d = dict(config.hf_config)
-            mt = d.pop("model_type")
-            hf_cfg = AutoConfig.for_model(mt, **d)
-        elif config.hf_path:
-            hf_cfg = AutoConfig.from_pretrained(config.hf_path, local_files_only=True,
-                                                trust_remote_code=config.trust_remote_code)
-        else:
-            raise ValueError("HFCausalLM needs `hf_config` or a local `hf_path`")
+        hf_cfg = _hf_auto_config(config)
         impl = config.attn_implementation
         if impl in (None, "flash_attention_2", "flash", "hip", HF_ATTN_IMPL):
             _register_hf_attention()
@@ -223,10 +238,42 @@ class HFCausalLM(BaseModel):
 
     @classmethod
     def convert_state_dict_to_hf(cls, sd, config):
-        return {k[len("hf_model."):]: v for k, v in sd.items() if k.startswith("hf_model.")}
+        """Our names -> transformers keys. Checkpoints name tensors by ``named_parameters()``, so a model built
+        with ``enable_liger_kernel`` stores its fused projections (``self_attn.qkv_weight`` / ``qkv_bias``,
+        ``mlp.gate_up_weight``); they are split back into the per-projection HF keys here (rows
+        [q | k | v] and [gate | up], as ``_fuse_linears`` concatenated them)."""
+        out: dict[str, torch.Tensor] = {}
+        qkv_rows = None
+        for k, v in sd.items():
+            if not k.startswith("hf_model."):
+                continue
+            k = k[len("hf_model."):]
+            if k.endswith(".gate_up_weight"):
+                base, half = k[:-len("gate_up_weight")], v.shape[0] // 2
+                out[base + "gate_proj.weight"], out[base + "up_proj.weight"] = v[:half], v[half:]
+            elif k.endswith((".self_attn.qkv_weight", ".self_attn.qkv_bias")):
+                if qkv_rows is None:
+                    qkv_rows = _qkv_rows(_hf_auto_config(config))
+                base, suffix = k.rsplit(".", 1)
+                kind = "weight" if suffix == "qkv_weight" else "bias"
+                lo = 0
+                for name, n in zip(("q_proj", "k_proj", "v_proj"), qkv_rows):
+                    out[f"{base}.{name}.{kind}"] = v[lo:lo + n]
+                    lo += n
+                if lo != v.shape[0]:
+                    raise ValueError(f"{k}: {v.shape[0]} rows, config gives q/k/v rows {qkv_rows}")
+            else:
+                out[k] = v
+        return out
 
     def hf_config_dict(self) -> dict:
-        return self.hf_model.config.to_dict()
+        hm = self.__dict__.get("_modules", {}).get("hf_model")
+        if hm is not None:
+            return hm.config.to_dict()
+        # an unbuilt instance (convert_to_hf's config probe): from the model config alone
+        d = _hf_auto_config(self.config).to_dict()
+        d.pop("_attn_implementation_autoset", None)
+        return d
 
     def _tp_rule(self, key):
         return "rep", None
@@ -238,6 +285,13 @@ class HFCausalLM(BaseModel):
 _NORM_SKIP = ("Gemma",)
 
 
+def _bind(m: nn.Module, fn) -> None:
+    """Install ``fn(self, ...)`` as ``m``'s forward, bound to ``m``: ``copy.deepcopy`` rebinds a bound method
+    to the copied module (a closure over ``m`` would keep calling the original module's weights, e.g. in
+    DPO's deep-copied reference model)."""
+    m.forward = types.MethodType(fn, m)
+
+
 def _patch_norm(m: nn.Module) -> bool:
     if getattr(m, "weight", None) is None or type(m).__name__.startswith(_NORM_SKIP):
         return False
@@ -245,11 +299,11 @@ def _patch_norm(m: nn.Module) -> bool:
     if eps is None:
         return False
 
-    def forward(hidden_states, _m=m, _eps=float(eps)):
+    def forward(self, hidden_states, _eps=float(eps)):
         from ..ops.fused import rms_norm
-        return rms_norm(hidden_states, _m.weight, _eps)
+        return rms_norm(hidden_states, self.weight, _eps)
 
-    m.forward = forward
+    _bind(m, forward)
     return True
 
 
@@ -367,13 +421,13 @@ def _patch_attention(m: nn.Module) -> bool:
     # window as transformers hands it to the attention function (Mistral / Phi-3: the config's, Qwen2: per layer)
     win = getattr(cfg, "sliding_window", None) if name in ("MistralAttention", "Phi3Attention") else \
         getattr(m, "sliding_window", None)
-    original = type(m).forward.__get__(m)  # still valid: q / k / v read slices of the fused parameter
-
-    def forward(hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None, _m=m,
+    def forward(_m, hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None,
                 **kwargs):
         if (past_key_values is not None or attention_mask is not None or position_embeddings is None
-                or position_embeddings[0].shape[-1] != D):  # (partial rotary: transformers' own path)
-            return original(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+                or position_embeddings[0].shape[-1] != D):  # (partial rotary: transformers' own path; still
+            # valid after the fusion: q / k / v read slices of the fused parameter)
+            return type(_m).forward(_m, hidden_states, position_embeddings, attention_mask, past_key_values,
+                                    **kwargs)
         from ..ops.fused import linear, rope_attention_bm
         B, S = hidden_states.shape[:2]
         if fused_proj:
@@ -387,7 +441,7 @@ def _patch_attention(m: nn.Module) -> bool:
                               dropout_p=float(_m.attention_dropout) if _m.training else 0.0)
         return linear(o.reshape(B, S, nq * D), _m.o_proj.weight, _m.o_proj.bias), None
 
-    m.forward = forward
+    _bind(m, forward)
     return True
 
 
@@ -399,12 +453,12 @@ def _patch_mlp(m: nn.Module) -> bool:
         # one GEMM for gate and up, the SwiGLU kernel on the fused [.., 2I] buffer, then down_proj
         # (Liger's LigerSwiGLUMLP); gate / up weights live in one fused parameter (no per-call concat)
         if _fuse_gate_up(m):
-            def forward(x, _m=m):
+            def forward(_m, x):
                 from ..ops.fused import linear, swiglu
                 c = swiglu(linear(x, _m.gate_up_weight), dy_t_consumer=True)
                 return linear(c, _m.down_proj.weight, _m.down_proj.bias)
         else:  # biased projections: concatenated per call
-            def forward(x, _m=m):
+            def forward(_m, x):
                 from ..ops.fused import swiglu
                 w = torch.cat([_m.gate_proj.weight, _m.up_proj.weight], 0)
                 b = None
@@ -412,13 +466,13 @@ def _patch_mlp(m: nn.Module) -> bool:
                     b = torch.cat([_m.gate_proj.bias, _m.up_proj.bias], 0)
                 return _m.down_proj(swiglu(torch.nn.functional.linear(x, w, b)))
     elif hasattr(m, "gate_up_proj") and hasattr(m, "down_proj"):  # Phi-3: fused [gate | up] projection
-        def forward(x, _m=m):
+        def forward(_m, x):
             from ..ops.fused import linear, swiglu
             gu = linear(x, _m.gate_up_proj.weight, _m.gate_up_proj.bias)
             return linear(swiglu(gu, dy_t_consumer=True), _m.down_proj.weight, _m.down_proj.bias)
     else:
         return False
-    m.forward = forward
+    _bind(m, forward)
     return True
 
 
@@ -436,8 +490,8 @@ def _patch_decoder_layer(m: nn.Module) -> bool:
     if eps is None or getattr(norm, "weight", None) is None or type(norm).__name__.startswith(_NORM_SKIP):
         return False
 
-    def forward(hidden_states, attention_mask=None, position_ids=None, past_key_values=None, use_cache=False,
-                position_embeddings=None, _m=m, _eps=float(eps), **kwargs):
+    def forward(_m, hidden_states, attention_mask=None, position_ids=None, past_key_values=None, use_cache=False,
+                position_embeddings=None, _eps=float(eps), **kwargs):
         from ..ops.fused import rms_norm
         a, _ = _m.self_attn(hidden_states=_m.input_layernorm(hidden_states), attention_mask=attention_mask,
                             position_ids=position_ids, past_key_values=past_key_values, use_cache=use_cache,
@@ -445,7 +499,7 @@ def _patch_decoder_layer(m: nn.Module) -> bool:
         h, res = rms_norm(a, _m.post_attention_layernorm.weight, _eps, residual=hidden_states)
         return res + _m.mlp(h)
 
-    m.forward = forward
+    _bind(m, forward)
     return True
 
 

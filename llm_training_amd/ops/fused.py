@@ -92,6 +92,99 @@ _LAYOUT_TUNE = os.environ.get("LLMT_GEMM_LAYOUT_TUNE", "1").strip().lower() not 
 _TR_DGRAD_MIN_M = 16384
 _TR_WGRAD_MIN_M = 4096
 _LAYOUT_CACHE: dict[tuple, str] = {}
+# Where each cached choice came from, and how every rank ends up with the same one:
+#  * "table": the shipped shape-keyed table (tuning/gemm_layouts_gfx950.json, measured on MI355X by timed
+#    runs of the BASELINE workloads): no timing at all, the same choice on every rank and every box;
+#  * "timed": measured on this rank's first sight of the problem (shapes the table does not list);
+#  * "rank0": adopted from rank 0 by agree_layouts(), which the ZeRO engine calls once after its first
+#    optimizer step, so every rank runs rank 0's algorithms from the second step on (a rank whose
+#    timings were disturbed by its own collectives cannot pick a different, slower layout);
+#  * "static": the rule below (LLMT_DETERMINISTIC=1, LLMT_GEMM_LAYOUT_TUNE=0, graph capture).
+# LLMT_GEMM_LAYOUTS=table (default) | timed (ignore the table) | static.
+_LAYOUT_SOURCE: dict[tuple, str] = {}
+_LAYOUT_MODE = os.environ.get("LLMT_GEMM_LAYOUTS", "table").strip().lower()
+_LAYOUT_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
+                                  "gemm_layouts_gfx950.json")
+_LAYOUT_TABLE: list = [None]
+_AGREED: dict[str, str] = {}  # rank 0's choices for problems this rank has not met yet
+
+
+def layout_key_str(key: tuple) -> str:
+    return "|".join(str(x).replace("torch.", "") for x in key)
+
+
+def _layout_table() -> dict:
+    if _LAYOUT_TABLE[0] is None:
+        tbl = {}
+        if _LAYOUT_MODE == "table" and os.path.exists(_LAYOUT_TABLE_PATH):
+            import json
+            with open(_LAYOUT_TABLE_PATH) as f:
+                tbl = json.load(f).get("layouts", {})
+        _LAYOUT_TABLE[0] = tbl
+    return _LAYOUT_TABLE[0]
+
+
+def _time_variants(variants: dict) -> dict:
+    """Milliseconds per call of each variant on the current stream (host-synchronising)."""
+    for fn in variants.values():
+        fn()  # warm-up (and hipBLASLt's own solution choice for the problem)
+    # two interleaved rounds of 2 runs per variant, the faster round kept: a clock or power swing during
+    # one variant's window cannot decide the choice on its own
+    times = {name: float("inf") for name in variants}
+    for _ in range(2):
+        for name, fn in variants.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(2):
+                fn()
+            e1.record()
+            e1.synchronize()
+            times[name] = min(times[name], e0.elapsed_time(e1) / 2)
+    return times
+
+
+def agree_layouts(group=None) -> int:
+    """Make every rank use rank 0's GEMM layout choices: one ``broadcast_object_list`` of rank 0's table
+    (called by the engine after its first optimizer step, a point every rank reaches in the same order);
+    choices this rank made differently are replaced, problems it has not met yet take rank 0's choice on
+    first sight. Returns the number of local choices that changed."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) <= 1:
+        return 0
+    obj = [{layout_key_str(k): v for k, v in _LAYOUT_CACHE.items()} if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    theirs = obj[0] or {}
+    changed = 0
+    for k in list(_LAYOUT_CACHE):
+        c = theirs.get(layout_key_str(k))
+        if c is not None and c != _LAYOUT_CACHE[k]:
+            _LAYOUT_CACHE[k] = c
+            changed += 1
+        if c is not None and _LAYOUT_SOURCE.get(k) == "timed" and dist.get_rank() != 0:
+            _LAYOUT_SOURCE[k] = "rank0"
+    _AGREED.update(theirs)
+    if changed:
+        log.info("GEMM layouts: %d choice(s) replaced by rank 0's", changed)
+    return changed
+
+
+def layout_summary() -> dict:
+    """{source: how the cached choices were made, n, hash} for run records (bench.py's JSON line)."""
+    import hashlib
+    from collections import Counter
+    items = sorted((layout_key_str(k), v) for k, v in _LAYOUT_CACHE.items())
+    srcs = Counter(_LAYOUT_SOURCE.get(k, "timed") for k in _LAYOUT_CACHE)
+    src = next(iter(srcs)) if len(srcs) == 1 else ("+".join(sorted(srcs)) if srcs else "static")
+    h = hashlib.sha256(repr(items).encode()).hexdigest()[:16]
+    return {"source": src, "n": len(items), "hash": h, "mode": _LAYOUT_MODE, "sources": dict(srcs)}
+
+
+def dump_layouts(path: str) -> None:
+    """Write the choices of this process as a table in the shipped format (tuning/gemm_layouts_gfx950.json)."""
+    import json
+    with open(path, "w") as f:
+        json.dump({"layouts": {layout_key_str(k): v for k, v in sorted(_LAYOUT_CACHE.items(), key=lambda kv:
+                                                                      layout_key_str(kv[0]))}}, f, indent=1)
 
 
 # largest weight-gradient output (elements) offered the split-K candidates (fp32 slabs: 8 bytes / element)
@@ -115,31 +208,25 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
 
 
 def _layout(key: tuple, variants: dict, default: str, can_time: bool) -> str:
-    """Cached layout for ``key``; on first sight (and when the call may overwrite its output) every
-    variant in ``variants`` (name -> zero-argument launcher producing the same result) is timed on the
-    current stream and the fastest is kept. Otherwise ``default``."""
+    """Cached layout for ``key``: the shipped table's choice, rank 0's (after :func:`agree_layouts`), or, on
+    first sight (and when the call may overwrite its output), the fastest of ``variants`` (name ->
+    zero-argument launcher producing the same result) timed on the current stream. Otherwise ``default``."""
     hit = _LAYOUT_CACHE.get(key)
     if hit is not None:
         return hit
-    if not (can_time and _LAYOUT_TUNE and len(variants) > 1) or os.environ.get("LLMT_DETERMINISTIC") == "1" \
-            or torch.cuda.is_current_stream_capturing():
+    det = os.environ.get("LLMT_DETERMINISTIC") == "1" or _LAYOUT_MODE == "static"
+    if not det:
+        ks = layout_key_str(key)
+        for src, tbl in (("rank0", _AGREED), ("table", _layout_table())):
+            c = tbl.get(ks)
+            if c in variants:
+                _LAYOUT_CACHE[key], _LAYOUT_SOURCE[key] = c, src
+                return c
+    if not (can_time and _LAYOUT_TUNE and len(variants) > 1) or det or torch.cuda.is_current_stream_capturing():
         return default
-    for fn in variants.values():
-        fn()  # warm-up (and hipBLASLt's own solution choice for the problem)
-    # two interleaved rounds of 2 runs per variant, the faster round kept: a clock or power swing during
-    # one variant's window cannot decide the choice on its own
-    times = {name: float("inf") for name in variants}
-    for _ in range(2):
-        for name, fn in variants.items():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(2):
-                fn()
-            e1.record()
-            e1.synchronize()
-            times[name] = min(times[name], e0.elapsed_time(e1) / 2)
+    times = _time_variants(variants)
     best = min(times, key=times.get)
-    _LAYOUT_CACHE[key] = best
+    _LAYOUT_CACHE[key], _LAYOUT_SOURCE[key] = best, "timed"
     log.debug("GEMM layout %s -> %s (%s)", key, best, ", ".join(f"{k} {v:.3f}" for k, v in sorted(times.items(),
                                                                                          key=lambda kv: kv[1])))
     return best

@@ -6,6 +6,7 @@ PyTorch. CPU tensors use the torch reference ops in :mod:`llm_training_amd.ops.r
 """
 from __future__ import annotations
 
+import logging
 import os
 import threading
 from pathlib import Path
@@ -50,14 +51,36 @@ def lib():
     return torch.ops.llmt
 
 
+# GPU dtypes that ran the torch reference ops instead of the HIP kernels in this process (-> op count):
+# read by the trainer / bench into their run metadata, warned about once per dtype
+REFERENCE_ON_GPU: dict[str, int] = {}
+
+
+def compute_path(device_type: str, dtype: torch.dtype) -> str:
+    """Which implementation the fused ops (attention, norms, SwiGLU, RoPE, CE, AdamW) of a model whose
+    activations have ``dtype`` run on ``device_type``: ``"hip"`` (the gfx950 kernels) or
+    ``"torch-reference"`` (the kernels are bf16 MFMA kernels: fp32 / fp16 GPU runs and CPU runs use the
+    torch ops of :mod:`llm_training_amd.ops.reference`)."""
+    return "hip" if device_type == "cuda" and dtype == torch.bfloat16 else "torch-reference"
+
+
 def use_native(t: torch.Tensor) -> bool:
     """bf16 GPU tensors always go to the HIP kernels (no silent fallback: a missing library raises).
 
-    The kernels are bf16 MFMA kernels; fp32 GPU tensors (``precision: 32-true``) and CPU tensors run
-    the torch reference ops of :mod:`llm_training_amd.ops.reference`."""
+    The kernels are bf16 MFMA kernels; fp32 / fp16 GPU tensors (``precision: 32-true`` / ``16-*``) and
+    CPU tensors run the torch reference ops of :mod:`llm_training_amd.ops.reference`. On the GPU that
+    switch is announced once per dtype (a warning) and counted in ``REFERENCE_ON_GPU``."""
     if t.device.type == "cuda":
         lib()
-        return t.dtype == torch.bfloat16
+        if t.dtype == torch.bfloat16:
+            return True
+        key = str(t.dtype).replace("torch.", "")
+        if key not in REFERENCE_ON_GPU:
+            logging.getLogger("llm_training").warning(
+                "%s GPU tensors run the torch reference ops, not the HIP kernels (bf16 only): expect a much "
+                "slower step; use precision bf16-true / bf16-mixed for the kernel path", key)
+        REFERENCE_ON_GPU[key] = REFERENCE_ON_GPU.get(key, 0) + 1
+        return False
     return False
 
 

@@ -147,7 +147,13 @@ class RopeTables:
 
     def __post_init__(self):
         self._cache: dict[str, tuple[torch.Tensor, torch.Tensor, int]] = {}
-        self._dyn_cached = self.max_position_embeddings  # the reference's max_seq_len_cached (dynamic NTK)
+        # dynamic NTK state, as the reference's rotary module keeps it (llama_model.py:312-341, 367-371): its
+        # constructor builds the cache for max_position_embeddings rounded up to a multiple of 4096, so both the
+        # initial and the "original" (reset) frequencies are NTK-scaled for that length whenever
+        # max_position_embeddings is not a multiple of 4096 (e.g. 2048 -> 4096)
+        self._dyn_orig = reference_rope_seq_len(self.max_position_embeddings)
+        self._dyn_cached = self._dyn_orig  # the reference's max_seq_len_cached
+        self._dyn_freq = self._dyn_orig  # the length the current frequencies were computed for
 
     @property
     def dynamic(self) -> bool:
@@ -167,11 +173,11 @@ class RopeTables:
             orig = self.max_position_embeddings
             if not (orig <= L <= self._dyn_cached):
                 R = reference_rope_seq_len(L)
-                if R > self._dyn_cached:
-                    self._dyn_cached = R  # growth
-                if R < orig and self._dyn_cached > orig:
-                    self._dyn_cached = orig  # reset to the original frequencies
-            ntk = self._dyn_cached
+                if R > self._dyn_cached:  # growth
+                    self._dyn_cached = self._dyn_freq = R
+                if R < orig and self._dyn_cached > orig:  # reset to the original frequencies
+                    self._dyn_cached, self._dyn_freq = orig, self._dyn_orig
+            ntk = self._dyn_freq
         key = (str(device), ntk)
         hit = self._cache.get(key)
         if hit is not None and hit[2] >= min_positions:

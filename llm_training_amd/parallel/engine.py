@@ -849,6 +849,12 @@ class DataParallelEngine:
     @torch.no_grad()
     def step(self, lr: float):
         self.step_count += 1
+        if self.step_count == 1 and self.pc.world_size > 1:
+            # every GEMM problem of the step has met its layout choice by now: from the next step on all
+            # ranks run rank 0's choices (ops/fused.py agree_layouts), so no rank keeps a layout its own
+            # noisy first-sight timing picked and the step does not run at the slowest rank's pace
+            from ..ops.fused import agree_layouts
+            agree_layouts()
         if self.offload:
             self._step_units_offload(lr)
             return

@@ -22,12 +22,17 @@ padding never enters the softmax normaliser and its gradient rows stay zero.
 """
 from __future__ import annotations
 
+import logging
+import os
+
 import torch
 import torch.distributed as dist
 from torch.autograd import Function
 
 from ..ops.fused import _apply_weight_grad, dw_accumulator, dw_add_chunk, mm_nn, mm_nt, weight_t
 from ..ops.native import lib, use_native
+
+log = logging.getLogger("llm_training")
 
 
 def _combine(stats: torch.Tensor, group) -> torch.Tensor:
@@ -132,7 +137,12 @@ class _VPLogps(Function):
         native = use_native(h)
         N = h.shape[0]
         w = w_full[:n_valid]
-        keep = ctx.needs_input_grad[0] and N * n_valid * h.element_size() <= keep_budget
+        need = N * n_valid * h.element_size()
+        keep = ctx.needs_input_grad[0] and need <= _keep_budget(keep_budget, h)
+        if ctx.needs_input_grad[0] and not keep and not _RECOMPUTE_LOGGED[0]:
+            _RECOMPUTE_LOGGED[0] = True
+            log.info("vocab-parallel log-probs: %.2f GiB of local logits exceed the keep budget; the backward "
+                     "recomputes them (LLMT_LOGPS_KEEP_GIB)", need / 2 ** 30)
         stats = torch.zeros(3, N, device=h.device, dtype=torch.float32)
         kept = []
         for s0 in range(0, N, chunk):
@@ -195,8 +205,23 @@ def vocab_parallel_cross_entropy(h, w_local, labels, vocab_start, group, ignore_
                             chunk_size, _n_valid(w_local, vocab_start, vocab_size))
 
 
-# local logits kept from the log-prob forward for its backward (no lm_head recompute) up to this many bytes
-LOGPS_KEEP_BYTES = [8 << 30]
+# Local logits kept from the log-prob forward for its backward (no lm_head recompute) up to this many bytes.
+# None = automatic: at most 8 GiB and at most a quarter of the device memory free when the forward runs, so
+# a configuration that fits with the recompute path does not run out of HBM because of the kept logits.
+# LLMT_LOGPS_KEEP_GIB=<float> pins the budget (0: always recompute).
+_KEEP_ENV = os.environ.get("LLMT_LOGPS_KEEP_GIB", "auto").strip().lower()
+LOGPS_KEEP_BYTES = [None if _KEEP_ENV in ("", "auto") else int(float(_KEEP_ENV) * 2 ** 30)]
+_RECOMPUTE_LOGGED = [False]
+
+
+def _keep_budget(budget, h: torch.Tensor) -> int:
+    if budget is not None:
+        return int(budget)
+    cap = 8 << 30
+    if h.is_cuda:
+        free, _ = torch.cuda.mem_get_info(h.device)
+        cap = min(cap, free // 4)
+    return cap
 
 
 def vocab_parallel_token_logps(h, w_local, labels, vocab_start, group, ignore_index=-100, chunk_size=8192,

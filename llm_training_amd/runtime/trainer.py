@@ -277,6 +277,7 @@ class Trainer:
         rank, local, world, device = init_distributed(st.process_group_backend, st.timeout_minutes,
                                                       device_type="cpu" if self.accelerator == "cpu" else None)
         self.device = device
+        self.run_meta = self.compute_path_meta(device)
         if self.gemm_tuning is not None:
             from .gemm_tuning import setup_gemm_tuning
             setup_gemm_tuning(self.gemm_tuning)
@@ -335,10 +336,27 @@ class Trainer:
             load_checkpoint(self, ckpt_path)
         for lg in self.loggers:
             _call(lg, "setup", self)
+            if self.pc.rank == 0:
+                _call(lg, "log_hyperparams", {"run_meta": dict(self.run_meta)})
         self.meter = ThroughputMeter(self.pc.dp_size, device=device)
         self.profiler = StepProfiler(out_dir=self.log_dir, rank=self.pc.rank)
         self.watchdog = StallWatchdog(path=os.path.join(self.log_dir, f"stall_rank{self.pc.rank}.txt"))
         self.collectives = collective_debug.maybe_enable_from_env()
+
+    def compute_path_meta(self, device: torch.device) -> dict:
+        """Run metadata on the kernel path this precision takes on ``device``. The HIP kernels are bf16 MFMA
+        kernels: ``precision: 32-true`` / ``16-*`` on a GPU runs the torch reference ops for every fused op
+        (reference FSDP2Precision runs fp32 / fp16 through the same Liger / flash-attn kernels instead,
+        fsdp2_precision.py:19-21,92-96), which is announced here once rather than left silent."""
+        from ..ops.native import compute_path
+        path = compute_path(device.type, self.param_dtype)
+        meta = {"device": device.type, "precision": str(self.precision), "compute_kernels": path}
+        if device.type == "cuda" and path != "hip":
+            logger.warning("precision %r on the GPU: the fused ops (attention, RMSNorm, SwiGLU, RoPE, loss, "
+                           "AdamW) run the torch reference ops, not the bf16 HIP kernels (run_meta "
+                           "compute_kernels=%s); use bf16-true or bf16-mixed for the kernel path",
+                           self.precision, path)
+        return meta
 
     @staticmethod
     def _prepare_data(datamodule, rank: int, local_rank: int):

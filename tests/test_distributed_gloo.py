@@ -598,3 +598,60 @@ def test_hf_model_zero2_gradient_hooks_match_single_process(liger):
             assert torch.allclose(out[r]["params"][k], v, atol=5e-5, rtol=1e-4), (r, k)
     avg = [(a + b) / 2 for a, b in zip(out[0]["losses"], out[1]["losses"])]
     assert max(abs(a - b) for a, b in zip(avg, ref_losses)) < 1e-5
+
+
+def _agree_worker(rank, world):
+    """Each rank 'times' the same GEMM problems with perturbed timings (rank 1's favour other layouts); after the engine's first optimizer step every rank holds rank 0's choices,
+    and a problem met only later takes rank 0's choice without timing."""
+    import torch.distributed as dist
+
+    import llm_training_amd.ops.fused as F
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    F._LAYOUT_CACHE.clear()
+    F._LAYOUT_SOURCE.clear()
+    F._AGREED.clear()
+    F._LAYOUT_TABLE[0] = {}
+
+    def fake_times(variants):
+        names = sorted(variants)
+        # rank 0 prefers the first name, rank 1 the last (a disturbed timing)
+        return {n: float(i if rank == 0 else -i) for i, n in enumerate(names)}
+    F._time_variants = fake_times
+    variants = {n: (lambda: None) for n in ("nn", "nt", "tn", "tt")}
+    old = os.environ.pop("LLMT_DETERMINISTIC", None)
+    torch_cuda_cap = torch.cuda.is_current_stream_capturing
+    torch.cuda.is_current_stream_capturing = lambda: False
+    try:
+        keys = [("wgrad", 32768, n, 4096, 4096, n, torch.bfloat16, True) for n in (6144, 4096, 28672)]
+        first = [F._layout(k, variants, "nn", True) for k in keys]
+        F._layout(("dgrad", 32768, 4096, 14336, 4096, 14336, False), variants, "tn", True)
+        assert first == (["nn"] * 3 if rank == 0 else ["tt"] * 3)
+        pc = ParallelContext.create(world, 1, torch.device("cpu"))
+        m = Llama(tiny_llama_cfg(), pc, dtype=torch.float32)
+        m.init_weights(0)
+        _train(m, pc, 2, _batches(m.config.vocab_size, 1, seed=rank))  # step 1 -> agree_layouts()
+        tables = [None] * world
+        dist.all_gather_object(tables, {F.layout_key_str(k): v for k, v in F._LAYOUT_CACHE.items()})
+        assert all(t[F.layout_key_str(k)] == "nn" for t in tables for k in keys), tables
+        summ = F.layout_summary()
+        assert summ["source"] == ("timed" if rank == 0 else "rank0")
+        # a problem rank 0 met first is taken from rank 0 on this rank's first sight, without timing
+        k2 = ("wgrad", 8192, 1024, 1024, 1024, 1024, torch.float32, True)
+        if rank == 0:
+            F._LAYOUT_CACHE[k2] = "tn"
+        F.agree_layouts()
+        F._time_variants = None  # timing would now raise
+        assert F._layout(k2, variants, "nn", True) == "tn"
+        hashes = [None] * world
+        dist.all_gather_object(hashes, F.layout_summary()["hash"])
+        return hashes
+    finally:
+        torch.cuda.is_current_stream_capturing = torch_cuda_cap
+        if old is not None:
+            os.environ["LLMT_DETERMINISTIC"] = old
+
+
+def test_gemm_layouts_agree_across_ranks():
+    out = run_gloo(_agree_worker, world=2)
+    assert out[0] == out[1] and out[0][0] == out[0][1]  # the same table (hash) on both ranks

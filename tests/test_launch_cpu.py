@@ -172,7 +172,12 @@ def test_device_list_pins_ranks_to_the_listed_gpus(tmp_path, monkeypatch):
     envs = [json.load(open(tmp_path / f"env{r}")) for r in range(2)]
     assert [e["HIP_VISIBLE_DEVICES"] for e in envs] == ["2,3", "2,3"]
     assert [e["LOCAL_RANK"] for e in envs] == ["0", "1"]
-    assert visible_devices_env([1, 3], {"HIP_VISIBLE_DEVICES": "4,5,6,7"}) == {"HIP_VISIBLE_DEVICES": "5,7"}
+    assert [e["CUDA_VISIBLE_DEVICES"] for e in envs] == ["2,3", "2,3"]
+    assert visible_devices_env([1, 3], {"HIP_VISIBLE_DEVICES": "4,5,6,7"}) == {"HIP_VISIBLE_DEVICES": "5,7",
+                                                                             "CUDA_VISIBLE_DEVICES": "5,7"}
+    # a parent selecting through CUDA_VISIBLE_DEVICES only: composed, and the child's alias agrees
+    assert visible_devices_env([0, 2], {"CUDA_VISIBLE_DEVICES": "3,4,6"}) == {"HIP_VISIBLE_DEVICES": "3,6",
+                                                                            "CUDA_VISIBLE_DEVICES": "3,6"}
     with pytest.raises(SystemExit):
         visible_devices_env([0, 0], {})
     with pytest.raises(SystemExit):

@@ -458,3 +458,56 @@ def test_dynamic_ntk_length_follows_the_reference_rule():
     pos = torch.cat([torch.arange(100), torch.arange(300)]).unsqueeze(0)
     m._runtime(None, pos, None, torch.device("cpu"), 400, 1)
     assert m.rope._dyn_cached == 4096
+
+
+def test_dynamic_ntk_initial_state_when_context_is_not_a_multiple_of_4096():
+    """The reference builds its first rotary cache for max_position_embeddings rounded up to a multiple of
+    4096 (llama_model.py:312, 320-324, 367-371): with an original context of 2048 the initial and the reset
+    ("original") frequencies are NTK-scaled for 4096, also for batches shorter than 4096. The reference keeps
+    no fixture of this case (parity unpinned beyond the rule itself)."""
+    from llm_training_amd.ops.rope_utils import RopeTables, compute_rope_tables
+    sc = {"rope_type": "dynamic", "factor": 2.0}
+    rt = RopeTables(16, 10000.0, sc, 2048)
+    # (the reference's reset compares the ROUNDED length with the original context, so with 2048 it never
+    # resets: 1000 -> 4096 >= 2048 keeps the grown 8192 frequencies)
+    seq = [(1000, 4096), (3000, 4096), (5000, 8192), (4500, 8192), (1000, 8192), (2048, 8192)]
+    for L, want in seq:
+        cos, _ = rt.get(None, L, ntk_positions=L)
+        ref_cos, _ = compute_rope_tables(16, cos.shape[0], 10000.0, sc, 2048, seq_len=want)
+        assert torch.equal(cos, ref_cos), (L, want)
+    plain, _ = compute_rope_tables(16, 8192, 10000.0, None, 2048)
+    first, _ = RopeTables(16, 10000.0, sc, 2048).get(None, 100)
+    assert not torch.allclose(first, plain)  # scaled from the start, unlike a 2048-length table
+
+
+@pytest.mark.parametrize("model_type", ["llama", "phi3"])
+def test_hf_fused_patch_survives_deepcopy(model_type):
+    """The patched forwards are bound methods, so ``copy.deepcopy`` (DPO's reference model when none is given)
+    rebinds them to the copy: perturbing the copy's weights changes only the copy's output."""
+    import copy
+
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 2,
+          "hidden_size": 64, "intermediate_size": 96, "vocab_size": 100, "max_position_embeddings": 64}
+    if model_type == "phi3":
+        hc.update(pad_token_id=0, bos_token_id=1, eos_token_id=2)
+    m = HFCausalLM(HFCausalLMConfig(hf_config=hc, enable_liger_kernel=True, attn_implementation="flash"))
+    m.init_weights(0)
+    assert any(n.endswith("DecoderLayer") for n in m.fused_modules) or model_type == "phi3"
+    ids = torch.randint(0, 100, (2, 12), generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        h0 = m.hidden_states(ids).clone()
+        c = copy.deepcopy(m)
+        for p in c.parameters():
+            p.mul_(1.5)
+        hc_ = c.hidden_states(ids)
+        h1 = m.hidden_states(ids)
+    assert torch.equal(h0, h1)  # the original is untouched by the copy's weights
+    assert not torch.allclose(hc_, h0, atol=1e-3)
+    fresh = copy.deepcopy(m)
+    with torch.no_grad():
+        assert torch.equal(fresh.hidden_states(ids), h0)  # and an unmodified copy computes the same thing
+    for mod in c.modules():
+        f = mod.__dict__.get("forward")
+        if f is not None:
+            assert f.__self__ is mod

@@ -323,3 +323,67 @@ def test_convert_to_hf_roundtrip_phi3_longrope(tmp_path):
             a = lm.model(input_ids=ids).logits
             b = hf(input_ids=ids).logits
         assert torch.allclose(a, b, atol=2e-4), (S, (a - b).abs().max())
+
+
+@pytest.mark.parametrize("model_type", ["llama", "qwen2"])
+def test_convert_to_hf_splits_fused_hf_projections(tmp_path, model_type):
+    """HFCausalLM with ``enable_liger_kernel`` trains with fused q/k/v (Qwen2: and their biases) and gate/up
+    parameters, and checkpoints name them as such; the HF export splits them back into the per-projection
+    keys, so transformers loads every projection (none randomly initialised) and reproduces the logits."""
+    from transformers import AutoModelForCausalLM
+
+    from llm_training_amd.tools.convert_to_hf import convert
+    hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 2,
+          "hidden_size": 64, "intermediate_size": 96, "vocab_size": 96, "max_position_embeddings": 64}
+    lm = CLM({"model": {"model_class": "llm_training.models.HFCausalLM",
+                        "model_config": {"hf_config": hc, "enable_liger_kernel": True,
+                                         "attn_implementation": "flash"}},
+              "optim": {"optimizer_class": "torch.optim.AdamW", "optimizer_kwargs": {"lr": 5e-3}}})
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=2, log_every_n_steps=1, seed=1,
+                default_root_dir=str(tmp_path))
+    t.fit(lm, _dm())
+    names = {n for n, _ in lm.model.named_parameters()}
+    assert any(n.endswith("mlp.gate_up_weight") for n in names), sorted(names)[:8]
+    ck = tmp_path / "ck"
+    t.save_checkpoint(str(ck))
+    out = convert(str(ck), str(tmp_path / "hf"), dtype="float32")
+    from safetensors.torch import load_file
+    keys = set(load_file(os.path.join(out, "model.safetensors")))
+    assert not any("qkv_" in k or "gate_up_weight" in k for k in keys), sorted(keys)
+    for proj in ("self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.v_proj.weight",
+                 "mlp.gate_proj.weight", "mlp.up_proj.weight"):
+        assert f"model.layers.1.{proj}" in keys, proj
+    assert ("model.layers.0.self_attn.k_proj.bias" in keys) == (model_type == "qwen2")
+    hf = AutoModelForCausalLM.from_pretrained(out, local_files_only=True)
+    hf.eval()
+    lm.model.eval()
+    sd = lm.model.state_dict()  # transformers key view of the fused parameters
+    for k, v in hf.state_dict().items():
+        if "hf_model." + k in sd:
+            assert torch.equal(v, sd["hf_model." + k].float()), k
+    ids = torch.randint(0, 96, (2, 16))
+    with torch.no_grad():
+        a = lm.model(input_ids=ids).logits
+        b = hf(input_ids=ids).logits
+    assert torch.allclose(a, b, atol=1e-4), (a - b).abs().max()
+
+
+@pytest.mark.parametrize("model_type", ["llama", "qwen2"])
+def test_hf_fused_qkv_names_convert_to_hf_keys(model_type):
+    """The fused q/k/v parameters (built when the attention runs on the flash path) of a parameter-named
+    state dict (what checkpoints hold) convert to exactly the unpatched model's transformers state dict."""
+    from llm_training_amd.models.hf_causal_lm import HFCausalLM, HFCausalLMConfig
+    hc = {"model_type": model_type, "num_hidden_layers": 2, "num_attention_heads": 4, "num_key_value_heads": 2,
+          "hidden_size": 256, "intermediate_size": 96, "vocab_size": 96, "max_position_embeddings": 64}
+    cfg = HFCausalLMConfig(hf_config=hc, enable_liger_kernel=True, attn_implementation="flash")
+    m = HFCausalLM(cfg)
+    m.init_weights(0)
+    named = {n: p.detach() for n, p in m.named_parameters()}
+    assert any(n.endswith("self_attn.qkv_weight") for n in named)
+    assert any(n.endswith("self_attn.qkv_bias") for n in named) == (model_type == "qwen2")
+    hf = HFCausalLM.convert_state_dict_to_hf(named, cfg)
+    want = {k[len("hf_model."):]: v for k, v in m.state_dict().items()}
+    want.pop("lm_head.weight", None) if "lm_head.weight" not in hf else None
+    assert set(hf) == set(want), sorted(set(hf) ^ set(want))
+    for k in want:
+        assert torch.equal(hf[k], want[k]), k

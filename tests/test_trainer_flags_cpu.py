@@ -227,3 +227,56 @@ def test_use_distributed_sampler_false_gives_every_rank_the_whole_set(tmp_path):
                 default_root_dir=str(tmp_path))
     t.fit(_lm(), _dm())
     assert t._dp() == (0, 1)
+
+
+@pytest.mark.parametrize("precision,path", [("32-true", "torch-reference"), ("16-mixed", "torch-reference"),
+                                            ("bf16-true", "hip"), ("bf16-mixed", "hip")])
+def test_gpu_precision_kernel_path_is_announced(precision, path):
+    """The HIP kernels are bf16-only: a GPU run at 32-true / 16-* takes the torch reference ops. The trainer
+    says so (a warning) and records it in its run metadata instead of switching paths silently; bf16
+    precisions record the kernel path without a warning (device mocked: no GPU needed)."""
+    import logging
+
+    class _Keep(logging.Handler):
+        def __init__(self):
+            super().__init__(logging.WARNING)
+            self.msgs = []
+
+        def emit(self, record):
+            self.msgs.append(record.getMessage())
+    h = _Keep()
+    lg = logging.getLogger("llm_training")  # the package logger (it does not propagate to the root)
+    lg.addHandler(h)
+    try:
+        t = Trainer(precision=precision)
+        meta = t.compute_path_meta(torch.device("cuda", 0))
+        assert meta["compute_kernels"] == path and meta["device"] == "cuda"
+        assert any("torch reference ops" in m for m in h.msgs) == (path != "hip")
+        h.msgs.clear()
+        assert t.compute_path_meta(torch.device("cpu"))["compute_kernels"] == "torch-reference"
+        assert not h.msgs  # the CPU reference path is the expected one there
+    finally:
+        lg.removeHandler(h)
+
+
+def test_run_meta_reaches_the_logger(tmp_path):
+    import json
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=1, seed=1, logger=JSONLLogger(str(tmp_path), "r"),
+                enable_checkpointing=False)
+    t.fit(_lm(), _dm())
+    hp = json.load(open(tmp_path / "r" / "hparams.json"))
+    assert hp["run_meta"] == {"device": "cpu", "precision": "32-true", "compute_kernels": "torch-reference"}
+
+
+def test_use_native_counts_reference_ops_on_gpu(monkeypatch):
+    """use_native on a non-bf16 GPU tensor warns once per dtype and counts the calls (mocked device)."""
+    from llm_training_amd.ops import native
+    monkeypatch.setattr(native, "lib", lambda: None)
+    monkeypatch.setattr(native, "REFERENCE_ON_GPU", {})
+
+    class _T:
+        def __init__(self, dtype):
+            self.device, self.dtype = torch.device("cuda", 0), dtype
+    assert native.use_native(_T(torch.bfloat16))
+    assert not native.use_native(_T(torch.float32)) and not native.use_native(_T(torch.float32))
+    assert native.REFERENCE_ON_GPU == {"float32": 2}
