@@ -386,6 +386,9 @@ def main():
     prev[0] = None
     meter = {}
     engine.wait_meter = meter
+    from llm_training_amd.parallel import tensor_parallel as tpl
+    if pc.tp_size > 1:  # compute-stream stalls on the staged TP collectives (tensor_parallel._tp_wait)
+        tpl.TP_WAIT_METER = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = run(args.warmup + i, f"timed step {i}", args.setup_timeout if args.warmup == 0 and i == 0
@@ -400,6 +403,11 @@ def main():
     waits = engine.wait_meter_ms(meter)
     rccl["exposed_comm_ms_per_step"] = round(waits.get("comm", 0.0) / args.steps, 3)
     rccl["exposed_optimizer_wait_ms_per_step"] = round(waits.get("opt", 0.0) / args.steps, 3)
+    if tpl.TP_WAIT_METER is not None:
+        rccl["exposed_tp_comm_ms_per_step"] = round(
+            sum(a.elapsed_time(b) for a, b in tpl.TP_WAIT_METER) / args.steps, 3)
+        rccl["tp_stages"] = int(os.environ.get("LLMT_TP_STAGES", "4"))
+        tpl.TP_WAIT_METER = None
     el = torch.tensor([el_host], device=device, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)

@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <initializer_list>
 #include <type_traits>
+#include <utility>
 
 namespace llmt {
 
@@ -2048,6 +2049,487 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   }
 }
 
+// ============================================================================ forward, D = 128, v4
+// One wave per SIMD with 64 query rows per wave (two 32-row halves that share every K and V^T fragment
+// read, so a tile's LDS reads feed twice the MFMAs of fa_fwd3_kernel), 256-row blocks of 4 waves, 64-key
+// K/V tiles by LDS-DMA into a 4-slot ring (one barrier per tile, tile t+2 in flight under tile t).
+// Register files by role, allocated by hand (cdna guide §B, the 4-wave one-wave-per-SIMD structure): the
+// accumulator file holds O^T (a[0:127]), Q (a[128:191]) and the current K tile (a[192:255]) under literal
+// register names in the asm MFMAs and asm LDS reads (hipcc's allocator moved "a"-constrained copies of
+// them between registers and spilled when it owned them); the arch VGPRs hold two 64-score sets, bf16 P,
+// the V^T fragments and the softmax state, compiler-allocated. Each tile t is two phases of 32 MFMAs:
+//  * phase A: S^T(t) = K(t) Q^T, while the softmax of tile t-1 finishes (exps of its second key half, row
+//    sums, bf16 P) and the first V^T(t-1) fragments are read;
+//  * phase B: O^T += V^T(t-1) P^T(t-1), while the softmax of tile t starts (mask on diagonal / window / end
+//    tiles, row max, defer-max decision, exps of the first key half), the rest of V^T(t-1) is read just in
+//    time and K(t+1) is read into the accumulator file.
+// A rescale (a row max growing past kThr) multiplies O^T and l after phase B, when every P at the old max
+// (tile t-1) has been added and none at the new one. Dense rows (no segment ids), D = 128, no dropout.
+#define LLMT_ACLOB "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127","a128","a129","a130","a131","a132","a133","a134","a135","a136","a137","a138","a139","a140","a141","a142","a143","a144","a145","a146","a147","a148","a149","a150","a151","a152","a153","a154","a155","a156","a157","a158","a159","a160","a161","a162","a163","a164","a165","a166","a167","a168","a169","a170","a171","a172","a173","a174","a175","a176","a177","a178","a179","a180","a181","a182","a183","a184","a185","a186","a187","a188","a189","a190","a191","a192","a193","a194","a195","a196","a197","a198","a199","a200","a201","a202","a203","a204","a205","a206","a207","a208","a209","a210","a211","a212","a213","a214","a215","a216","a217","a218","a219","a220","a221","a222","a223","a224","a225","a226","a227","a228","a229","a230","a231","a232","a233","a234","a235","a236","a237","a238","a239","a240","a241","a242","a243","a244","a245","a246","a247","a248","a249","a250","a251","a252","a253","a254","a255"
+
+template <int... Is, class F>
+__device__ __forceinline__ void sfor_seq(std::integer_sequence<int, Is...>, F&& f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+// f(std::integral_constant<int, i>) for i = 0 .. N-1: compile-time indices for "i" asm operands
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_seq(std::make_integer_sequence<int, N>{}, f);
+}
+constexpr int fa4_ao(int dt, int qh) { return (dt * 2 + qh) * 16; }  // O^T tile (d tile, query half)
+constexpr int fa4_aq(int qh, int kk) { return 128 + (qh * 8 + kk) * 4; }  // Q fragment (query half, k-step)
+constexpr int fa4_ak(int kh, int kk) { return 192 + (kh * 8 + kk) * 4; }  // K fragment (key half, k-step)
+// phase B of fa_fwd4 exponentiates the first key half's 32 scores in gaps 10 .. 31: one in gaps 10 .. 21, two
+// in gaps 22 .. 31 (score index of the gap's first exp, and how many)
+constexpr int fa4_nexp(int g) { return g < 10 ? 0 : (g < 22 ? 1 : 2); }
+constexpr int fa4_exp0(int g) { return g < 22 ? g - 10 : 12 + 2 * (g - 22); }
+
+// two floats -> packed bf16 pair, issued where it stands (hipcc lowered element-wise bf16 inserts as one
+// block of conversions in front of the first MFMA that reads them)
+__device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
+  uint32_t r;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+// exp2(x) with its row-sum add one instruction behind (the trans-use wait state by placement, see fwd3)
+__device__ __forceinline__ float exp_sum(float x, float& rs) {
+  float e;
+  asm volatile("v_exp_f32 %0, %2\n\ts_nop 0\n\tv_add_f32 %1, %1, %0" : "=&v"(e), "+v"(rs) : "v"(x));
+  return e;
+}
+
+// LDS-DMA of one 64-key K/V tile (no segment ids) for fa_fwd4: this wave's 16 K and 16 V rows, 4 per
+// instruction; the per-lane byte offsets (voffset: range-checked against the descriptor, so rows past the
+// sequence end read zeros) hold the tile's first row. The leading s_nop covers descriptor words written by
+// a VALU just before (VALU write of an SGPR -> VMEM read of it: 5 wait states; hipcc does not look inside
+// the statement).
+__device__ __forceinline__ void dma_tile8(const Rsrc& k, const Rsrc& v, uint32_t lds, int img, const int (&vk)[4],
+                                          const int (&vv)[4]) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %11, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %7, %12, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %11, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %8, %12, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, 0x800\n\ts_nop 0\n\tbuffer_load_dwordx4 %5, %11, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %9, %12, 0 offen lds\n\t"
+      "s_add_u32 m0, %1, 0xc00\n\ts_nop 0\n\tbuffer_load_dwordx4 %6, %11, 0 offen lds\n\t"
+      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %10, %12, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds), "s"(img), "v"(vk[0]), "v"(vk[1]), "v"(vk[2]), "v"(vk[3]), "v"(vv[0]), "v"(vv[1]), "v"(vv[2]),
+        "v"(vv[3]), "s"(k.w), "s"(v.w)
+      : "memory", "scc");
+}
+// x if key offset o is inside the row's range (base + o <= span, unsigned: idx_range), else -inf, in place;
+// VCC only (hipcc's 64-bit compare masks for a whole masked tile ran the kernel out of scalar registers)
+template <int O>
+__device__ __forceinline__ float range_or_ninf(float x, uint32_t base, uint32_t span) {
+  uint32_t t;
+  asm("v_add_u32 %1, %c3, %2\n\tv_cmp_le_u32 vcc, %1, %4\n\tv_cndmask_b32 %0, %5, %0, vcc"
+      : "+v"(x), "=&v"(t)
+      : "v"(base), "i"(O), "v"(span), "v"(-INFINITY)
+      : "vcc");
+  return x;
+}
+// single VALU instructions for the hand-spaced softmax gaps (hipcc would pair or fuse neighbours)
+__device__ __forceinline__ float v_exp1(float x) {
+  float r;
+  asm volatile("v_exp_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ void v_add_ip(float& acc, float x) { asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc) : "v"(x)); }
+__device__ __forceinline__ float v_fma1(float x, float c, float d) {
+  float r;
+  asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(c), "v"(d));
+  return r;
+}
+
+template <int D = 128>
+__global__ __launch_bounds__(256, 1) void fa_fwd4_kernel(AttnArgs a) {
+  static_assert(D == 128, "fa_fwd4 is the D = 128 kernel");
+  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG, NSL = 4;
+  using KI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[NSL * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  const int nqb = (S + 255) / 256;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  const int h = hk * grp + L % grp;
+  L /= grp;
+  int b, mb;
+  block_of(a, L, nqb, true, b, mb);
+  const int qs = mb * 256, qw = qs + wid * 64;
+  const int qrow0 = qw + r, qrow1 = qw + 32 + r;
+  const float sl2 = a.scale * kLog2e;
+
+  // O^T = 0 and Q into the accumulator file; this statement also claims all 256 accumulator registers for
+  // the kernel descriptor (the clobbers), so hipcc neither allocates nor spills into them
+  asm volatile(
+#define Z4(n) "v_accvgpr_write_b32 a" #n ", 0\n\t"
+      Z4(0) Z4(1) Z4(2) Z4(3) Z4(4) Z4(5) Z4(6) Z4(7) Z4(8) Z4(9) Z4(10) Z4(11) Z4(12) Z4(13) Z4(14) Z4(15)
+      Z4(16) Z4(17) Z4(18) Z4(19) Z4(20) Z4(21) Z4(22) Z4(23) Z4(24) Z4(25) Z4(26) Z4(27) Z4(28) Z4(29) Z4(30)
+      Z4(31) Z4(32) Z4(33) Z4(34) Z4(35) Z4(36) Z4(37) Z4(38) Z4(39) Z4(40) Z4(41) Z4(42) Z4(43) Z4(44) Z4(45)
+      Z4(46) Z4(47) Z4(48) Z4(49) Z4(50) Z4(51) Z4(52) Z4(53) Z4(54) Z4(55) Z4(56) Z4(57) Z4(58) Z4(59) Z4(60)
+      Z4(61) Z4(62) Z4(63) Z4(64) Z4(65) Z4(66) Z4(67) Z4(68) Z4(69) Z4(70) Z4(71) Z4(72) Z4(73) Z4(74) Z4(75)
+      Z4(76) Z4(77) Z4(78) Z4(79) Z4(80) Z4(81) Z4(82) Z4(83) Z4(84) Z4(85) Z4(86) Z4(87) Z4(88) Z4(89) Z4(90)
+      Z4(91) Z4(92) Z4(93) Z4(94) Z4(95) Z4(96) Z4(97) Z4(98) Z4(99) Z4(100) Z4(101) Z4(102) Z4(103) Z4(104)
+      Z4(105) Z4(106) Z4(107) Z4(108) Z4(109) Z4(110) Z4(111) Z4(112) Z4(113) Z4(114) Z4(115) Z4(116) Z4(117)
+      Z4(118) Z4(119) Z4(120) Z4(121) Z4(122) Z4(123) Z4(124) Z4(125) Z4(126) Z4(127)
+#undef Z4
+      ::: LLMT_ACLOB);
+  {
+    const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
+    sfor<2>([&](auto qc) {
+      constexpr int qh = decltype(qc)::value;
+      const int q = qh ? qrow1 : qrow0;
+      sfor<8>([&](auto kc) {
+        constexpr int kk = decltype(kc)::value;
+        const bfv8 x = gload8(qp + (int64_t)min(q, S - 1) * a.q_ss + kk * 16 + hh * 8, q < S);
+        const u32x4 w = __builtin_bit_cast(u32x4, x);
+        asm volatile("v_accvgpr_write_b32 a%c0, %4\n\tv_accvgpr_write_b32 a%c1, %5\n\t"
+                     "v_accvgpr_write_b32 a%c2, %6\n\tv_accvgpr_write_b32 a%c3, %7"
+                     :: "i"(fa4_aq(qh, kk)), "i"(fa4_aq(qh, kk) + 1), "i"(fa4_aq(qh, kk) + 2), "i"(fa4_aq(qh, kk) + 3),
+                     "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+      });
+    });
+  }
+  // per-row key ranges as IdxRange pieces relative to key 0 of the tile: base0 + n0 is added per tile
+  int klo0, khi0, klo1, khi1;
+  key_interval(a, b, qrow0, klo0, khi0);
+  key_interval(a, b, qrow1, klo1, khi1);
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, nm[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f};
+
+  int kv_end = a.causal ? min(S, qs + 256) : S;
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = kv_beg / BN * BN;
+  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+  // this wave's tiles with any visible key: [wt0, wt1] (wave-uniform)
+  int wt1 = T - 1, wt0 = 0;
+  if (a.causal) wt1 = min(wt1, (min(qw + 63, S - 1) - kv_beg) / BN);
+  if (a.window >= 0) wt0 = max(0, (qw - a.window - kv_beg) / BN);
+  if (qw >= S) wt1 = -1;
+
+  if (T > 0) {
+    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
+    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
+    int vk[4], vv[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int row = 16 * wid + 4 * n + (lane >> 4);
+      const int ch = (lane & 15) ^ KI::swz(row);
+      vk[n] = (row * a.k_ss + ch * 8) * 2;
+      vv[n] = (row * a.v_ss + ch * 8) * 2;
+    }
+    const uint32_t lds0 = lds_addr(smem) + 16 * wid * 256;
+    const int kstep = BN * a.k_ss * 2, vstep = BN * a.v_ss * 2;
+    auto issue = [&](int t) {
+      int kr = (kv_beg / BN + t) * kstep, vr = (kv_beg / BN + t) * vstep;
+      // opaque: otherwise hipcc keeps the per-lane offsets of every unrolled step's tile precomputed in
+      // registers (it then parked some in the accumulator file, which the asm owns)
+      asm volatile("" : "+s"(kr), "+s"(vr));
+      const int ko[4] = {vk[0] + kr, vk[1] + kr, vk[2] + kr, vk[3] + kr};
+      const int vo[4] = {vv[0] + vr, vv[1] + vr, vv[2] + vr, vv[3] + vr};
+      dma_tile8(krs, vrs, lds0 + (t & 3) * SLOT, IMG, ko, vo);
+    };
+    int ro[8], to[4][2];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) ro[kk] = lds_addr(smem) + KI::roff(r, 2 * kk + hh);
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        to[dt][0] = lds_addr(smem) + KI::toff(BN, row, dt * 32 + col) + IMG;
+        to[dt][1] = lds_addr(smem) + KI::toff(BN, row + 8, dt * 32 + col) + IMG;
+      }
+    }
+    // K fragments (both key halves, k-step kk) of the tile in ring slot `sl` into the accumulator file
+    auto read_k = [&](int sl, auto kc) {
+      constexpr int kk = decltype(kc)::value;
+      const int addr = ro[kk] + sl * SLOT;
+      asm volatile("ds_read_b128 a[%c0:%c1], %4\n\tds_read_b128 a[%c2:%c3], %4 offset:8192"
+                   :: "i"(fa4_ak(0, kk)), "i"(fa4_ak(0, kk) + 3), "i"(fa4_ak(1, kk)), "i"(fa4_ak(1, kk) + 3), "v"(addr)
+                   : "memory");
+    };
+    // V^T fragment (keys 32kh + 16s2 .., columns 32dt ..) of the tile in ring slot `sl`
+    auto read_v = [&](int sl, int kh, int s2, int dt) -> bfv8 {
+      const int off = sl * SLOT + 256 * (32 * kh + 16 * s2);
+      using lp = __attribute__((address_space(3))) s16v4*;
+      const s16v4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(uintptr_t)(uint32_t)(to[dt][0] + off));
+      const s16v4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(uintptr_t)(uint32_t)(to[dt][1] + off));
+      return __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+
+    // ring slot 3 holds the "previous tile" V^T of a wave's first step when that is tile 0: P = 0 there, but
+    // 0 * (stale NaN / inf bits) would not be 0 — zero it once
+#pragma unroll
+    for (int i = 0; i < IMG / (16 * 256); ++i)
+      *reinterpret_cast<uint4*>(smem + 3 * SLOT + IMG + 16 * (tid + 256 * i)) = make_uint4(0, 0, 0, 0);
+    issue(0);
+    if (T > 1) issue(1);
+    wait_vm<0>();
+    ring_barrier();
+    sfor<8>([&](auto kc) { read_k(0, kc); });
+
+    // score sets of alternate steps ([key half][query half]); the set the wave's first step finishes as "the
+    // previous tile" starts at -inf (exp -> P = 0, row sums 0), so every step runs the same two phases
+    f32v16 sA[2][2], sB[2][2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) sB[x >> 1][x & 1][i] = -INFINITY;
+    uint32_t pw[2][2][2][4];  // bf16 P of the previous tile: [key half][query half][k-step][pair]
+#pragma unroll
+    for (int i = 0; i < 32; ++i) (&pw[0][0][0][0])[i] = 0u;  // the wave's first step has no previous tile
+    bool resc = false;
+
+    // phase A of tile t: S^T(t) into sc || finish the softmax of tile t-1: exps of its second key half sp[1]
+    // (the first half was exponentiated, summed and converted in phase B of the previous step), their row
+    // sums, bf16 P of that half
+    auto phase_a = [&](f32v16 (&sc)[2][2], f32v16 (&sp)[2][2], int vsl, bfv8 (&vr)[16]) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K tile in the accumulator file
+      __builtin_amdgcn_sched_barrier(0);
+      float rs0 = 0.f, rs1 = 0.f;
+      sfor<32>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        constexpr int kk = g >> 2, kh = (g >> 1) & 1, qh = g & 1;
+        if constexpr (kk == 0)
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], 0"
+                       : "=v"(sc[kh][qh])
+                       : "i"(fa4_ak(kh, kk)), "i"(fa4_ak(kh, kk) + 3), "i"(fa4_aq(qh, kk)), "i"(fa4_aq(qh, kk) + 3));
+        else
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], %0"
+                       : "+v"(sc[kh][qh])
+                       : "i"(fa4_ak(kh, kk)), "i"(fa4_ak(kh, kk) + 3), "i"(fa4_aq(qh, kk)), "i"(fa4_aq(qh, kk) + 3));
+        // the second key half's 32 scores e = 16 fq + fi, three gap-stages apart so no gap waits on its own
+        // results: gap g scales (fma) and exponentiates score g, adds score g - 2 to its row sum and packs
+        // pair (g - 4, g - 3)
+        {
+          constexpr int fq = g >> 4, fi = g & 15;
+          sp[1][fq][fi] = v_exp1(v_fma1(sp[1][fq][fi], sl2, nm[fq]));
+        }
+        if constexpr (g >= 2) {
+          constexpr int e = g - 2;
+          v_add_ip((e >> 4) ? rs1 : rs0, sp[1][e >> 4][e & 15]);
+        }
+        if constexpr (g >= 4 && (g & 1) == 0) {
+          constexpr int e = g - 4, pq = e >> 4, ei = e & 15;
+          pw[1][pq][ei >> 3][(ei & 7) >> 1] = cvt_pk(sp[1][pq][ei], sp[1][pq][ei + 1]);
+        }
+        if constexpr (g == 30) {  // the first V^T fragments of phase B
+          vr[0] = read_v(vsl, 0, 0, 0);
+          vr[1] = read_v(vsl, 0, 0, 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      // the tail: scores 30, 31 into the sum, pairs 28 and 30 (a VALU pad after the last exp)
+      asm volatile("s_nop 1");
+      v_add_ip(rs1, sp[1][1][14]);
+      v_add_ip(rs1, sp[1][1][15]);
+      pw[1][1][1][2] = cvt_pk(sp[1][1][12], sp[1][1][13]);
+      pw[1][1][1][3] = cvt_pk(sp[1][1][14], sp[1][1][15]);
+      l[0] += rs0;
+      l[1] += rs1;
+      // the asm MFMAs are invisible to hipcc's hazard recognizer: XDL write -> VALU read (and VALU write ->
+      // MFMA operand read) wait states before the next phase touches their registers
+      asm volatile("s_nop 7\n\ts_nop 7");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // phase B of tile t: O^T += V^T(t-1) P^T(t-1) || start the softmax of tile t in sc (mask, row max,
+    // defer-max decision, exps + row sums of the first key half, its bf16 P into pw[0] once the P.V MFMAs of
+    // tile t-1 no longer read that half); K(t+1) into the accumulator file (a stale slot past the last tile is
+    // read and never used). `dummy`: the drain step past the wave's last tile, whose scores are all masked.
+    // Returns the first half's row sums (added to l after a rescale)
+    auto phase_b = [&](f32v16 (&sc)[2][2], int vsl, bfv8 (&vr)[16], int t, bool dummy, float (&rsn)[2]) {
+      const int n0 = kv_beg + t * BN;
+      const bool need_mask = dummy || (a.causal && n0 + BN - 1 > qw) || (a.window >= 0 && n0 < qw + 63 - a.window) ||
+                             n0 + BN > S || qw + 63 >= S;
+      if (need_mask) {  // diagonal / window / sequence-end tiles: out-of-range keys -> -inf
+        const IdxRange r0 = dummy ? IdxRange{1u, 0u} : idx_range(klo0, khi0, n0 + 4 * hh);
+        const IdxRange r1 = dummy ? IdxRange{1u, 0u} : idx_range(klo1, khi1, n0 + 4 * hh);
+        sfor<32>([&](auto ec) {
+          constexpr int e = decltype(ec)::value, kh = e >> 4, i = e & 15;
+          constexpr int o = 32 * kh + 8 * (i >> 2) + (i & 3);
+          sc[kh][0][i] = range_or_ninf<o>(sc[kh][0][i], r0.base, r0.span);
+          sc[kh][1][i] = range_or_ninf<o>(sc[kh][1][i], r1.base, r1.span);
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float mx[2] = {0.f, 0.f}, mxa[2] = {0.f, 0.f}, mxb[2] = {0.f, 0.f}, u1 = 0.f, u2 = 0.f, u3 = 0.f;
+      rsn[0] = rsn[1] = 0.f;
+      sfor<32>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        // MFMA g: V^T fragment f = g / 2 (k-step f / 4 = (key half, s2), d tile f % 4), query half g % 2
+        constexpr int f = g >> 1, ks = f >> 2, dt = f & 3, qh = g & 1;
+        {
+          const uint32_t(&pp)[4] = pw[ks >> 1][qh][ks & 1];
+          const u32x4 pb = {pp[0], pp[1], pp[2], pp[3]};
+          asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                       :: "i"(fa4_ao(dt, qh)), "i"(fa4_ao(dt, qh) + 15), "v"(vr[f]), "v"(pb));
+        }
+        if constexpr (qh == 0 && f + 2 < 16) {  // fragment f + 2, three MFMAs ahead of its first use
+          constexpr int f2 = f + 2, k2 = f2 >> 2;
+          vr[f2] = read_v(vsl, k2 >> 1, k2 & 1, f2 & 3);
+        }
+        if constexpr (g < 9) {  // row maxima: 32 scores per query half, 8 per gap in three independent max3,
+          // folded into two running maxima one gap later
+          if constexpr (g >= 1) {
+            constexpr int q2 = (g - 1) >> 2;
+            mxa[q2] = (((g - 1) & 3) == 0) ? vmax3(u1, u2, u2) : vmax3(mxa[q2], u1, u2);
+            mxb[q2] = (((g - 1) & 3) == 0) ? u3 : fmaxf(mxb[q2], u3);
+          }
+          if constexpr (g < 8) {
+            constexpr int q2 = g >> 2, part = g & 3, k2 = part >> 1, i0 = (part & 1) * 8;
+            u1 = vmax3(sc[k2][q2][i0], sc[k2][q2][i0 + 1], sc[k2][q2][i0 + 2]);
+            u2 = vmax3(sc[k2][q2][i0 + 3], sc[k2][q2][i0 + 4], sc[k2][q2][i0 + 5]);
+            u3 = vmax3(sc[k2][q2][i0 + 6], sc[k2][q2][i0 + 7], sc[k2][q2][i0 + 7]);
+          }
+        }
+        if constexpr (g == 9) {  // both lane halves' maxima, then the defer-max decision
+#pragma unroll
+          for (int q2 = 0; q2 < 2; ++q2) {
+            mx[q2] = fmaxf(mxa[q2], mxb[q2]);
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx[q2]), __float_as_uint(mx[q2]),
+                                                            false, false);
+            mx[q2] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
+          }
+          resc = __any(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr);
+#pragma unroll
+          for (int q2 = 0; q2 < 2; ++q2) {
+            const float mnew = resc ? fmaxf(m[q2], mx[q2]) : m[q2];
+            alpha[q2] = (mnew == -INFINITY || mnew == m[q2]) ? 1.f : fexp2(m[q2] - mnew);
+            m[q2] = mnew;
+            nm[q2] = (mnew == -INFINITY) ? 0.f : -mnew;
+          }
+        }
+        if constexpr (g >= 10) {  // exps of the first key half: 32 scores over gaps 10 .. 31; row sums 2 gaps later
+          constexpr int n = fa4_nexp(g), e0 = fa4_exp0(g);
+          sfor<n>([&](auto jc) {
+            constexpr int s = e0 + decltype(jc)::value, sq = s >> 4, si = s & 15;
+            sc[0][sq][si] = v_exp1(v_fma1(sc[0][sq][si], sl2, nm[sq]));
+          });
+        }
+        if constexpr (g >= 12) {
+          constexpr int n = fa4_nexp(g - 2), e0 = fa4_exp0(g - 2);
+          sfor<n>([&](auto jc) {
+            constexpr int s = e0 + decltype(jc)::value, sq = s >> 4, si = s & 15;
+            v_add_ip(rsn[sq], sc[0][sq][si]);
+          });
+        }
+        // bf16 pair p = g - 18 of the first half (its exps done, tile t-1's first-half P no longer read)
+        if constexpr (g >= 18) {
+          constexpr int p = g - 18, s = 2 * p, sq = s >> 4, si = s & 15;
+          pw[0][sq][si >> 3][(si & 7) >> 1] = cvt_pk(sc[0][sq][si], sc[0][sq][si + 1]);
+        }
+        if constexpr (g >= 4 && g < 12) read_k((t + 1) & 3, std::integral_constant<int, g - 4>{});
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      asm volatile("s_nop 1");  // the last exps -> their row-sum adds and packs
+      sfor<4>([&](auto jc) {  // row sums of the last two gaps' scores (28 .. 31)
+        constexpr int s = 28 + decltype(jc)::value;
+        v_add_ip(rsn[1], sc[0][1][s - 16]);
+      });
+      pw[0][1][1][2] = cvt_pk(sc[0][1][12], sc[0][1][13]);
+      pw[0][1][1][3] = cvt_pk(sc[0][1][14], sc[0][1][15]);
+    };
+
+    // the rare rescale of O^T (a[0:127]) after phase B: every P at the old max is in it, none at the new one
+    auto rescale = [&]() {
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // the last P.V MFMAs' results
+      // (tile t-1's P is all in O^T: phase B issued its last P.V MFMA before this)
+      sfor<8>([&](auto tc) {
+        constexpr int tile = decltype(tc)::value, qh = tile & 1;
+        sfor<16>([&](auto ic) {
+          constexpr int reg = tile * 16 + decltype(ic)::value;
+          float x;
+          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(reg));
+          x *= alpha[qh];
+          asm volatile("v_accvgpr_write_b32 a%c1, %0" :: "v"(x), "i"(reg));
+        });
+      });
+      asm volatile("s_nop 3" ::: "memory");  // accumulator write -> MFMA C read
+      l[0] *= alpha[0];
+      l[1] *= alpha[1];
+    };
+    auto finish_step = [&]() {
+      wait_vm<0>();  // this wave's DMA of tile t + 2
+      ring_barrier();
+    };
+    // a step with nothing to compute for this wave: its share of the ring traffic only
+    auto step_idle = [&](int t) {
+      if (t + 2 < T) issue(t + 2);
+      sfor<8>([&](auto kc) { read_k((t + 1) & 3, kc); });
+      finish_step();
+    };
+    // a compute step; sc = tile t's score set, sp = tile t-1's
+    auto step = [&](f32v16 (&sc)[2][2], f32v16 (&sp)[2][2], int t) {
+      if (t + 2 < T) issue(t + 2);
+      bfv8 vr[16];
+      float rsn[2];
+      phase_a(sc, sp, (t - 1) & 3, vr);
+      phase_b(sc, (t - 1) & 3, vr, t, t > wt1, rsn);
+      if (resc) rescale();
+      l[0] += rsn[0];  // tile t's first-half row sums, at the new scale
+      l[1] += rsn[1];
+      finish_step();
+    };
+
+    int t = 0;
+    if (wt0 <= wt1) {
+      for (; t < wt0; ++t) step_idle(t);
+      // steps wt0 .. wt1 + 1 (the last one drains P.V of tile wt1), score sets alternating A, B
+      for (; t <= wt1 + 1; t += 2) {
+        step(sA, sB, t);
+        if (t + 1 <= wt1 + 1) step(sB, sA, t + 1);
+      }
+      t = wt1 + 2;
+    }
+    for (; t <= T; ++t) step_idle(t);
+  }
+  // the last asm MFMAs' results are read by the epilogue
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  sfor<2>([&](auto qc) {
+    constexpr int qh = decltype(qc)::value;
+    const float lt = l[qh] + __shfl_xor(l[qh], 32, 64);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    uint2 w[16];
+    sfor<4>([&](auto dc) {
+      constexpr int dt = decltype(dc)::value;
+      float ov[16];
+      sfor<16>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        float x;
+        asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(fa4_ao(dt, qh) + i));
+        ov[i] = x;
+      });
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        w[4 * dt + c].x = pack_bf16x2(ov[4 * c] * inv, ov[4 * c + 1] * inv);
+        w[4 * dt + c].y = pack_bf16x2(ov[4 * c + 2] * inv, ov[4 * c + 3] * inv);
+      }
+    });
+    widen_pairs(w);
+    const int q = qh ? qrow1 : qrow0;
+    if (q < S) {
+      store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)q * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
+      if (hh == 0) {
+        const float mu = (m[qh] == -INFINITY) ? 0.f : m[qh];
+        a.lse[((int64_t)b * a.Hq + h) * S + q] = lt > 0.f ? (mu + __log2f(lt)) * kLn2 : -INFINITY;
+      }
+    }
+  });
+}
+#undef LLMT_ACLOB
+
 // ============================================================================ forward, head-chained
 // fa_fwd3 with NH query heads per workgroup (same batch row and query block, so the same key-tile range,
 // masks and segment runs): the NH heads' tiles form one sequence through the K/V LDS-DMA ring, so the
@@ -2703,6 +3185,8 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
     case 128: {
       if (a.drop_thresh)  // dropout lives in the generic kernels
         fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
+      else if (variant == 10 && a.rmask && !seg)  // one wave per SIMD, 64 rows per wave (fa_fwd4_kernel)
+        fa_fwd4_kernel<128><<<(S + 255) / 256 * Hq * B, 256, 0, stream>>>(a);
       else if (variant == 2)  // row sums through the inline-asm add (each behind its own wait state)
         fa_fwd3_kernel<128><<<nb1, 256, 0, stream>>>(a);
       else if (variant == 3)  // dwordx2 O store tail (A/B reference)

@@ -12,17 +12,31 @@ residual stream sharded on the sequence dim. The reference expresses it with DTe
 - ``copy_to_tp``   fwd identity            bwd all-reduce            (non-SP input)
 - ``reduce_tp``    fwd all-reduce          bwd identity
 
-With SP the collectives next to the projection GEMMs are overlapped with GEMM work instead of
-running back to back with it (``ag_linear`` / ``linear_rs``, used by the decoder layers):
+With SP the collectives next to the projection GEMMs are pipelined with the GEMMs (``ag_linear`` /
+``linear_rs``, used by the decoder layers) as a staged collective matmul sized for MI355X's xGMI: every
+GPU of a node has a direct link to each of the other seven, so one RCCL all-gather / reduce-scatter keeps
+all seven links busy, while a peer-by-peer ring of P2P transfers would move each step over a single link
+(and P2P operations on one communicator run one after another on its stream). Each rank's sequence shard
+is therefore cut into ``m`` sub-chunks (``LLMT_TP_STAGES``, default 4) and each collective into ``m``
+full-mesh collectives of one sub-chunk each, issued together on the communicator's stream; the compute
+stream waits only for the stage it is about to use:
 
-- ``ag_linear``  (q/k/v, gate/up):  forward all-gathers the sequence shards asynchronously while the GEMM
-  of this rank's own rows runs, then the GEMM of the other ranks' rows; backward starts the
-  reduce-scatter of the input gradient and runs the weight-gradient GEMM under it.
-- ``linear_rs``  (o, down):  backward all-gathers the output gradient asynchronously while the
-  input-gradient GEMM of this rank's own rows runs. (The forward reduce-scatter has no independent
-  GEMM work beside it.)
+- ``ag_linear``  (q/k/v, gate/up), forward: all-gather stage j+1 is in flight while the GEMMs of stage j's
+  rows (one per source rank, written straight into their rows of the output) run; backward: the input
+  gradient of stage j (one GEMM per destination rank) is reduce-scattered while stage j+1's is computed,
+  and the weight gradient accumulates per (stage, rank) block beside them.
+- ``linear_rs``  (o, down), forward: the output rows of stage j are reduce-scattered while stage j+1's are
+  computed; backward: the staged all-gather of the output gradient feeds the input-gradient GEMMs stage by
+  stage, as in ``ag_linear``'s forward.
+
+Gathered tensors are kept stage-major ([m, n, S/(n m), ...]): each stage's all-gather writes one
+contiguous block, and every GEMM reads or writes a contiguous row block of it, so no reordering copy is
+made. The compute stream's waits are metered when ``TP_WAIT_METER`` holds a list (bench.py reports the
+exposed tensor-parallel communication per step from it).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -141,95 +155,144 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
     return t.reshape(-1, t.shape[-1])
 
 
+# compute-stream stalls on tensor-parallel collectives: a list of (start, end) CUDA events, or None
+TP_WAIT_METER: list | None = None
+
+
+def _tp_wait(work) -> None:
+    m = TP_WAIT_METER
+    if m is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        work.wait()
+        b.record()
+        m.append((a, b))
+    else:
+        work.wait()
+
+
+def tp_stages(rows: int) -> int:
+    """Pipeline stages for a sequence shard of ``rows`` rows: LLMT_TP_STAGES (default 4), reduced to divide it."""
+    m = max(1, int(os.environ.get("LLMT_TP_STAGES", "4")))
+    while rows % m:
+        m -= 1
+    return m
+
+
 class _AGLinear(Function):
-    """y = all_gather_seq(x) @ W^T (+ b) for seq-major x [S/n, B, K] -> [S, B, N]."""
+    """y = all_gather_seq(x) @ W^T (+ b) for seq-major x [S/n, B, K] -> [S, B, N], staged (module doc)."""
 
     @staticmethod
     def forward(ctx, x, w, b, group):
         from ..ops.fused import mm_nt
-        n, r = _ws(group), dist.get_rank(group)
+        n = _ws(group)
         x = x.contiguous()
         c = x.shape[0]
-        full = torch.empty((c * n, *x.shape[1:]), dtype=x.dtype, device=x.device)
-        work = dist.all_gather_into_tensor(full, x, group=group, async_op=True)
-        y = torch.empty((c * n, *x.shape[1:-1], w.shape[0]), dtype=x.dtype, device=x.device)
-        y2, f2 = _rows(y), _rows(full)
-        per = y2.shape[0] // n
-        mm_nt(_rows(x), w, out=y2[r * per:(r + 1) * per])  # own rows while the others arrive
-        work.wait()
-        if r > 0:
-            mm_nt(f2[:r * per], w, out=y2[:r * per])
-        if r < n - 1:
-            mm_nt(f2[(r + 1) * per:], w, out=y2[(r + 1) * per:])
-        if b is not None:
-            y += b
+        m = tp_stages(c)
+        cm = c // m
+        tail = x.shape[1:]
+        full = torch.empty((m, n, cm, *tail), dtype=x.dtype, device=x.device)  # stage-major gathered input
+        works = [dist.all_gather_into_tensor(full[j].view(n * cm, *tail), x[j * cm:(j + 1) * cm], group=group,
+                                             async_op=True) for j in range(m)]
+        y = torch.empty((c * n, *tail[:-1], w.shape[0]), dtype=x.dtype, device=x.device)
+        y5 = y.view(n, m, cm, *tail[:-1], w.shape[0])
+        for j in range(m):
+            _tp_wait(works[j])
+            for d in range(n):  # rows of source rank d, stage j -> their place in the output
+                mm_nt(_rows(full[j, d]), w, out=_rows(y5[d, j]), bias=b)
         ctx.save_for_backward(full)
-        ctx.w, ctx.group, ctx.has_bias = w, group, b is not None
+        ctx.w, ctx.group, ctx.has_bias, ctx.m = w, group, b is not None, m
         return y
 
     @staticmethod
     def backward(ctx, dy):
         from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn
         (full,) = ctx.saved_tensors
-        w, group = ctx.w, ctx.group
-        n = _ws(group)
-        dy2 = _rows(dy.contiguous())
-        dx = db = dw = None
-        work = None
+        w, group, m = ctx.w, ctx.group, ctx.m
+        n, cm = full.shape[1], full.shape[2]
+        tail = full.shape[3:]
+        dy = dy.contiguous()
+        dy5 = dy.view(n, m, cm, *dy.shape[1:])
+        dx = dw = db = None
+        works = []
         if ctx.needs_input_grad[0]:
-            dx_full = mm_nn(dy2, w).view(*full.shape)
-            dx = torch.empty((full.shape[0] // n, *full.shape[1:]), dtype=full.dtype, device=full.device)
-            work = dist.reduce_scatter_tensor(dx, dx_full, group=group, async_op=True)
+            dx = torch.empty((m * cm, *tail), dtype=full.dtype, device=full.device)
+            for j in range(m):  # stage j's input gradient is reduce-scattered while stage j+1's is computed
+                part = torch.empty((n, cm, *tail), dtype=full.dtype, device=full.device)
+                for d in range(n):
+                    mm_nn(_rows(dy5[d, j]), w, out=_rows(part[d]))
+                works.append(dist.reduce_scatter_tensor(dx[j * cm:(j + 1) * cm], part.view(n * cm, *tail), group=group,
+                                                        async_op=True))
         if ctx.needs_input_grad[1]:
-            dw = _wgrad_mm(w, dy2.t(), _rows(full))  # runs under the reduce-scatter
+            # the weight gradient per (stage, rank) block, accumulated, under the last reduce-scatters
+            for j in range(m):
+                for d in range(n):
+                    r = _wgrad_mm(w, _rows(dy5[d, j]).t(), _rows(full[j, d]))
+                    dw = r if dw is None else (dw + r if r is not None else dw)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy2.sum(0)
-        if work is not None:
-            work.wait()
+            db = _rows(dy).sum(0)
+        for wk in works:
+            _tp_wait(wk)
         drop_dy_t()  # a SwiGLU-produced dy^T is only used by the plain linear path
         return dx, dw, db, None
 
 
 class _LinearRS(Function):
-    """y = reduce_scatter_seq(x @ W^T) (+ b once) for seq-major x [S, B, K] -> [S/n, B, N]."""
+    """y = reduce_scatter_seq(x @ W^T) (+ b once) for seq-major x [S, B, K] -> [S/n, B, N], staged."""
 
     @staticmethod
     def forward(ctx, x, w, b, group):
         from ..ops.fused import mm_nt
+        n = _ws(group)
         x = x.contiguous()
-        y = mm_nt(_rows(x), w).view(*x.shape[:-1], w.shape[0])
-        y = reduce_scatter_seq(y, group)
+        assert x.shape[0] % n == 0, "sequence length must be divisible by the tensor-parallel size"
+        c = x.shape[0] // n
+        m = tp_stages(c)
+        cm = c // m
+        x5 = x.view(n, m, cm, *x.shape[1:])
+        y = torch.empty((c, *x.shape[1:-1], w.shape[0]), dtype=x.dtype, device=x.device)
+        works, parts = [], []
+        for j in range(m):  # stage j's rows are reduce-scattered while stage j+1's are computed
+            part = torch.empty((n, cm, *x.shape[1:-1], w.shape[0]), dtype=x.dtype, device=x.device)
+            for d in range(n):
+                mm_nt(_rows(x5[d, j]), w, out=_rows(part[d]))
+            works.append(dist.reduce_scatter_tensor(y[j * cm:(j + 1) * cm], part.view(n * cm, *part.shape[2:]),
+                                                    group=group, async_op=True))
+            parts.append(part)
+        for wk in works:
+            _tp_wait(wk)
+        del parts
         if b is not None:
             y = y + b
         ctx.save_for_backward(x)
-        ctx.w, ctx.group, ctx.has_bias = w, group, b is not None
+        ctx.w, ctx.group, ctx.has_bias, ctx.m = w, group, b is not None, m
         return y
 
     @staticmethod
     def backward(ctx, dy):
         from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn
         (x,) = ctx.saved_tensors
-        w, group = ctx.w, ctx.group
-        n, r = _ws(group), dist.get_rank(group)
+        w, group, m = ctx.w, ctx.group, ctx.m
+        n = _ws(group)
         dy = dy.contiguous()
-        full = torch.empty((dy.shape[0] * n, *dy.shape[1:]), dtype=dy.dtype, device=dy.device)
-        work = dist.all_gather_into_tensor(full, dy, group=group, async_op=True)
+        c = dy.shape[0]
+        cm = c // m
+        x5 = x.view(n, m, cm, *x.shape[1:])
+        full = torch.empty((m, n, cm, *dy.shape[1:]), dtype=dy.dtype, device=dy.device)  # stage-major dy
+        works = [dist.all_gather_into_tensor(full[j].view(n * cm, *dy.shape[1:]), dy[j * cm:(j + 1) * cm],
+                                             group=group, async_op=True) for j in range(m)]
         dx = dw = db = None
-        f2 = _rows(full)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            dx2 = _rows(dx)
-            per = dx2.shape[0] // n
-            mm_nn(_rows(dy), w, out=dx2[r * per:(r + 1) * per])  # own rows while the others arrive
-            work.wait()
-            if r > 0:
-                mm_nn(f2[:r * per], w, out=dx2[:r * per])
-            if r < n - 1:
-                mm_nn(f2[(r + 1) * per:], w, out=dx2[(r + 1) * per:])
-        else:
-            work.wait()
-        if ctx.needs_input_grad[1]:
-            dw = _wgrad_mm(w, f2.t(), _rows(x))
+            dx5 = dx.view(n, m, cm, *x.shape[1:])
+        for j in range(m):
+            _tp_wait(works[j])
+            for d in range(n):
+                if ctx.needs_input_grad[0]:
+                    mm_nn(_rows(full[j, d]), w, out=_rows(dx5[d, j]))
+                if ctx.needs_input_grad[1]:
+                    r = _wgrad_mm(w, _rows(full[j, d]).t(), _rows(x5[d, j]))
+                    dw = r if dw is None else (dw + r if r is not None else dw)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _rows(dy).sum(0)
         drop_dy_t()  # a SwiGLU-produced dy^T is only used by the plain linear path
@@ -237,7 +300,7 @@ class _LinearRS(Function):
 
 
 def ag_linear(x, w, b, group):
-    """Column-parallel projection of the sequence-gathered input, gather overlapped with the GEMM."""
+    """Column-parallel projection of the sequence-gathered input, staged gather overlapped with the GEMMs."""
     if _ws(group) == 1:
         from ..ops.fused import linear
         return linear(x, w, b)
@@ -245,7 +308,7 @@ def ag_linear(x, w, b, group):
 
 
 def linear_rs(x, w, b, group):
-    """Row-parallel projection reduce-scattered over the sequence, backward gather overlapped."""
+    """Row-parallel projection reduce-scattered over the sequence, staged with the GEMMs both ways."""
     if _ws(group) == 1:
         from ..ops.fused import linear
         return linear(x, w, b)
