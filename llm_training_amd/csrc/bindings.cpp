@@ -42,7 +42,10 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
                                int B, int S, int Hq, int Hkv, int D, int64_t q_sb, int64_t q_ss, int64_t q_sh,
                                int64_t k_sb, int64_t k_ss, int64_t k_sh, int64_t v_sb, int64_t v_ss, int64_t v_sh,
                                int64_t o_sb, int64_t o_ss, int64_t o_sh, float scale, int causal, int window,
-                               int seg_runs, float drop_p, uint32_t drop_seed, hipStream_t stream);
+                               int seg_runs, float drop_p, uint32_t drop_seed, const void* rpos, int rpos64,
+                               int64_t rp_sb, int64_t rp_ss, const float* rcos, const float* rsin, int64_t rP,
+                               void* qrot, hipStream_t stream);
+int llmt_flash_attn_fwd_rope_inkernel(int D, float drop_p, int has_seg, int seg_runs);
 hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N, int K,
                      int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream);
 hipError_t llmt_gemm_splitk(const void* x, const void* y, float* slabs, int x_mn, int y_mn, int M, int N, int K,
@@ -59,7 +62,9 @@ hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const void* v, cons
                                int64_t v_sh, int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss,
                                int64_t dq_sh, int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb,
                                int64_t dv_ss, int64_t dv_sh, float scale, int causal, int window, int seg_runs,
-                               float drop_p, uint32_t drop_seed, hipStream_t stream);
+                               float drop_p, uint32_t drop_seed, const void* rpos, int rpos64, int64_t rp_sb,
+                               int64_t rp_ss, const float* rcos, const float* rsin, int64_t rP, void* qrot,
+                               hipStream_t stream);
 }
 
 namespace {
@@ -443,9 +448,53 @@ static int seg_layout(const c10::optional<at::Tensor>& seg, int64_t B, int64_t S
   *sp = seg->data_ptr<int>();
   return seg->numel() == 3 * B * S + nord ? 2 : seg->numel() == 3 * B * S ? 1 : 0;
 }
+// fused RoPE operands of the attention ops: positions of token (b, s) at pos[b * sb + s * ss] (int32 / int64),
+// fp32 half-width tables [P, D/2] (the standalone rope_'s contract)
+struct RopeIn {
+  const void* pos = nullptr;
+  int pos64 = 0;
+  const float* cos = nullptr;
+  const float* sin = nullptr;
+  int64_t P = 0, sb = 0, ss = 0;
+};
+RopeIn rope_in(const c10::optional<at::Tensor>& pos, const c10::optional<at::Tensor>& cos_t,
+               const c10::optional<at::Tensor>& sin_t, int64_t sb, int64_t ss, int64_t B, int64_t S, int64_t D) {
+  RopeIn r;
+  if (!cos_t.has_value()) {
+    TORCH_CHECK(!pos.has_value() && !sin_t.has_value(), "flash_attn rope: cos / sin tables required");
+    return r;
+  }
+  TORCH_CHECK(sin_t.has_value(), "flash_attn rope: cos / sin tables required");
+  TORCH_CHECK(cos_t->scalar_type() == at::kFloat && sin_t->scalar_type() == at::kFloat && cos_t->is_contiguous() &&
+                  sin_t->is_contiguous() && cos_t->dim() == 2 && cos_t->size(1) * 2 == D && sin_t->sizes() == cos_t->sizes() &&
+                  cos_t->is_cuda() && sin_t->is_cuda(),
+              "flash_attn rope: cos/sin tables must be fp32 [rows, D/2] on the GPU");
+  TORCH_CHECK(sb >= 0 && ss >= 0, "flash_attn rope: row strides");
+  if (pos.has_value()) {  // position ids index the tables
+    TORCH_CHECK(pos->is_cuda() && pos->is_contiguous() &&
+                    (pos->scalar_type() == at::kLong || pos->scalar_type() == at::kInt),
+                "flash_attn rope: positions must be contiguous int32 / int64 on the GPU");
+    TORCH_CHECK((B - 1) * sb + (S - 1) * ss < pos->numel(), "flash_attn rope: position strides");
+    r.pos = pos->data_ptr();
+    r.pos64 = pos->scalar_type() == at::kLong;
+  } else {  // per-token tables: row b * sb + s * ss is token (b, s)'s own
+    TORCH_CHECK((B - 1) * sb + (S - 1) * ss < cos_t->size(0), "flash_attn rope: token-table strides");
+  }
+  r.cos = cos_t->data_ptr<float>();
+  r.sin = sin_t->data_ptr<float>();
+  r.P = cos_t->size(0);
+  r.sb = sb;
+  r.ss = ss;
+  return r;
+}
+
 std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                                   const c10::optional<at::Tensor>& seg, double scale, bool causal,
-                                                  int64_t window, double dropout_p, int64_t seed) {
+                                                  int64_t window, double dropout_p, int64_t seed,
+                                                  const c10::optional<at::Tensor>& rope_pos,
+                                                  const c10::optional<at::Tensor>& rope_cos,
+                                                  const c10::optional<at::Tensor>& rope_sin, int64_t rope_sb,
+                                                  int64_t rope_ss) {
   check_bf16_cuda(q, "q");
   check_bf16_cuda(k, "k");
   check_bf16_cuda(v, "v");
@@ -462,11 +511,18 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
   auto lse = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   const int* sp = nullptr;
   const int runs = seg_layout(seg, B, S, &sp);
+  // fused RoPE: q arrives unrotated and is never written; kernels without the in-kernel rotation read a
+  // rotated copy (qrot)
+  const RopeIn rp = rope_in(rope_pos, rope_cos, rope_sin, rope_sb, rope_ss, B, S, D);
+  at::Tensor qrot;
+  if (rp.cos && !llmt_flash_attn_fwd_rope_inkernel((int)D, (float)dropout_p, sp != nullptr, runs))
+    qrot = at::empty({B, S, Hq, D}, q.options());
   check(llmt_flash_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), sp, (int)B,
                             (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(0), q.stride(1), q.stride(2), k.stride(0),
                             k.stride(1), k.stride(2), v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1),
                             o.stride(2), (float)scale, causal ? 1 : 0, (int)window, runs, (float)dropout_p,
-                            (uint32_t)seed, cur_stream()),
+                            (uint32_t)seed, rp.pos, rp.pos64, rp.sb, rp.ss, rp.cos, rp.sin, rp.P,
+                            qrot.defined() ? qrot.data_ptr() : nullptr, cur_stream()),
         "flash_attn_fwd");
   return {o, lse};
 }
@@ -475,7 +531,9 @@ std::tuple<at::Tensor, at::Tensor> flash_attn_fwd(const at::Tensor& q, const at:
 void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
                     const at::Tensor& dout, const at::Tensor& lse, const c10::optional<at::Tensor>& seg, at::Tensor dq,
                     at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window, double dropout_p,
-                    int64_t seed) {
+                    int64_t seed, const c10::optional<at::Tensor>& rope_pos, const c10::optional<at::Tensor>& rope_cos,
+                    const c10::optional<at::Tensor>& rope_sin, int64_t rope_sb, int64_t rope_ss,
+                    bool rope_q_rotated) {
   const int64_t B = q.size(0), S = q.size(1), Hq = q.size(2), D = q.size(3);
   const int64_t Hkv = k.size(2);
   check_bf16_cuda(dout, "dout");
@@ -492,6 +550,12 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   // only the generic kernels (dropout, or LLMT_FA_D96_GENERIC at D 64 / 96) reduce GQA through partials
   if (Hq != Hkv && (dropout_p > 0 || (D != 128 && std::getenv("LLMT_FA_D96_GENERIC"))))
     work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
+  // fused RoPE: dq / dk come back for the unrotated q / k. q holds the UNROTATED queries (k rotated) unless
+  // rope_q_rotated (both rotated in memory: only the inverse rotation of the gradients is fused); qrot
+  // receives the rotated queries the dK/dV pass stages through LDS.
+  const RopeIn rp = rope_in(rope_pos, rope_cos, rope_sin, rope_sb, rope_ss, B, S, D);
+  at::Tensor qrot;
+  if (rp.cos && !rope_q_rotated) qrot = at::empty({B, S, Hq, D}, q.options());
   check(llmt_flash_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
                             lse.data_ptr<float>(), delta.data_ptr<float>(), sp, dq.data_ptr(), dk.data_ptr(),
                             dv.data_ptr(), work.defined() ? work.data_ptr<float>() : nullptr, (int)B, (int)S, (int)Hq, (int)Hkv, (int)D,
@@ -499,7 +563,8 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
                             v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
                             dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2), dv.stride(0),
                             dv.stride(1), dv.stride(2), (float)scale, causal ? 1 : 0, (int)window, runs,
-                            (float)dropout_p, (uint32_t)seed, cur_stream()),
+                            (float)dropout_p, (uint32_t)seed, rp.pos, rp.pos64, rp.sb, rp.ss, rp.cos, rp.sin, rp.P,
+                            qrot.defined() ? qrot.data_ptr() : nullptr, cur_stream()),
         "flash_attn_bwd");
 }
 
@@ -532,10 +597,13 @@ TORCH_LIBRARY(llmt, m) {
   m.def("gemm_splitk_(Tensor a, Tensor b, Tensor(a!) slabs, bool a_mn, bool b_mn) -> ()");
   m.def(
       "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window, "
-      "float dropout_p=0., int seed=0) -> (Tensor, Tensor)");
+      "float dropout_p=0., int seed=0, Tensor? rope_pos=None, Tensor? rope_cos=None, Tensor? rope_sin=None, "
+      "int rope_sb=0, int rope_ss=0) -> (Tensor, Tensor)");
   m.def(
       "flash_attn_bwd(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor? seg, Tensor(a!) dq, "
-      "Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int window, float dropout_p=0., int seed=0) -> ()");
+      "Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int window, float dropout_p=0., int seed=0, "
+      "Tensor? rope_pos=None, Tensor? rope_cos=None, Tensor? rope_sin=None, int rope_sb=0, int rope_ss=0, "
+      "bool rope_q_rotated=False) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(llmt, CUDA, m) {

@@ -200,7 +200,101 @@ struct AttnArgs {
   // backward: non-null -> the dQ kernel computes delta = rowsum(dO * O) itself and writes the packed per-tile
   // row constants the dK/dV kernel reads here (no separate prep pass); null -> the prep kernel ran
   float* ldw;
+  // RoPE fused into the kernels (ops/fused.py _RopeFlashAttnFn; the reference applies it as its own op,
+  // src/llm_training/ops/rope_op.py:10-20 <- models/llama/llama_model.py:553). Token (b, s) sits at position
+  // rpos[b * rp_sb + s * rp_ss] (int64 when rpos64) of the half-width fp32 tables rcos / rsin [rP, D/2].
+  //  * rope_q: the forward / dQ kernels rotate their Q rows as they load them (q holds UNROTATED queries;
+  //    k is rotated by the caller); the dQ kernel also writes the rotated rows to qrot for the dK/dV pass.
+  //  * rope_dq / rope_dk: the dQ / dK epilogues apply the inverse rotation, so the kernels return the
+  //    gradient of the unrotated q / k.
+  const void* rpos;
+  const float* rcos;
+  const float* rsin;
+  int rp_sb, rp_ss, rpos64, rP;
+  int rope_q, rope_dq, rope_dk;
+  bf16* qrot;
+  int qr_sb, qr_ss, qr_sh;
 };
+
+// ---------------------------------------------------------------------------- fused RoPE helpers
+// table row of token (b, s): through the position ids, or (rpos null) per-token tables whose row b * rp_sb +
+// s * rp_ss holds the token's own cos / sin (one gather per forward, shared by every layer: no dependent
+// position load in front of the table read)
+__device__ __forceinline__ int rope_pos(const AttnArgs& a, int b, int s) {
+  const int64_t i = (int64_t)b * a.rp_sb + (int64_t)s * a.rp_ss;
+  const int64_t p = !a.rpos ? i
+                    : a.rpos64 ? reinterpret_cast<const int64_t*>(a.rpos)[i]
+                               : (int64_t)reinterpret_cast<const int*>(a.rpos)[i];
+  return (int)(p < 0 ? 0 : (p >= a.rP ? a.rP - 1 : p));  // out-of-table positions were flagged by the K pass
+}
+// rotate one row's fragments (lane half hh holds element 16 kk + 8 hh + j in f[kk][j]; the partner of
+// element e < D/2 is e + D/2, i.e. fragment kk + NKK/2 in the same lane) with the row's tables cr / sr;
+// sign -1 = inverse. Same arithmetic and bf16 rounding as the standalone kernel (csrc/elementwise.hip).
+template <int NKK>
+__device__ __forceinline__ void rope_frags(bfv8 (&f)[NKK], const float* cr, const float* sr, int hh) {
+  constexpr int H = NKK / 2;
+#pragma unroll
+  for (int kk = 0; kk < H; ++kk) {
+    float c[8], s[8];
+    *reinterpret_cast<float4*>(c) = *reinterpret_cast<const float4*>(cr + 16 * kk + 8 * hh);
+    *reinterpret_cast<float4*>(c + 4) = *reinterpret_cast<const float4*>(cr + 16 * kk + 8 * hh + 4);
+    *reinterpret_cast<float4*>(s) = *reinterpret_cast<const float4*>(sr + 16 * kk + 8 * hh);
+    *reinterpret_cast<float4*>(s + 4) = *reinterpret_cast<const float4*>(sr + 16 * kk + 8 * hh + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x1 = (float)f[kk][j], x2 = (float)f[kk + H][j];
+      f[kk][j] = (__bf16)(x1 * c[j] - x2 * s[j]);
+      f[kk + H][j] = (__bf16)(x2 * c[j] + x1 * s[j]);
+    }
+  }
+}
+// inverse rotation of one row's fp32 gradient in the row-per-lane store layout (element 32 dt + 8 c + 4 hh + j
+// in acc[dt][4 c + j]): 8-column group g = 4 dt + c pairs with group g + D/16 in the same lane
+template <int D>
+__device__ __forceinline__ void rope_acc_inv(f32v16 (&acc)[D / 32], const float* cr, const float* sr, int hh) {
+  constexpr int NG = D / 16;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int g2 = g + NG;
+    const float4 c4 = *reinterpret_cast<const float4*>(cr + 8 * g + 4 * hh);
+    const float4 s4 = *reinterpret_cast<const float4*>(sr + 8 * g + 4 * hh);
+    const float c[4] = {c4.x, c4.y, c4.z, c4.w}, s[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x1 = acc[g >> 2][4 * (g & 3) + j], x2 = acc[g2 >> 2][4 * (g2 & 3) + j];
+      acc[g >> 2][4 * (g & 3) + j] = x1 * c[j] + x2 * s[j];
+      acc[g2 >> 2][4 * (g2 & 3) + j] = x2 * c[j] - x1 * s[j];
+    }
+  }
+}
+// RoPE outside the attention kernels, for the launch paths without the fused form (dropout, the generic
+// kernels, opt-in variants): strided [B, S, H, D] rows x -> y (y may alias x), one thread per 8 pairs
+__global__ __launch_bounds__(256) void rope_bshd_kernel(AttnArgs a, const bf16* x, int x_sb, int x_ss, int x_sh, bf16* y,
+                                                        int y_sb, int y_ss, int y_sh, int H, int D, float sign) {
+  const int G = D / 16, half = D / 2;
+  const int64_t n = (int64_t)a.B * a.S * H * G;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int g = (int)(e % G);
+    int64_t t = e / G;
+    const int h = (int)(t % H);
+    t /= H;
+    const int s = (int)(t % a.S), b = (int)(t / a.S);
+    const int p = rope_pos(a, b, s);
+    const float* cr = a.rcos + (int64_t)p * half + 8 * g;
+    const float* sr = a.rsin + (int64_t)p * half + 8 * g;
+    const bf16* xr = x + (int64_t)b * x_sb + (int64_t)s * x_ss + (int64_t)h * x_sh + 8 * g;
+    bf16* yr = y + (int64_t)b * y_sb + (int64_t)s * y_ss + (int64_t)h * y_sh + 8 * g;
+    bfv8 lo = *reinterpret_cast<const bfv8*>(xr), hi = *reinterpret_cast<const bfv8*>(xr + half);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = cr[j], sn = sign * sr[j], x1 = (float)lo[j], x2 = (float)hi[j];
+      lo[j] = (__bf16)(x1 * c - x2 * sn);
+      hi[j] = (__bf16)(x2 * c + x1 * sn);
+    }
+    *reinterpret_cast<bfv8*>(yr) = lo;
+    *reinterpret_cast<bfv8*>(yr + half) = hi;
+  }
+}
 
 __device__ __forceinline__ uint32_t drop_hash(uint32_t seed, uint32_t bh, uint32_t q, uint32_t k) {
   uint32_t x = seed ^ (bh * 0x9E3779B1u);
@@ -1728,6 +1822,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
     wait_vm<0>();  // no LDS-DMA may outlive the workgroup
   }
 
+  if (a.rope_dk && kr < S) {  // fused RoPE: gradient of the unrotated k
+    const int p = rope_pos(a, b, kr);
+    rope_acc_inv<D>(dkt, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
+  }
   uint2 wk[4 * NDT], wv[4 * NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
@@ -1834,6 +1932,10 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   bfv8 qf[NKK];
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+  if (a.rope_q && qrow < S) {  // fused RoPE: the rows arrive unrotated
+    const int p = rope_pos(a, b, qrow);
+    rope_frags<NKK>(qf, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
+  }
   // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
   asm volatile("" : "+v"(sq), "+v"(klo), "+v"(khi));
 #pragma unroll
@@ -2528,6 +2630,371 @@ __global__ __launch_bounds__(256, 1) void fa_fwd4_kernel(AttnArgs a) {
     }
   });
 }
+// ============================================================================ backward dK/dV, v6
+// 64 keys per wave (two 32-key halves), dV^T and dK^T of both halves in the 256 accumulator registers
+// (asm-owned, like fa_fwd4: a[0:127] dV^T, a[128:255] dK^T), so every Q^T / dO^T transposed fragment read
+// from LDS feeds two MFMAs (one per key half) where fa_bwd_dkdv5 feeds one, and a 256-key workgroup of 4
+// waves moves each Q / dO tile through the LDS-DMA ring for twice the keys (cdna guide, 'Attention
+// backward': 64 keys per wave in 256 accumulator registers). The wave's K fragments stay in VGPRs (64
+// registers); V of the workgroup's 256 keys sits in LDS (a 64 KB swizzled image, the dP operand), next to a
+// 5-slot Q / dO ring (tiles issued 3 ahead). Per 32-row query tile t, four phases of 16 MFMAs:
+//   1  S chain, then dP chain of key half 0 (tile t)  || in the dP gaps: mask, P = exp2(...) of half 0
+//   2  dV / dK of half 1 (tile t-1)                    || dS of half 0, bf16 P / dS of half 0
+//   3  S chain, then dP chain of key half 1 (tile t)  || P of half 1
+//      (ring wait + barrier: tile t+1 landed)
+//   4  dV / dK of half 0 (tile t)                      || dS, bf16 P / dS of half 1
+// One fp32 score set (S, dP: 32 registers) serves both halves: each half's softmax ends in the phase after
+// its chains. Operand reads run three MFMAs ahead of their use (the LDS latency under load); one
+// accumulation chain per MFMA shape needs no interleaving (MI355X_MICROARCH: 32 cycles back to back on one
+// accumulator). Dense rows only (D = 128, causal / window, no segments): packed rows keep fa_bwd_dkdv5.
+constexpr int d6_av(int h, int dt) { return (h * 4 + dt) * 16; }        // dV^T accumulator (key half, d tile)
+constexpr int d6_ak(int h, int dt) { return 128 + (h * 4 + dt) * 16; }  // dK^T accumulator
+
+template <int D = 128, int PF = 3>
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const float* ld) {
+  static_assert(D == 128, "fa_bwd_dkdv6 is the D = 128 kernel");
+  constexpr int NKK = 8, NDT = 4, NB = 16;
+  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 512, NS = 5, NDMA = 5;
+  constexpr int VIMG = 256 * 256;  // V of the workgroup's 256 keys
+  using QI = Img<128>;
+  __shared__ __attribute__((aligned(16))) char smem[VIMG + NS * SLOT];
+  char* const ring = smem + VIMG;
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.S, grp = a.Hq / a.Hkv;
+  int L = (int)blockIdx.x;
+  const int hk = L % a.Hkv;
+  L /= a.Hkv;
+  int b, kb;
+  block_of(a, L, (S + 255) / 256, false, b, kb);
+  const int ks = kb * 256, kw = ks + wid * 64;
+  const int nT = (S + 31) / 32;
+  const float sl2 = a.scale * kLog2e;
+
+  // dV^T = dK^T = 0; the clobbers claim all 256 accumulator registers for the kernel descriptor, so hipcc
+  // neither allocates nor spills into them
+  asm volatile("s_nop 0" ::: LLMT_ACLOB);
+  sfor<256>([&](auto ic) __attribute__((always_inline)) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(ic)::value)); });
+
+  // the wave's K fragments (lane: key kw + 32 h + r, columns 16 kk + 8 hh ..), rows past S read as zeros
+  bfv8 kf[2][NKK];
+  {
+    const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int key = kw + 32 * h + r;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) kf[h][kk] = gload8(kp + (int64_t)min(key, S - 1) * a.k_ss + kk * 16 + hh * 8, key < S);
+    }
+  }
+  // query range of each half's key (range masks) and the block's query tiles
+  int qlo[2], qhi[2];
+  query_interval(a, b, kw + r, qlo[0], qhi[0]);
+  query_interval(a, b, kw + 32 + r, qlo[1], qhi[1]);
+  const int q_beg = a.causal ? ks : 0;
+  const int q_end = a.window >= 0 ? min(S, ks + 256 + a.window) : S;
+  const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
+  const int T = nq * grp;
+  // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[0][kk]), "+v"(kf[1][kk]));
+  asm volatile("" : "+v"(qlo[0]), "+v"(qhi[0]), "+v"(qlo[1]), "+v"(qhi[1]));
+
+  if (T > 0) {
+    int dq_off[2], dd_off[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int row = 8 * wid + 4 * n + (lane >> 4);
+      const int ch = (lane & 15) ^ QI::swz(row);
+      dq_off[n] = (row * a.q_ss + ch * 8) * 2;
+      dd_off[n] = (row * a.d_ss + ch * 8) * 2;
+    }
+    const int ld_off = ((wid & 1) * 64 + lane) * 4;
+    asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]));
+    const int64_t q_rows = S - q_beg;
+    const int64_t nrec_q = ((q_rows - 1) * a.q_ss + D) * 2, nrec_d = ((q_rows - 1) * a.d_ss + D) * 2;
+    const int64_t nrec_l = (int64_t)nq * kLdTile * 4;
+    const bf16* qh0 = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * grp) * a.q_sh + (int64_t)q_beg * a.q_ss;
+    const bf16* dh0 = a.dout + (int64_t)b * a.d_sb + (int64_t)(hk * grp) * a.d_sh + (int64_t)q_beg * a.d_ss;
+    const float* lh0 = ld + (((int64_t)b * a.Hq + hk * grp) * nT + (q_beg >> 5)) * kLdTile;
+    const int step_q = BM * a.q_ss * 2, step_d = BM * a.d_ss * 2;
+    Rsrc qrs = make_rsrc4(qh0, nrec_q), drs = make_rsrc4(dh0, nrec_d), lrs = make_rsrc4(lh0, nrec_l);
+    int iss_g = 0, iss_q = 0, iss_n = 0, toff_q = 0, toff_d = 0, toff_l = 0;
+    // one tile's DMA into ring slot `sl`; past the last tile the last one is loaded again (every iteration
+    // issues the same number of pieces, so one counted wait fits every iteration)
+    auto issue = [&](int sl) __attribute__((always_inline)) {
+      const char* q0 = ring + sl * SLOT + 8 * wid * 256;
+      dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, ring + sl * SLOT + 2 * IMG + (wid & 1) * 256,
+                dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
+      if (++iss_n < T) {
+        toff_q += step_q;
+        toff_d += step_d;
+        toff_l += kLdTile * 4;
+        if (++iss_q == nq) {
+          iss_q = 0;
+          ++iss_g;
+          toff_q = toff_d = toff_l = 0;
+          qrs = make_rsrc4(qh0 + (int64_t)iss_g * a.q_sh, nrec_q);
+          drs = make_rsrc4(dh0 + (int64_t)iss_g * a.d_sh, nrec_d);
+          lrs = make_rsrc4(lh0 + (int64_t)iss_g * nT * kLdTile, nrec_l);
+        }
+      }
+    };
+    // tiles 0 .. NS-3, then V of the workgroup's keys (16 pieces of 4 rows per wave, swizzled like QI)
+#pragma unroll
+    for (int t = 0; t < NS - 2; ++t) issue(t);
+    {
+      const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh + (int64_t)ks * a.v_ss,
+                                  S > ks ? ((int64_t)(S - 1 - ks) * a.v_ss + D) * 2 : 0);
+#pragma unroll
+      for (int n = 0; n < 16; ++n) {
+        const int row = 64 * wid + 4 * n + (lane >> 4);
+        const int ch = (lane & 15) ^ QI::swz(row);
+        dma16(vrs, smem + (64 * wid + 4 * n) * 256, (row * a.v_ss + ch * 8) * 2);
+      }
+    }
+    wait_vm<0>();
+    ring_barrier();
+
+    // LDS offsets: row reads of k-step kk at ro0 ^ (32 kk) (the swizzle moves 16-byte chunks within bits 4-7
+    // of the offset, disjoint from the row's bits), transposed reads of d tile dt at to0[x] ^ (64 dt)
+    const int ro0 = QI::roff(r, hh);
+    int to0[2];
+    {
+      const int g = lane >> 4, i16 = lane & 15;
+      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
+      to0[0] = QI::toff(BM, row, col);
+      to0[1] = QI::toff(BM, row + 8, col);
+    }
+    const char* vimg = smem + 64 * wid * 256;
+    auto rd_q = [&](int sl, int kk) __attribute__((always_inline)) { return lds_b128(ring + sl * SLOT + (ro0 ^ (32 * kk))); };
+    auto rd_d = [&](int sl, int kk) __attribute__((always_inline)) { return lds_b128(ring + sl * SLOT + IMG + (ro0 ^ (32 * kk))); };
+    auto rd_v = [&](int h, int kk) __attribute__((always_inline)) { return lds_b128(vimg + 32 * 256 * h + (ro0 ^ (32 * kk))); };
+    // transposed fragment i of a dV / dK phase: i < 8 -> dO^T (dV product), else Q^T (dK); s2 = (i / 4) & 1
+    auto rd_t = [&](int sl, int i) __attribute__((always_inline)) -> bfv8 {
+      const int s2 = (i / NDT) & 1, dt = i % NDT;
+      const char* base = ring + sl * SLOT + (i < 2 * NDT ? IMG : 0) + 4096 * s2;
+      const s16v4 lo = lds_tr(base + (to0[0] ^ (64 * dt))), hi = lds_tr(base + (to0[1] ^ (64 * dt)));
+      return __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+
+    f32v16 sc, dc;             // S (then P) and dP (then dS) of the half in flight
+    u32x4 pw[2][2], dw[2][2];  // bf16 P / dS operands [key half][k-step]
+    float lq[16], nd[16];      // the tile's row constants (-lse log2e, -delta) for the half in flight
+    bfv8 qf[NKK], df[NKK], vf[NKK], tf[NB];
+    auto q0_of = [&](int t) __attribute__((always_inline)) { return q_beg + (t % nq) * BM; };
+    auto need_mask = [&](int q0, int H) __attribute__((always_inline)) {
+      const int k0 = kw + 32 * H;
+      return (a.causal && q0 < k0 + 31) || (a.window >= 0 && q0 + 31 - k0 > a.window);
+    };
+    auto pref_q = [&](int sl) __attribute__((always_inline)) {
+#pragma unroll
+      for (int kk = 0; kk < PF; ++kk) qf[kk] = rd_q(sl, kk);
+    };
+
+    // S chain then dP chain of key half H (tile in slot sl), P = exp2(S * scale * log2e - lse * log2e) of its
+    // first 12 elements in the dP gaps (from gap 10: two MFMAs behind the last S MFMA, the XDL-write ->
+    // VALU-read wait states); MSK: the tile needs the range mask (diagonal / window), applied at gap 9.
+    // `tsl`: the slot whose first transposed fragments the next (dV / dK) phase reads, fetched at gaps 13 .. 15
+    auto sd_phase = [&](auto hc, auto mc, int sl, int q0, int tsl) __attribute__((always_inline)) {
+      constexpr int H = decltype(hc)::value;
+      constexpr bool MSK = decltype(mc)::value;
+      const float* Ls = reinterpret_cast<const float*>(ring + sl * SLOT + 2 * IMG);
+      sfor<16>([&](auto gc) __attribute__((always_inline)) {
+        constexpr int g = decltype(gc)::value;
+        if constexpr (g < NKK) {
+          if constexpr (g == 0)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(sc) : "v"(qf[0]), "v"(kf[H][0]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sc) : "v"(qf[g]), "v"(kf[H][g]));
+          if constexpr (g + PF < NKK) qf[g + PF] = rd_q(sl, g + PF);
+          if constexpr (g >= NKK - PF) {  // the dP chain's first operands
+            constexpr int k2 = g - (NKK - PF);
+            df[k2] = rd_d(sl, k2);
+            vf[k2] = rd_v(H, k2);
+          }
+          if constexpr (g == 1 || g == 2) {  // -lse * log2e of the tile's rows (floats 96 ..)
+#pragma unroll
+            for (int c = 2 * (g - 1); c < 2 * g; ++c) {
+              const float4 l4 = *reinterpret_cast<const float4*>(Ls + 96 + 8 * c + 4 * hh);
+              lq[4 * c] = l4.x; lq[4 * c + 1] = l4.y; lq[4 * c + 2] = l4.z; lq[4 * c + 3] = l4.w;
+            }
+          }
+        } else {
+          constexpr int kk = g - NKK;
+          if constexpr (kk == 0)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(dc) : "v"(df[0]), "v"(vf[0]));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(dc) : "v"(df[kk]), "v"(vf[kk]));
+          if constexpr (kk + PF < NKK) {
+            df[kk + PF] = rd_d(sl, kk + PF);
+            vf[kk + PF] = rd_v(H, kk + PF);
+          }
+          if constexpr (g == 9 && MSK) {  // out-of-range queries -> -inf (P = 0, dS = 0)
+            const IdxRange rg = idx_range(qlo[H], qhi[H], q0 + 4 * hh);
+            sfor<16>([&](auto vc) __attribute__((always_inline)) {
+              constexpr int v = decltype(vc)::value, o = 8 * (v >> 2) + (v & 3);
+              sc[v] = range_or_ninf<o>(sc[v], rg.base, rg.span);
+            });
+          }
+          if constexpr (g >= 10) {
+            sfor<2>([&](auto jc) __attribute__((always_inline)) {
+              constexpr int v = 2 * (g - 10) + decltype(jc)::value;
+              sc[v] = v_exp1(v_fma1(sc[v], sl2, lq[v]));
+            });
+          }
+          if constexpr (g >= 13) tf[g - 13] = rd_t(tsl, g - 13);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    };
+    // finish the softmax of key half HS (P of elements 12 .. 15, dS = P (dP - delta), bf16 pairs) in gaps 0 .. 10
+    auto sm_tail = [&](auto hsc, int sl) __attribute__((always_inline)) {
+      const float* Ls = reinterpret_cast<const float*>(ring + sl * SLOT + 2 * IMG);
+      return [&, hsc, Ls](auto gc) __attribute__((always_inline)) {
+        constexpr int HS = decltype(hsc)::value, g = decltype(gc)::value;
+        if constexpr (g == 0) {  // -delta of the tile's rows (floats 32 ..)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
+            nd[4 * c] = d4.x; nd[4 * c + 1] = d4.y; nd[4 * c + 2] = d4.z; nd[4 * c + 3] = d4.w;
+          }
+        }
+        if constexpr (g < 2) {
+          sfor<2>([&](auto jc) __attribute__((always_inline)) {
+            constexpr int v = 12 + 2 * g + decltype(jc)::value;
+            sc[v] = v_exp1(v_fma1(sc[v], sl2, lq[v]));
+          });
+        }
+        if constexpr (g >= 2 && g < 10) {  // dS of pair p = g - 2, its P pair packed
+          constexpr int p = g - 2;
+          sfor<2>([&](auto jc) __attribute__((always_inline)) {
+            constexpr int v = 2 * p + decltype(jc)::value;
+            float t;
+            asm volatile("v_add_f32 %0, %1, %2\n\tv_mul_f32 %0, %3, %0" : "=&v"(t) : "v"(dc[v]), "v"(nd[v]), "v"(sc[v]));
+            dc[v] = t;
+          });
+          pw[HS][p >> 2][p & 3] = cvt_pk(sc[2 * p], sc[2 * p + 1]);
+        }
+        if constexpr (g >= 3 && g < 11) {
+          constexpr int p = g - 3;
+          dw[HS][p >> 2][p & 3] = cvt_pk(dc[2 * p], dc[2 * p + 1]);
+        }
+      };
+    };
+    auto no_valu = [](auto) __attribute__((always_inline)) {};
+    // dV / dK of key half H from the transposed fragments of slot `sl` (the first PF fetched by the S / dP phase
+    // before) || `valu` at each gap; `qsl` >= 0: the next S / dP phase's first Q rows, fetched at gaps 13 .. 15
+    auto g_phase = [&](auto hc, int sl, auto&& valu, int qsl) __attribute__((always_inline)) {
+      constexpr int H = decltype(hc)::value;
+      sfor<16>([&](auto gc) __attribute__((always_inline)) {
+        constexpr int i = decltype(gc)::value, s2 = (i / NDT) & 1, dt = i % NDT;
+        if constexpr (i < 2 * NDT)
+          asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                       :: "i"(d6_av(H, dt)), "i"(d6_av(H, dt) + 15), "v"(tf[i]), "v"(pw[H][s2]));
+        else
+          asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
+                       :: "i"(d6_ak(H, dt)), "i"(d6_ak(H, dt) + 15), "v"(tf[i]), "v"(dw[H][s2]));
+        if constexpr (i + PF < NB) tf[i + PF] = rd_t(sl, i + PF);
+        valu(gc);
+        if constexpr (i >= NB - PF) {
+          if (qsl >= 0) qf[i - (NB - PF)] = rd_q(qsl, i - (NB - PF));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    };
+    auto sd = [&](auto hc, int sl, int q0, int tsl) __attribute__((always_inline)) {
+      if (need_mask(q0, decltype(hc)::value))
+        sd_phase(hc, std::true_type{}, sl, q0, tsl);
+      else
+        sd_phase(hc, std::false_type{}, sl, q0, tsl);
+    };
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+
+    int sl_c = 0;  // ring slot of tile t
+    pref_q(0);
+    {  // tile 0: phase 2 without the previous tile's dV / dK
+      const int q0 = q0_of(0);
+      issue(NS - 2);
+      sd(H0{}, 0, q0, 0);
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // no MFMA between the chain and its reads
+      sfor<16>([&](auto gc) __attribute__((always_inline)) { sm_tail(H0{}, 0)(gc); });
+      pref_q(0);
+      sd(H1{}, 0, q0, 0);
+      wait_vm<2 * NDMA>();
+      ring_barrier();
+      g_phase(H0{}, 0, sm_tail(H1{}, 0), T > 1 ? 1 % NS : -1);
+    }
+    for (int t = 1; t < T; ++t) {
+      const int sl_p = sl_c;
+      sl_c = sl_c + 1 == NS ? 0 : sl_c + 1;
+      const int q0 = q0_of(t);
+      issue(sl_c + NS - 2 >= NS ? sl_c - 2 : sl_c + NS - 2);
+      sd(H0{}, sl_c, q0, sl_p);
+      g_phase(H1{}, sl_p, sm_tail(H0{}, sl_c), sl_c);
+      sd(H1{}, sl_c, q0, sl_c);
+      wait_vm<2 * NDMA>();  // tile t + 1 (issued three iterations ago) landed
+      ring_barrier();
+      const int sl_n = sl_c + 1 == NS ? 0 : sl_c + 1;
+      g_phase(H0{}, sl_c, sm_tail(H1{}, sl_c), t + 1 < T ? sl_n : -1);
+    }
+    {  // drain: the last tile's half 1
+#pragma unroll
+      for (int i = 0; i < PF; ++i) tf[i] = rd_t(sl_c, i);
+      asm volatile("s_nop 7" ::: "memory");  // the last packs -> MFMA operand reads
+      g_phase(H1{}, sl_c, no_valu, -1);
+    }
+    wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+  }
+  // the last asm MFMAs' accumulator writes -> the reads below
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32v16 dkt[NDT], dvt[NDT];
+    sfor<NDT>([&](auto dc_) __attribute__((always_inline)) {
+      constexpr int dt = decltype(dc_)::value;
+      sfor<16>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        float x, y;
+        if (h == 0) {
+          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(d6_ak(0, dt) + i));
+          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(y) : "i"(d6_av(0, dt) + i));
+        } else {
+          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(d6_ak(1, dt) + i));
+          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(y) : "i"(d6_av(1, dt) + i));
+        }
+        dkt[dt][i] = x;
+        dvt[dt][i] = y;
+      });
+    });
+    const int kr = kw + 32 * h + r;
+    if (a.rope_dk && kr < S) {  // fused RoPE: gradient of the unrotated k
+      const int p = rope_pos(a, b, kr);
+      rope_acc_inv<D>(dkt, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
+    }
+    uint2 wk[4 * NDT], wv[4 * NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int g = 4 * dt + c;
+        wk[g].x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
+        wk[g].y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
+        wv[g].x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
+        wv[g].y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
+      }
+    widen_pairs(wk);
+    widen_pairs(wv);
+    if (kr < S) {
+      store_pairs(a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh + 8 * hh, wk);
+      store_pairs(a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh + 8 * hh, wv);
+    }
+  }
+}
+
 #undef LLMT_ACLOB
 
 // ============================================================================ forward, head-chained
@@ -2845,6 +3312,12 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
     qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
     df[kk] = gload8(dop + (int64_t)min(qrow, S - 1) * a.d_ss + kk * 16 + hh * 8, qrow < S);
   }
+  if (a.rope_q && qrow < S) {
+    // fused RoPE: rotate the unrotated rows on load and hand them to the dK/dV pass (which stages Q through
+    // LDS-DMA, so it needs them rotated in memory)
+    const int p = rope_pos(a, b, qrow);
+    rope_frags<NKK>(qf, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
+  }
   if (a.ldw) {
     // the backward prep fused in: delta = rowsum(dO * O) from this lane's half row (64 of D elements, the
     // other half in lane r + 32), then the row constants of this wave's 32-row tile for the dK/dV kernel
@@ -3021,6 +3494,17 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
     }
   }
 
+  if (a.rope_q && qrow < S) {
+    // the rotated rows for the dK/dV pass, stored after the loop (the wave's vmcnt counts stores: at the start
+    // they held up its first DMA wait)
+    bf16* qo = a.qrot + (int64_t)b * a.qr_sb + (int64_t)h * a.qr_sh + (int64_t)qrow * a.qr_ss + hh * 8;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) *reinterpret_cast<bfv8*>(qo + kk * 16) = qf[kk];
+  }
+  if (a.rope_dq && qrow < S) {  // fused RoPE: gradient of the unrotated q
+    const int p = rope_pos(a, b, qrow);
+    rope_acc_inv<D>(dqt, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
+  }
   if constexpr (WS) {
     uint2 w[4 * NDT];
 #pragma unroll
@@ -3109,16 +3593,55 @@ static bool aligned16(const void* p, int64_t s0, int64_t s1, int64_t s2) {
   return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (s0 % 8 == 0) && (s1 % 8 == 0) && (s2 % 8 == 0);
 }
 
+// fused-RoPE arguments (AttnArgs::rpos ...); qrot: contiguous [B, S, Hq, D] scratch for rotated queries
+static void set_rope(AttnArgs& a, const void* rpos, int rpos64, int64_t rp_sb, int64_t rp_ss, const float* rcos,
+                     const float* rsin, int64_t rP, void* qrot, int D) {
+  a.rpos = rpos; a.rpos64 = rpos64; a.rp_sb = (int)rp_sb; a.rp_ss = (int)rp_ss;
+  a.rcos = rcos; a.rsin = rsin; a.rP = (int)rP;
+  a.qrot = (bf16*)qrot;
+  a.qr_sh = D; a.qr_ss = a.Hq * D; a.qr_sb = a.S * a.Hq * D;
+}
+static void rope_launch(const AttnArgs& a, const bf16* x, int x_sb, int x_ss, int x_sh, bf16* y, int y_sb, int y_ss,
+                        int y_sh, int H, int D, float sign, hipStream_t stream) {
+  const int64_t n = (int64_t)a.B * a.S * H * (D / 16);
+  rope_bshd_kernel<<<stream_grid(n, 256), 256, 0, stream>>>(a, x, x_sb, x_ss, x_sh, y, y_sb, y_ss, y_sh, H, D, sign);
+}
+// the rotated queries in qrot become the kernels' q
+static void use_qrot(AttnArgs& a) {
+  a.q = a.qrot; a.q_sb = a.qr_sb; a.q_ss = a.qr_ss; a.q_sh = a.qr_sh;
+}
+static bool rope_ok(const void* rpos, const float* rcos, const float* rsin, int64_t rP, int64_t rp_sb, int64_t rp_ss) {
+  if (!rcos) return rpos == nullptr && rsin == nullptr;
+  return rsin && rP > 0 && rP < 0x7fffffffLL && ((reinterpret_cast<uintptr_t>(rcos) | reinterpret_cast<uintptr_t>(rsin)) & 15) == 0 &&
+         strides32({rp_sb, rp_ss});
+}
+
+static int fwd_variant() {
+  const char* fve = getenv("LLMT_FA_FWD_VARIANT");
+  return fve ? atoi(fve) : 4;
+}
+// does the forward launch for this problem go to fa_fwd3_kernel (the kernel with the fused Q rotation)?
+static bool fwd_uses_fwd3(int D, int variant, bool drop, bool rmask, bool seg) {
+  if (drop) return false;
+  const bool chain = variant == 5 || variant == 6;
+  if (D == 64 || D == 96) return variant != 0 && !chain;
+  return !chain && !(variant == 10 && rmask && !seg) && (variant == 2 || variant == 3 || variant >= 4);
+}
+
 extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
                                           const int* seg, int B, int S, int Hq, int Hkv, int D, int64_t q_sb,
                                           int64_t q_ss, int64_t q_sh, int64_t k_sb, int64_t k_ss, int64_t k_sh,
                                           int64_t v_sb, int64_t v_ss, int64_t v_sh, int64_t o_sb, int64_t o_ss,
                                           int64_t o_sh, float scale, int causal, int window, int seg_runs,
-                                          float drop_p, uint32_t drop_seed, hipStream_t stream) {
+                                          float drop_p, uint32_t drop_seed, const void* rpos, int rpos64,
+                                          int64_t rp_sb, int64_t rp_ss, const float* rcos, const float* rsin,
+                                          int64_t rP, void* qrot, hipStream_t stream) {
   if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
   if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
       !aligned16(o, o_sb, o_ss, o_sh))
     return hipErrorInvalidValue;
+  if (!rope_ok(rpos, rcos, rsin, rP, rp_sb, rp_ss)) return hipErrorInvalidValue;
+  const bool rope = rcos != nullptr;
   if (!(drop_p >= 0.f && drop_p < 1.f)) return hipErrorInvalidValue;
   if (B == 0 || S == 0) return hipSuccess;
   if (!fits32(S, q_ss) || !fits32(S, k_ss) || !fits32(S, v_ss)) return hipErrorInvalidValue;
@@ -3144,11 +3667,22 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907 (variant 0), the
   // removed one-wave-per-SIMD ring forward 1.043; 3 = fwd3 with compiler-placed row-sum adds, 2 = with the
   // inline-asm adds (A/B reference); read per launch
-  const char* fve = getenv("LLMT_FA_FWD_VARIANT");
   // 4 = 3 with the widened O store tail (T21), in one process: B4 S8192 2.199 vs 2.203 ms, B32 S1024 0.429
   // vs 0.458, B64 S512 0.314 vs 0.343 ms (the per-block cost of short sequences / packed documents),
   // bitwise-equal output (profiles/r3_attention_wide_store_ab.jsonl)
-  const int variant = fve ? atoi(fve) : 4;  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
+  const int variant = fwd_variant();  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
+  if (rope) {
+    // fused RoPE: q holds unrotated queries (k is already rotated). fa_fwd3_kernel rotates its rows on load;
+    // every other kernel gets the rotated rows in the qrot scratch (q itself is never written)
+    set_rope(a, rpos, rpos64, rp_sb, rp_ss, rcos, rsin, rP, qrot, D);
+    if (fwd_uses_fwd3(D, variant, a.drop_thresh != 0, a.rmask, seg != nullptr)) {
+      a.rope_q = 1;
+    } else {
+      if (!qrot) return hipErrorInvalidValue;
+      rope_launch(a, a.q, a.q_sb, a.q_ss, a.q_sh, a.qrot, a.qr_sb, a.qr_ss, a.qr_sh, Hq, D, 1.f, stream);
+      use_qrot(a);
+    }
+  }
   // head chains (fa_fwd3c: 4 query heads per workgroup, bitwise-equal output) pay standalone where a
   // block's heads have their own K/V: MHA B8 S4096 H32 D128 1.567 -> 1.391 ms, D96 1.631 -> 1.245 ms; with
   // GQA they lose (B4 S8192 Hq32 Hkv8 2.230 -> 2.507 ms; profiles/r3_attention_head_chain_ab.jsonl). In the
@@ -3211,6 +3745,12 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   return hipGetLastError();
 }
 
+// 1: a forward with fused RoPE needs no qrot scratch (the launch goes to fa_fwd3_kernel)
+extern "C" int llmt_flash_attn_fwd_rope_inkernel(int D, float drop_p, int has_seg, int seg_runs) {
+  const bool rmask = range_masks() && (!has_seg || seg_runs);
+  return fwd_uses_fwd3(D, fwd_variant(), drop_p > 0.f, rmask, has_seg != 0) ? 1 : 0;
+}
+
 // floats of the `delta` workspace llmt_flash_attn_bwd needs
 extern "C" int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D) {
   const int64_t n = (int64_t)B * Hq * S;
@@ -3225,8 +3765,15 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
                                           int64_t o_ss, int64_t o_sh, int64_t dq_sb, int64_t dq_ss, int64_t dq_sh,
                                           int64_t dk_sb, int64_t dk_ss, int64_t dk_sh, int64_t dv_sb, int64_t dv_ss,
                                           int64_t dv_sh, float scale, int causal, int window, int seg_runs,
-                                          float drop_p, uint32_t drop_seed, hipStream_t stream) {
+                                          float drop_p, uint32_t drop_seed, const void* rpos, int rpos64,
+                                          int64_t rp_sb, int64_t rp_ss, const float* rcos, const float* rsin,
+                                          int64_t rP, void* qrot, hipStream_t stream) {
   if (!(drop_p >= 0.f && drop_p < 1.f)) return hipErrorInvalidValue;
+  if (!rope_ok(rpos, rcos, rsin, rP, rp_sb, rp_ss)) return hipErrorInvalidValue;
+  // rope: dq / dk are returned for the unrotated q / k. qun: q holds UNROTATED queries (the forward rotated
+  // them on load; qrot = scratch for the rotated rows); otherwise (qrot null) q / k are both rotated in
+  // memory and only the inverse rotation of the gradients is fused
+  const bool rope = rcos != nullptr, qun = rope && qrot != nullptr;
   if (Hkv <= 0 || Hq % Hkv) return hipErrorInvalidValue;
   if (!aligned16(q, q_sb, q_ss, q_sh) || !aligned16(k, k_sb, k_ss, k_sh) || !aligned16(v, v_sb, v_ss, v_sh) ||
       !aligned16(o, o_sb, o_ss, o_sh) || !aligned16(dout, o_sb, o_ss, o_sh) || !aligned16(dq, dq_sb, dq_ss, dq_sh) ||
@@ -3266,7 +3813,24 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   dim3 grid((S + 127) / 128, Hq, B);
   const int dgrid = stream_grid(nrows, 256);
   static const bool small_v3 = getenv("LLMT_FA_D96_GENERIC") == nullptr;  // A/B switch for D = 64 / 96
+  // fused RoPE: with qun the dQ kernel rotates its rows on load and writes them to qrot for the dK/dV
+  // kernel; the dQ / dK epilogues (dq3, dkdv5 / dkdv6) apply the inverse rotation. Other kernels: qrot by
+  // the standalone rotation, inverse passes after.
+  if (rope) set_rope(a, rpos, rpos64, rp_sb, rp_ss, rcos, rsin, rP, qrot, D);
+  auto rope_to_dkdv = [&](bool fused_dk) {  // after the dQ kernel: the dK/dV kernel reads qrot
+    if (!rope) return;
+    if (qun) use_qrot(a);
+    a.rope_q = a.rope_dq = 0;
+    a.rope_dk = fused_dk;
+  };
+  auto rope_finish_dk = [&](bool fused_dk) {
+    if (rope && !fused_dk) rope_launch(a, a.dk, a.dk_sb, a.dk_ss, a.dk_sh, a.dk, a.dk_sb, a.dk_ss, a.dk_sh, Hkv, D, -1.f, stream);
+  };
   if ((D == 128 || ((D == 96 || D == 64) && small_v3)) && !a.drop_thresh) {
+    if (rope) {
+      a.rope_q = qun;
+      a.rope_dq = 1;
+    }
     // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws)
     float* ld = delta + nrows;
     const int64_t nT = (S + 31) / 32;
@@ -3286,6 +3850,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
         fa_bwd_dq3_kernel<96, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      const bool f5 = dkdv_variant() == 5;
+      rope_to_dkdv(f5);
       if (dkdv_variant() == 5 && a.rmask)
         fa_bwd_dkdv5_kernel<96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else if (dkdv_variant() == 5)
@@ -3294,6 +3860,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dkdv128_kernel<3, 96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
         fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      rope_finish_dk(f5);
       return hipGetLastError();
     }
     if (D == 64) {
@@ -3302,6 +3869,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       else
         fa_bwd_dq3_kernel<64, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
+      const bool f5 = dkdv_variant() == 5;
+      rope_to_dkdv(f5);
       if (dkdv_variant() == 5 && a.rmask)
         fa_bwd_dkdv5_kernel<64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else if (dkdv_variant() == 5)
@@ -3310,6 +3879,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dkdv128_kernel<3, 64, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else
         fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      rope_finish_dk(f5);
       return hipGetLastError();
     }
     prep(std::integral_constant<int, 128>{});
@@ -3336,9 +3906,15 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<128, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
     }
     const int variant = dkdv_variant();
+    // 7 = 64 keys per wave with asm-owned accumulators (fa_bwd_dkdv6_kernel), dense rows
+    const bool v6 = variant == 7 && a.rmask && !seg;
+    const bool f5 = variant == 5 || (variant == 6 && a.rmask) || v6;
+    rope_to_dkdv(f5);
     // dense rows: an 8-slot Q / dO ring (tiles 6 ahead; B4 S8192 backward 7.605 -> 7.544 ms in one process,
     // 7 slots 7.572); packed rows keep 6 (their key blocks often visit only a few tiles)
-    if (variant == 6 && a.rmask && !seg)
+    if (v6)
+      fa_bwd_dkdv6_kernel<128><<<(S + 255) / 256 * Hkv * B, 256, 0, stream>>>(a, ld);
+    else if (variant == 6 && a.rmask && !seg)
       fa_bwd_dkdv5_kernel<128, false, 8, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 6 && a.rmask)
       fa_bwd_dkdv5_kernel<128, false, 6, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
@@ -3354,9 +3930,14 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       fa_bwd_dkdv128_kernel<3, 128, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else
       fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+    rope_finish_dk(f5);
     return hipGetLastError();
   }
   if (gqa && !work) return hipErrorInvalidValue;
+  if (qun) {  // the generic kernels: rotated queries in qrot, inverse passes over dq / dk below
+    rope_launch(a, a.q, a.q_sb, a.q_ss, a.q_sh, a.qrot, a.qr_sb, a.qr_ss, a.qr_sh, Hq, D, 1.f, stream);
+    use_qrot(a);
+  }
 #define LLMT_BWD(DD)                                                                              \
   fa_bwd_delta_kernel<DD><<<dgrid, 256, 0, stream>>>(a);                                          \
   fa_bwd_dq_kernel<DD><<<grid, 256, 0, stream>>>(a);                                              \
@@ -3373,5 +3954,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     default: return hipErrorInvalidValue;
   }
 #undef LLMT_BWD
+  if (rope) {
+    rope_launch(a, a.out, a.dq_sb, a.dq_ss, a.dq_sh, a.out, a.dq_sb, a.dq_ss, a.dq_sh, Hq, D, -1.f, stream);
+    rope_finish_dk(false);
+  }
   return hipGetLastError();
 }

@@ -117,7 +117,7 @@ class LlamaAttention(nn.Module):
         def core(t):
             return F_.rope_attention(t, rt["positions"], rt["cos"], rt["sin"], self.nq, self.nkv, causal=True,
                                      segment_ids=rt["segment_ids"], window=rt.get("window", -1), impl=rt["impl"],
-                                     seg_info=rt.get("seg_info"),
+                                     seg_info=rt.get("seg_info"), rope_tok=rt.get("rope_tok"),
                                      dropout_p=self.cfg.attention_dropout if self.training else 0.0)
 
         if rt.get("selective") and rt["impl"] != "flash" and self.training and torch.is_grad_enabled():
@@ -276,11 +276,14 @@ class Llama(BaseModel):
         cos, sin = self.rope.get(device, max(S, n_pos), ntk_positions=n_pos)
         impl = self.config.resolved_attn_implementation(device.type)
         selective = self.gradient_checkpointing and self.config.recompute_granularity == "selective"
-        seg_info = None
-        if segment_ids is not None and device.type == "cuda" and impl in ("flash", "flash_attention_2", "hip"):
-            seg_info = F_.segment_info(segment_ids)  # run bounds, shared by every layer's attention
+        seg_info = rope_tok = None
+        if device.type == "cuda" and impl in ("flash", "flash_attention_2", "hip"):
+            if segment_ids is not None:
+                seg_info = F_.segment_info(segment_ids)  # run bounds, shared by every layer's attention
+            if F_.ROPE_FUSED[0] != "off":  # per-token RoPE table rows for the attention kernels, shared by every layer
+                rope_tok = F_.rope_token_tables(position_ids, cos, sin)
         return {"positions": position_ids, "cos": cos, "sin": sin, "segment_ids": segment_ids, "impl": impl,
-                "selective": selective, "seg_info": seg_info}
+                "selective": selective, "seg_info": seg_info, "rope_tok": rope_tok}
 
     def hidden_states(self, input_ids=None, position_ids=None, segment_ids=None, inputs_embeds=None,
                       gather_sequence: bool = True, embed_hook=None):

@@ -624,14 +624,41 @@ def swiglu(gate_up: torch.Tensor, dy_t_consumer: bool = False) -> torch.Tensor:
 
 # ----------------------------------------------------------------------------- RoPE + flash attention
 
+# RoPE inside the attention kernels (see _RopeFlashAttnFn), LLMT_ROPE_FUSED:
+#   "bwd"  the forward rotates q / k in place by the standalone kernel; the dQ / dK epilogues apply the
+#          inverse rotation (no pass over dq / dk);
+#   "full" only k is rotated by the standalone kernel; the forward / dQ kernels rotate their q rows on load
+#          (the dQ kernel hands the rotated rows to the dK/dV kernel), the epilogues as "bwd";
+#   "auto" (default) "full" for D = 128, "bwd" otherwise — the faster form of each in same-process A/B
+#          (profiles/r5_rope_fused.md: Llama-3-8B fwd + bwd 10.03 / 10.13 / 10.14 ms full / bwd / off;
+#          Phi-3 packed D96 3.15 / 3.12 / 3.22 ms);
+#   "off"  the standalone passes over q / k and dq / dk (A/B reference).
+_RF = os.environ.get("LLMT_ROPE_FUSED", "auto").strip().lower()
+ROPE_FUSED = ["off" if _RF in ("0", "false", "off") else (_RF if _RF in ("full", "bwd") else "auto")]
+
+
+def _rope_mode(D: int) -> str:
+    m = ROPE_FUSED[0]
+    return ("full" if D == 128 else "bwd") if m == "auto" else m
+
 
 class _RopeFlashAttnFn(Function):
     """qkv [B, S, Hq+2Hkv, D] (fused QKV GEMM output) -> attention output [B, S, Hq, D].
 
-    RoPE is applied IN PLACE to the q and k heads of ``qkv`` (the buffer has no other consumer: the
-    QKV GEMM's backward needs its input, not its output), then the flash kernels read q/k/v as strided
-    views of the same buffer. The backward writes dq/dk/dv into one fused dQKV buffer and un-rotates
-    it in place, producing exactly the gradient of the QKV GEMM output.
+    RoPE (reference ``ops/rope_op.py:10-20``, applied at ``models/llama/llama_model.py:553``) is fused into
+    the attention kernels (``ROPE_FUSED``): by default ("bwd") the forward rotates q / k in place with the
+    standalone kernel and the dQ / dK epilogues apply the inverse rotation; with "full":
+      * the k heads are rotated IN PLACE by the standalone kernel (the buffer has no other consumer: the QKV
+        GEMM's backward needs its input, not its output) — the forward and dQ kernels stage K through
+        LDS-DMA, so K must sit rotated in memory;
+      * the q heads stay unrotated in ``qkv``: the forward kernel rotates its rows as it loads them, the dQ
+        kernel does the same and writes the rotated rows to a scratch buffer for the dK/dV kernel;
+      * the dQ and dK epilogues apply the inverse rotation, so the backward writes the gradient of the QKV
+        GEMM output directly (no inverse pass over dQKV).
+    "full" leaves ``qkv`` consistent under selective recompute (the saved buffer never depends on whether the
+    attention forward ran), but its on-load rotation costs the forward / dQ kernels about what the q pass
+    costs (per-WG table reads of 2x the Q bytes), so "bwd" is the default
+    (profiles/r5_rope_fused.md).
     """
 
     # Activations are sequence-major: qkv is [S, B, Htot, D] contiguous, positions [S, B]. The flash
@@ -640,20 +667,37 @@ class _RopeFlashAttnFn(Function):
     # bm=True: a batch-major buffer [B, S, Htot, D] (transformers' layout), positions [B * S] in the same
     # token order; O comes back batch-major [B, S, Hq, D]
     @staticmethod
-    def forward(ctx, qkv, pos, cos, sin, seg, nq, nkv, causal, window, scale, dropout_p=0.0, seed=0, bm=False):
+    def forward(ctx, qkv, pos, cos, sin, seg, nq, nkv, causal, window, scale, dropout_p=0.0, seed=0, bm=False,
+                tok=None):
+        # tok: per-token tables (ct, st, sb, ss) whose row b * sb + s * ss is token (b, s)'s cos / sin (see
+        # rope_token_tables); None -> the kernels index cos / sin through pos
         L = lib()
-        L.rope_(qkv, pos, cos, sin, nq + nkv, False)
+        mode = _rope_mode(qkv.shape[-1])
+        if mode == "full":
+            L.rope_(qkv[..., nq:nq + nkv, :], pos, cos, sin, nkv, False)  # the k heads only
+        else:
+            L.rope_(qkv, pos, cos, sin, nq + nkv, False)
         x = qkv if bm else qkv.transpose(0, 1)
         q, k, v = x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:]
-        o, lse = L.flash_attn_fwd(q, k, v, seg, scale, causal, window, dropout_p, seed)
+        if mode != "off":
+            if tok is None:  # positions of token (b, s): pos[b * S + s] (batch-major) or pos[s * B + b] (seq-major)
+                B, S = q.shape[0], q.shape[1]
+                rp, rc, rs, (sb, ss) = pos, cos, sin, ((S, 1) if bm else (1, B))
+            else:
+                rp, (rc, rs, sb, ss) = None, tok
+            ctx.rope = (rp, rc, rs, sb, ss)
+        if mode == "full":
+            o, lse = L.flash_attn_fwd(q, k, v, seg, scale, causal, window, dropout_p, seed, *ctx.rope)
+        else:
+            o, lse = L.flash_attn_fwd(q, k, v, seg, scale, causal, window, dropout_p, seed)
         ctx.save_for_backward(qkv, o, lse, pos, cos, sin, seg)
-        ctx.cfg = (nq, nkv, causal, window, scale, dropout_p, seed, bm)
+        ctx.cfg = (nq, nkv, causal, window, scale, dropout_p, seed, bm, mode)
         return o if bm else o.transpose(0, 1)
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse, pos, cos, sin, seg = ctx.saved_tensors
-        nq, nkv, causal, window, scale, dropout_p, seed, bm = ctx.cfg
+        nq, nkv, causal, window, scale, dropout_p, seed, bm, mode = ctx.cfg
         L = lib()
         if not bm:
             do = do.transpose(0, 1)
@@ -663,10 +707,14 @@ class _RopeFlashAttnFn(Function):
             do = do.as_strided(o.shape, o.stride())  # differs only in the strides of size-1 dims
         dqkv = torch.empty_like(qkv)
         x, dx = (qkv, dqkv) if bm else (qkv.transpose(0, 1), dqkv.transpose(0, 1))
-        L.flash_attn_bwd(x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:], o, do, lse, seg, dx[:, :, :nq],
-                         dx[:, :, nq:nq + nkv], dx[:, :, nq + nkv:], scale, causal, window, dropout_p, seed)
-        L.rope_(dqkv, pos, cos, sin, nq + nkv, True)
-        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
+        args = (x[:, :, :nq], x[:, :, nq:nq + nkv], x[:, :, nq + nkv:], o, do, lse, seg, dx[:, :, :nq],
+                dx[:, :, nq:nq + nkv], dx[:, :, nq + nkv:], scale, causal, window, dropout_p, seed)
+        if mode != "off":  # q unrotated ("full") or both rotated in memory ("bwd")
+            L.flash_attn_bwd(*args, *ctx.rope, mode == "bwd")
+        else:
+            L.flash_attn_bwd(*args)
+            L.rope_(dqkv, pos, cos, sin, nq + nkv, True)
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -770,14 +818,25 @@ def rope_tables_to_full(cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor)
     return torch.cat([c, c], -1), torch.cat([s, s], -1)
 
 
+def rope_token_tables(positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor):
+    """Per-token rows of the half-width tables for the attention kernels' fused RoPE: (cos[pos], sin[pos],
+    sb, ss) in the seq-major token order of the fused QKV buffer (row s * B + b). Computed once per forward
+    (the model's runtime dict) and shared by every layer, so the kernels read a token's table row directly
+    instead of through its position id."""
+    B, S = positions.shape
+    p = positions.t().reshape(-1).clamp(0, cos.shape[0] - 1)
+    return cos.index_select(0, p), sin.index_select(0, p), 1, B
+
+
 def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool = True, segment_ids=None,
                    window: int = -1, scale: float | None = None, impl: str = "flash", seg_info=None,
-                   dropout_p: float = 0.0):
+                   dropout_p: float = 0.0, rope_tok=None):
     """Fused RoPE + attention on the SEQ-MAJOR fused QKV buffer [S, B, n_q + 2 n_kv, D] -> [S, B, n_q, D].
 
     ``cos``/``sin``: fp32 half-width tables [max_pos, D/2]; ``positions``: [B, S] int;
     ``segment_ids``: optional [B, S] (tokens attend only within their contiguous run of equal ids);
-    ``seg_info``: its precomputed :func:`segment_info` (shared across layers); ``dropout_p``: attention
+    ``seg_info``: its precomputed :func:`segment_info` (shared across layers); ``rope_tok``: the
+    precomputed :func:`rope_token_tables` (shared across layers); ``dropout_p``: attention
     dropout on the probabilities (reference ``attention_dropout``, llama_model.py:593-621 — FA2 / SDPA
     ``dropout_p``): in the HIP kernels on the GPU (the generic forward / backward kernels, which carry the
     keep-mask hash), SDPA with dropout on the CPU / SDPA paths.
@@ -790,7 +849,8 @@ def rope_attention(qkv, positions, cos, sin, n_q: int, n_kv: int, causal: bool =
         pos = positions.t().contiguous().reshape(-1)
         seg = _native_seg(segment_ids, seg_info)
         seed = dropout_seed() if dropout_p > 0 else 0
-        return _RopeFlashAttnFn.apply(qkv, pos, cos, sin, seg, n_q, n_kv, causal, win, scale, float(dropout_p), seed)
+        return _RopeFlashAttnFn.apply(qkv, pos, cos, sin, seg, n_q, n_kv, causal, win, scale, float(dropout_p), seed,
+                                      False, rope_tok)
     if dropout_p > 0:
         return _ref_rope_attention(qkv.transpose(0, 1), positions, cos, sin, n_q, n_kv, causal, segment_ids, win,
                                    scale, "sdpa", dropout_p).transpose(0, 1)
@@ -823,9 +883,9 @@ def rope_attention_bm(qkv, cos, sin, n_q: int, n_kv: int, segment_ids=None, wind
                       scale: float | None = None, dropout_p: float = 0.0):
     """Causal fused RoPE + attention on a BATCH-MAJOR fused QKV buffer [B, S, n_q + 2 n_kv, D] (the HF
     decoder layer's layout) with transformers' rotary tables ``cos`` / ``sin`` [B or 1, S, D] -> [B, S, n_q, D].
-    The same kernels as :func:`rope_attention` (in-place RoPE on the q / k heads, flash attention on strided
-    views, un-rotation of dQKV in the backward), fed per-token tables so any rope_type / scaling the model's
-    rotary embedding computed applies unchanged."""
+    The same kernels as :func:`rope_attention` (RoPE fused into the flash kernels on strided views of the
+    buffer, see _RopeFlashAttnFn), fed per-token tables so any rope_type / scaling the model's rotary
+    embedding computed applies unchanged."""
     B, S, _, D = qkv.shape
     ct, st, pos = _token_tables(cos, sin, B, S)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -834,8 +894,10 @@ def rope_attention_bm(qkv, cos, sin, n_q: int, n_kv: int, segment_ids=None, wind
         qkv = qkv.contiguous()
         seg = _native_seg(segment_ids, None)
         seed = dropout_seed() if dropout_p > 0 else 0
+        # ct / st are already per-token rows (row b * S + s, or s when the tables are shared by the batch)
+        tok = (ct, st, S if ct.shape[0] == B * S and B > 1 else 0, 1)
         return _RopeFlashAttnFn.apply(qkv, pos.reshape(-1).contiguous(), ct, st, seg, n_q, n_kv, True, win, scale,
-                                      float(dropout_p), seed, True)
+                                      float(dropout_p), seed, True, tok)
     return _ref_rope_attention(qkv, pos, ct, st, n_q, n_kv, True, segment_ids, win, scale, "sdpa", dropout_p)
 
 
