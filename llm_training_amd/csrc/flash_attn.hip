@@ -2632,25 +2632,29 @@ __global__ __launch_bounds__(256, 1) void fa_fwd4_kernel(AttnArgs a) {
 }
 // ============================================================================ backward dK/dV, v6
 // 64 keys per wave (two 32-key halves), dV^T and dK^T of both halves in the 256 accumulator registers
-// (asm-owned, like fa_fwd4: a[0:127] dV^T, a[128:255] dK^T), so every Q^T / dO^T transposed fragment read
-// from LDS feeds two MFMAs (one per key half) where fa_bwd_dkdv5 feeds one, and a 256-key workgroup of 4
-// waves moves each Q / dO tile through the LDS-DMA ring for twice the keys (cdna guide, 'Attention
-// backward': 64 keys per wave in 256 accumulator registers). The wave's K fragments stay in VGPRs (64
-// registers); V of the workgroup's 256 keys sits in LDS (a 64 KB swizzled image, the dP operand), next to a
-// 5-slot Q / dO ring (tiles issued 3 ahead). Per 32-row query tile t, four phases of 16 MFMAs:
-//   1  S chain, then dP chain of key half 0 (tile t)  || in the dP gaps: mask, P = exp2(...) of half 0
-//   2  dV / dK of half 1 (tile t-1)                    || dS of half 0, bf16 P / dS of half 0
-//   3  S chain, then dP chain of key half 1 (tile t)  || P of half 1
-//      (ring wait + barrier: tile t+1 landed)
-//   4  dV / dK of half 0 (tile t)                      || dS, bf16 P / dS of half 1
-// One fp32 score set (S, dP: 32 registers) serves both halves: each half's softmax ends in the phase after
-// its chains. Operand reads run three MFMAs ahead of their use (the LDS latency under load); one
-// accumulation chain per MFMA shape needs no interleaving (MI355X_MICROARCH: 32 cycles back to back on one
-// accumulator). Dense rows only (D = 128, causal / window, no segments): packed rows keep fa_bwd_dkdv5.
+// (asm-owned, like fa_fwd4: a[0:127] dV^T, a[128:255] dK^T). Every operand fragment read from LDS (Q / dO
+// rows, Q^T / dO^T transposed) feeds the two halves' MFMAs back to back, so a tile needs 1.1 LDS reads per
+// MFMA against fa_bwd_dkdv5's 1.75, and a 256-key workgroup of 4 waves moves each Q / dO tile through the
+// LDS-DMA ring for twice the keys (cdna guide, 'Attention backward': 64 keys per wave in 256 accumulator
+// registers). The wave's K fragments stay in VGPRs (64 registers); V of the workgroup's 256 keys sits in LDS
+// (a 64 KB swizzled image, the dP operand) next to a 5-slot Q / dO ring (tiles issued 3 ahead). Per 32-row
+// query tile t, four phases of 16 MFMAs:
+//   1  S(t), both halves (one accumulation chain each, interleaved per k-step: one Q row read per pair)
+//                                          || dS(t-1) of k-step 1 and its bf16 pairs
+//   2  dP(t), both halves                  || P = exp2(S scale log2e - lse log2e) of k-step 0, bf16 pairs
+//   3  dK(t-1) from Q^T(t-1) and dS(t-1)   || P of k-step 1, bf16 pairs
+//      (ring wait + barrier: tile t+1 landed, tile t-1's slot free)
+//   4  dV(t) from dO^T(t) and P(t)         || dS(t) of k-step 0 and its bf16 pairs
+// (diagnostic probes with everything but the MFMAs and the packs removed put the MFMA floor of this loop at
+// ~55 % of its time: the softmax VALU must spread over all four phases to hide under the MFMAs)
+// The fp32 scores of both halves (S / P, dP / dS: 64 registers) live from phase 1 to phase 4; the bf16 P and
+// dS operands (32 registers) from their pack to their MFMAs. Operand reads run two to three MFMAs ahead (LDS
+// latency under load); one accumulation chain needs no interleaving for throughput (MI355X_MICROARCH: 32
+// cycles back to back on one accumulator). Dense rows only (D = 128, causal / window, no segments).
 constexpr int d6_av(int h, int dt) { return (h * 4 + dt) * 16; }        // dV^T accumulator (key half, d tile)
 constexpr int d6_ak(int h, int dt) { return 128 + (h * 4 + dt) * 16; }  // dK^T accumulator
 
-template <int D = 128, int PF = 3>
+template <int D = 128, int PF = 3, int PR = 0, bool DI = false>
 __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const float* ld) {
   static_assert(D == 128, "fa_bwd_dkdv6 is the D = 128 kernel");
   constexpr int NKK = 8, NDT = 4, NB = 16;
@@ -2688,10 +2692,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
       for (int kk = 0; kk < NKK; ++kk) kf[h][kk] = gload8(kp + (int64_t)min(key, S - 1) * a.k_ss + kk * 16 + hh * 8, key < S);
     }
   }
-  // query range of each half's key (range masks) and the block's query tiles
-  int qlo[2], qhi[2];
-  query_interval(a, b, kw + r, qlo[0], qhi[0]);
-  query_interval(a, b, kw + 32 + r, qlo[1], qhi[1]);
+  // the block's query tiles (dense rows: the range masks' query intervals are recomputed where a tile needs them)
   const int q_beg = a.causal ? ks : 0;
   const int q_end = a.window >= 0 ? min(S, ks + 256 + a.window) : S;
   const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
@@ -2699,19 +2700,20 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
   // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[0][kk]), "+v"(kf[1][kk]));
-  asm volatile("" : "+v"(qlo[0]), "+v"(qhi[0]), "+v"(qlo[1]), "+v"(qhi[1]));
 
   if (T > 0) {
-    int dq_off[2], dd_off[2];
+    // per-lane DMA offsets, recomputed per tile (a handful of VALU ops beside the MFMAs; held across the loop they
+    // cost five of the registers the pipeline needs)
+    auto dma_offs = [&](int (&dq)[2], int (&dd)[2], int& dl) __attribute__((always_inline)) {
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int row = 8 * wid + 4 * n + (lane >> 4);
-      const int ch = (lane & 15) ^ QI::swz(row);
-      dq_off[n] = (row * a.q_ss + ch * 8) * 2;
-      dd_off[n] = (row * a.d_ss + ch * 8) * 2;
-    }
-    const int ld_off = ((wid & 1) * 64 + lane) * 4;
-    asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]));
+      for (int n = 0; n < 2; ++n) {
+        const int row = 8 * wid + 4 * n + (lane >> 4);
+        const int ch = (lane & 15) ^ QI::swz(row);
+        dq[n] = (row * a.q_ss + ch * 8) * 2;
+        dd[n] = (row * a.d_ss + ch * 8) * 2;
+      }
+      dl = ((wid & 1) * 64 + lane) * 4;
+    };
     const int64_t q_rows = S - q_beg;
     const int64_t nrec_q = ((q_rows - 1) * a.q_ss + D) * 2, nrec_d = ((q_rows - 1) * a.d_ss + D) * 2;
     const int64_t nrec_l = (int64_t)nq * kLdTile * 4;
@@ -2725,6 +2727,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
     // issues the same number of pieces, so one counted wait fits every iteration)
     auto issue = [&](int sl) __attribute__((always_inline)) {
       const char* q0 = ring + sl * SLOT + 8 * wid * 256;
+      int dq_off[2], dd_off[2], ld_off;
+      dma_offs(dq_off, dd_off, ld_off);
+      asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]), "+v"(ld_off));
       dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, ring + sl * SLOT + 2 * IMG + (wid & 1) * 256,
                 dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
       if (++iss_n < T) {
@@ -2768,183 +2773,251 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
       to0[1] = QI::toff(BM, row + 8, col);
     }
     const char* vimg = smem + 64 * wid * 256;
-    auto rd_q = [&](int sl, int kk) __attribute__((always_inline)) { return lds_b128(ring + sl * SLOT + (ro0 ^ (32 * kk))); };
-    auto rd_d = [&](int sl, int kk) __attribute__((always_inline)) { return lds_b128(ring + sl * SLOT + IMG + (ro0 ^ (32 * kk))); };
-    auto rd_v = [&](int h, int kk) __attribute__((always_inline)) { return lds_b128(vimg + 32 * 256 * h + (ro0 ^ (32 * kk))); };
+    auto rd_q = [&](int sl, int kk) __attribute__((always_inline)) {
+      if constexpr (PR & 8) return kf[1][kk & 7];
+      return lds_b128(ring + sl * SLOT + (ro0 ^ (32 * kk)));
+    };
+    auto rd_d = [&](int sl, int kk) __attribute__((always_inline)) {
+      if constexpr (PR & 8) return kf[0][kk & 7];
+      return lds_b128(ring + sl * SLOT + IMG + (ro0 ^ (32 * kk)));
+    };
+    auto rd_v = [&](int h, int kk) __attribute__((always_inline)) {
+      if constexpr (PR & 8) return kf[h][(kk + 1) & 7];
+      return lds_b128(vimg + 32 * 256 * h + (ro0 ^ (32 * kk)));
+    };
     // transposed fragment i of a dV / dK phase: i < 8 -> dO^T (dV product), else Q^T (dK); s2 = (i / 4) & 1
     auto rd_t = [&](int sl, int i) __attribute__((always_inline)) -> bfv8 {
+      if constexpr (PR & 8) return kf[i & 1][i & 7];
       const int s2 = (i / NDT) & 1, dt = i % NDT;
       const char* base = ring + sl * SLOT + (i < 2 * NDT ? IMG : 0) + 4096 * s2;
       const s16v4 lo = lds_tr(base + (to0[0] ^ (64 * dt))), hi = lds_tr(base + (to0[1] ^ (64 * dt)));
       return __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     };
 
-    f32v16 sc, dc;             // S (then P) and dP (then dS) of the half in flight
+    f32v16 sc[2], dc[2];       // S and dP - delta of both key halves (the MFMA chains' accumulators)
+    f32v16 cdc;                // DI: -delta of the lane's 16 query rows, the dP chains' initial accumulator
+    const float* nds = nullptr;  // !DI: -delta of the tile whose dS is computed (LDS)
+    float pv[2][16], dsv[2][16];  // P and dS element-wise (scalars: no vector re-assembly around the updates)
     u32x4 pw[2][2], dw[2][2];  // bf16 P / dS operands [key half][k-step]
-    float lq[16], nd[16];      // the tile's row constants (-lse log2e, -delta) for the half in flight
-    bfv8 qf[NKK], df[NKK], vf[NKK], tf[NB];
+    const float* lqs = nullptr;  // the tile's row constants in LDS: -lse log2e (floats 96 ..), -delta (32 ..)
+    bfv8 qf[NKK], df[NKK], vf[2][NKK], tf[8];
     auto q0_of = [&](int t) __attribute__((always_inline)) { return q_beg + (t % nq) * BM; };
-    auto need_mask = [&](int q0, int H) __attribute__((always_inline)) {
-      const int k0 = kw + 32 * H;
-      return (a.causal && q0 < k0 + 31) || (a.window >= 0 && q0 + 31 - k0 > a.window);
+    auto need_mask = [&](int q0) __attribute__((always_inline)) {
+      return (a.causal && q0 < kw + 63) || (a.window >= 0 && q0 + 31 - kw > a.window);
     };
-    auto pref_q = [&](int sl) __attribute__((always_inline)) {
-#pragma unroll
-      for (int kk = 0; kk < PF; ++kk) qf[kk] = rd_q(sl, kk);
+    // exp element e of a tile (k-step e >> 4, half (e >> 3) & 1, value 8 k-step + (e & 7))
+    // row constant pair of values v, v + 1 (v even): rows 8 (v >> 2) + 4 hh + (v & 3), adjacent floats
+    auto cpair = [&](const float* base, int v) __attribute__((always_inline)) {
+      return *reinterpret_cast<const float2*>(base + 8 * (v >> 2) + 4 * hh + (v & 3));
     };
-
-    // S chain then dP chain of key half H (tile in slot sl), P = exp2(S * scale * log2e - lse * log2e) of its
-    // first 12 elements in the dP gaps (from gap 10: two MFMAs behind the last S MFMA, the XDL-write ->
-    // VALU-read wait states); MSK: the tile needs the range mask (diagonal / window), applied at gap 9.
-    // `tsl`: the slot whose first transposed fragments the next (dV / dK) phase reads, fetched at gaps 13 .. 15
-    auto sd_phase = [&](auto hc, auto mc, int sl, int q0, int tsl) __attribute__((always_inline)) {
-      constexpr int H = decltype(hc)::value;
-      constexpr bool MSK = decltype(mc)::value;
-      const float* Ls = reinterpret_cast<const float*>(ring + sl * SLOT + 2 * IMG);
+    // exps of the element pair e, e + 1 (e even)
+    auto ex2 = [&](auto ec) __attribute__((always_inline)) {
+      constexpr int e = decltype(ec)::value, h = (e >> 3) & 1, v = 8 * (e >> 4) + (e & 7);
+      if constexpr (PR & 4) return;
+      const float2 l = cpair(lqs, v);
+      float e0, e1;
+      asm volatile("v_fma_f32 %0, %2, %4, %5\n\tv_fma_f32 %1, %3, %4, %6\n\tv_exp_f32 %0, %0\n\tv_exp_f32 %1, %1"
+                   : "=&v"(e0), "=&v"(e1)
+                   : "v"(pv[h][v]), "v"(pv[h][v + 1]), "v"(sl2), "v"(l.x), "v"(l.y));
+      pv[h][v] = e0;
+      pv[h][v + 1] = e1;
+    };
+    // dS = P (dP - delta) of the pair e, e + 1
+    auto ds2 = [&](auto ec) __attribute__((always_inline)) {
+      constexpr int e = decltype(ec)::value, h = (e >> 3) & 1, v = 8 * (e >> 4) + (e & 7);
+      if constexpr (PR & 4) {
+        dsv[h][v] = dc[h][v];
+        dsv[h][v + 1] = dc[h][v + 1];
+        return;
+      }
+      float t0, t1;
+      if constexpr (DI) {  // dc already holds dP - delta (the dP chains start from -delta, see ph_s)
+        asm volatile("v_mul_f32 %0, %2, %3\n\tv_mul_f32 %1, %4, %5"
+                     : "=&v"(t0), "=&v"(t1) : "v"(dc[h][v]), "v"(pv[h][v]), "v"(dc[h][v + 1]), "v"(pv[h][v + 1]));
+      } else {
+        const float2 n = cpair(nds, v);
+        asm volatile("v_add_f32 %0, %2, %3\n\tv_add_f32 %1, %4, %5\n\tv_mul_f32 %0, %6, %0\n\tv_mul_f32 %1, %7, %1"
+                     : "=&v"(t0), "=&v"(t1)
+                     : "v"(dc[h][v]), "v"(n.x), "v"(dc[h][v + 1]), "v"(n.y), "v"(pv[h][v]), "v"(pv[h][v + 1]));
+      }
+      dsv[h][v] = t0;
+      dsv[h][v + 1] = t1;
+    };
+    // bf16 pair w of a tile's operands (k-step w >> 3, half (w >> 2) & 1, word w & 3)
+    auto pk_p = [&](auto wc) __attribute__((always_inline)) {
+      constexpr int w = decltype(wc)::value, s2 = w >> 3, h = (w >> 2) & 1, j = w & 3, v = 8 * s2 + 2 * j;
+      pw[h][s2][j] = cvt_pk(pv[h][v], pv[h][v + 1]);
+    };
+    auto pk_d = [&](auto wc) __attribute__((always_inline)) {
+      constexpr int w = decltype(wc)::value, s2 = w >> 3, h = (w >> 2) & 1, j = w & 3, v = 8 * s2 + 2 * j;
+      dw[h][s2][j] = cvt_pk(dsv[h][v], dsv[h][v + 1]);
+    };
+    auto consts_of = [&](int sl, int off) __attribute__((always_inline)) {
+      return reinterpret_cast<const float*>(ring + sl * SLOT + 2 * IMG) + off;
+    };
+    // phase 1: S(t) of both halves (tile in slot sl; Q rows 0, 1 prefetched), the dP operands' first k-steps
+    // and -lse log2e fetched in its gaps
+    auto ph_s = [&](int sl, auto&& valu) __attribute__((always_inline)) {
+      lqs = consts_of(sl, 96);
       sfor<16>([&](auto gc) __attribute__((always_inline)) {
-        constexpr int g = decltype(gc)::value;
-        if constexpr (g < NKK) {
-          if constexpr (g == 0)
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(sc) : "v"(qf[0]), "v"(kf[H][0]));
-          else
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sc) : "v"(qf[g]), "v"(kf[H][g]));
-          if constexpr (g + PF < NKK) qf[g + PF] = rd_q(sl, g + PF);
-          if constexpr (g >= NKK - PF) {  // the dP chain's first operands
-            constexpr int k2 = g - (NKK - PF);
-            df[k2] = rd_d(sl, k2);
-            vf[k2] = rd_v(H, k2);
-          }
-          if constexpr (g == 1 || g == 2) {  // -lse * log2e of the tile's rows (floats 96 ..)
+        constexpr int g = decltype(gc)::value, kk = g >> 1, h = g & 1;
+        valu(gc);
+        if constexpr (kk == 0)
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(sc[h]) : "v"(qf[0]), "v"(kf[h][0]));
+        else
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sc[h]) : "v"(qf[kk]), "v"(kf[h][kk]));
+        if constexpr (h == 0 && kk + 2 < NKK) qf[kk + 2] = rd_q(sl, kk + 2);
+        if constexpr (DI && g >= 14) {  // -delta of the tile's rows (floats 32 ..): the dP chains' initial value
 #pragma unroll
-            for (int c = 2 * (g - 1); c < 2 * g; ++c) {
-              const float4 l4 = *reinterpret_cast<const float4*>(Ls + 96 + 8 * c + 4 * hh);
-              lq[4 * c] = l4.x; lq[4 * c + 1] = l4.y; lq[4 * c + 2] = l4.z; lq[4 * c + 3] = l4.w;
-            }
+          for (int c = 2 * (g - 14); c < 2 * (g - 13); ++c) {
+            const float4 x = *reinterpret_cast<const float4*>(consts_of(sl, 32) + 8 * c + 4 * hh);
+            cdc[4 * c] = x.x; cdc[4 * c + 1] = x.y; cdc[4 * c + 2] = x.z; cdc[4 * c + 3] = x.w;
           }
-        } else {
-          constexpr int kk = g - NKK;
-          if constexpr (kk == 0)
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(dc) : "v"(df[0]), "v"(vf[0]));
-          else
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(dc) : "v"(df[kk]), "v"(vf[kk]));
-          if constexpr (kk + PF < NKK) {
-            df[kk + PF] = rd_d(sl, kk + PF);
-            vf[kk + PF] = rd_v(H, kk + PF);
-          }
-          if constexpr (g == 9 && MSK) {  // out-of-range queries -> -inf (P = 0, dS = 0)
-            const IdxRange rg = idx_range(qlo[H], qhi[H], q0 + 4 * hh);
-            sfor<16>([&](auto vc) __attribute__((always_inline)) {
-              constexpr int v = decltype(vc)::value, o = 8 * (v >> 2) + (v & 3);
-              sc[v] = range_or_ninf<o>(sc[v], rg.base, rg.span);
-            });
-          }
-          if constexpr (g >= 10) {
-            sfor<2>([&](auto jc) __attribute__((always_inline)) {
-              constexpr int v = 2 * (g - 10) + decltype(jc)::value;
-              sc[v] = v_exp1(v_fma1(sc[v], sl2, lq[v]));
-            });
-          }
-          if constexpr (g >= 13) tf[g - 13] = rd_t(tsl, g - 13);
+        }
+        if constexpr (g >= 13) {  // dP operands of k-step 0: dO row, V of both halves
+          constexpr int y = g - 13;
+          if constexpr (y == 0) df[0] = rd_d(sl, 0);
+          else vf[y - 1][0] = rd_v(y - 1, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
     };
-    // finish the softmax of key half HS (P of elements 12 .. 15, dS = P (dP - delta), bf16 pairs) in gaps 0 .. 10
-    auto sm_tail = [&](auto hsc, int sl) __attribute__((always_inline)) {
-      const float* Ls = reinterpret_cast<const float*>(ring + sl * SLOT + 2 * IMG);
-      return [&, hsc, Ls](auto gc) __attribute__((always_inline)) {
-        constexpr int HS = decltype(hsc)::value, g = decltype(gc)::value;
-        if constexpr (g == 0) {  // -delta of the tile's rows (floats 32 ..)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
-            nd[4 * c] = d4.x; nd[4 * c + 1] = d4.y; nd[4 * c + 2] = d4.z; nd[4 * c + 3] = d4.w;
-          }
-        }
-        if constexpr (g < 2) {
-          sfor<2>([&](auto jc) __attribute__((always_inline)) {
-            constexpr int v = 12 + 2 * g + decltype(jc)::value;
-            sc[v] = v_exp1(v_fma1(sc[v], sl2, lq[v]));
-          });
-        }
-        if constexpr (g >= 2 && g < 10) {  // dS of pair p = g - 2, its P pair packed
-          constexpr int p = g - 2;
-          sfor<2>([&](auto jc) __attribute__((always_inline)) {
-            constexpr int v = 2 * p + decltype(jc)::value;
-            float t;
-            asm volatile("v_add_f32 %0, %1, %2\n\tv_mul_f32 %0, %3, %0" : "=&v"(t) : "v"(dc[v]), "v"(nd[v]), "v"(sc[v]));
-            dc[v] = t;
-          });
-          pw[HS][p >> 2][p & 3] = cvt_pk(sc[2 * p], sc[2 * p + 1]);
-        }
-        if constexpr (g >= 3 && g < 11) {
-          constexpr int p = g - 3;
-          dw[HS][p >> 2][p & 3] = cvt_pk(dc[2 * p], dc[2 * p + 1]);
-        }
-      };
-    };
-    auto no_valu = [](auto) __attribute__((always_inline)) {};
-    // dV / dK of key half H from the transposed fragments of slot `sl` (the first PF fetched by the S / dP phase
-    // before) || `valu` at each gap; `qsl` >= 0: the next S / dP phase's first Q rows, fetched at gaps 13 .. 15
-    auto g_phase = [&](auto hc, int sl, auto&& valu, int qsl) __attribute__((always_inline)) {
-      constexpr int H = decltype(hc)::value;
+    // phase 2: dP(t) of both halves || exps 0 .. 19 (from gap 2: two MFMAs behind the last S MFMA, the
+    // XDL-write -> VALU-read wait states), P k-step 0 packed; MSK: the range mask on every score first
+    auto ph_dp = [&](auto mc, int sl, int q0) __attribute__((always_inline)) {
+      constexpr bool MSK = decltype(mc)::value;
       sfor<16>([&](auto gc) __attribute__((always_inline)) {
-        constexpr int i = decltype(gc)::value, s2 = (i / NDT) & 1, dt = i % NDT;
-        if constexpr (i < 2 * NDT)
+        constexpr int g = decltype(gc)::value, kk = g >> 1, h = g & 1;
+        if constexpr (kk == 0)
+          if constexpr (DI)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]), "v"(cdc));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]));
+        else
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(dc[h]) : "v"(df[kk]), "v"(vf[h][kk]));
+        // next k-step's operands one k-step (two MFMAs) ahead: deeper would not fit the register file
+        if constexpr (h == 0 && kk + 1 < NKK) df[kk + 1] = rd_d(sl, kk + 1);
+        if constexpr (kk + 1 < NKK) vf[h][kk + 1] = rd_v(h, kk + 1);
+        if constexpr (g == 1) {  // the scores as scalars; MSK: out-of-range queries -> -inf (P = 0, dS = 0)
+          sfor<2>([&](auto hc) __attribute__((always_inline)) {
+            constexpr int hm = decltype(hc)::value;
+            if constexpr (MSK) {
+              int qlo, qhi;
+              query_interval(a, b, kw + 32 * hm + r, qlo, qhi);
+              const IdxRange rg = idx_range(qlo, qhi, q0 + 4 * hh);
+              sfor<16>([&](auto vc) __attribute__((always_inline)) {
+                constexpr int v = decltype(vc)::value, o = 8 * (v >> 2) + (v & 3);
+                pv[hm][v] = range_or_ninf<o>(sc[hm][v], rg.base, rg.span);
+              });
+            } else {
+#pragma unroll
+              for (int v = 0; v < 16; ++v) pv[hm][v] = sc[hm][v];
+            }
+          });
+        }
+        if constexpr (g >= 2 && g < 10) ex2(std::integral_constant<int, 2 * (g - 2)>{});  // exps 0 .. 15
+        if constexpr (g >= 10) {  // P k-step 0
+          pk_p(std::integral_constant<int, g - 10>{});
+          if constexpr (g >= 14) pk_p(std::integral_constant<int, g - 8>{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    };
+    // VALU of the four phases (P and dS of a tile spread over all of them; one exp pair, dS pair or two packs
+    // per gap beside the MFMA and its operand reads):
+    //   phase 1 (S(t)):        dS of tile t-1, k-step 1 (gaps 0 .. 7), its bf16 pairs (2 .. 9)
+    //   phase 2 (dP(t)):       exps 0 .. 15 (gaps 2 .. 9), P k-step 0 (10 .. 15)
+    //   phase 3 (dK(t-1)):     exps 16 .. 31 (gaps 0 .. 7), P k-step 1 (8 .. 15)
+    //   phase 4 (dV(t)):       dS k-step 0 (gaps 0 .. 7), its bf16 pairs (8 .. 15)
+    auto v1 = [&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr (g < 8) ds2(std::integral_constant<int, 16 + 2 * g>{});
+      if constexpr (g >= 2 && g < 10) pk_d(std::integral_constant<int, g + 6>{});  // words 8 .. 15, a gap behind
+    };
+    auto v3 = [&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr (g < 8) ex2(std::integral_constant<int, 16 + 2 * g>{});
+      else pk_p(std::integral_constant<int, g>{});
+    };
+    auto v4 = [&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr (g < 8) ds2(std::integral_constant<int, 2 * g>{});
+      else pk_d(std::integral_constant<int, g - 8>{});
+    };
+    // phases 3 / 4: dK (KQ = true: Q^T fragments, dS operands) or dV (dO^T, P) of both halves from the slot
+    // `sl` (transposed fragments 0, 1 prefetched), || valu(gap); `qsl` >= 0: the next tile's first Q rows at
+    // gaps 14, 15
+    auto ph_g = [&](auto kc, int sl, auto&& valu, int qsl) __attribute__((always_inline)) {
+      constexpr bool KQ = decltype(kc)::value;
+      sfor<16>([&](auto gc) __attribute__((always_inline)) {
+        constexpr int i = decltype(gc)::value, f = i >> 1, h = i & 1, s2 = f >> 2, dt = f & 3;
+        if constexpr (KQ)
           asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
-                       :: "i"(d6_av(H, dt)), "i"(d6_av(H, dt) + 15), "v"(tf[i]), "v"(pw[H][s2]));
+                       :: "i"(d6_ak(h, dt)), "i"(d6_ak(h, dt) + 15), "v"(tf[f]), "v"(dw[h][s2]));
         else
           asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
-                       :: "i"(d6_ak(H, dt)), "i"(d6_ak(H, dt) + 15), "v"(tf[i]), "v"(dw[H][s2]));
-        if constexpr (i + PF < NB) tf[i + PF] = rd_t(sl, i + PF);
+                       :: "i"(d6_av(h, dt)), "i"(d6_av(h, dt) + 15), "v"(tf[f]), "v"(pw[h][s2]));
+        if constexpr (h == 0 && f + 2 < 8) tf[f + 2] = rd_t(sl, (KQ ? 8 : 0) + f + 2);
         valu(gc);
-        if constexpr (i >= NB - PF) {
-          if (qsl >= 0) qf[i - (NB - PF)] = rd_q(qsl, i - (NB - PF));
+        if constexpr (i >= 14) {
+          if (qsl >= 0) qf[i - 14] = rd_q(qsl, i - 14);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
     };
-    auto sd = [&](auto hc, int sl, int q0, int tsl) __attribute__((always_inline)) {
-      if (need_mask(q0, decltype(hc)::value))
-        sd_phase(hc, std::true_type{}, sl, q0, tsl);
-      else
-        sd_phase(hc, std::false_type{}, sl, q0, tsl);
+    auto pref_t = [&](int sl, bool kq) __attribute__((always_inline)) {
+      tf[0] = rd_t(sl, kq ? 8 : 0);
+      tf[1] = rd_t(sl, kq ? 9 : 1);
     };
-    using H0 = std::integral_constant<int, 0>;
-    using H1 = std::integral_constant<int, 1>;
+    auto dp = [&](int sl, int q0) __attribute__((always_inline)) {
+      if (need_mask(q0))
+        ph_dp(std::true_type{}, sl, q0);
+      else
+        ph_dp(std::false_type{}, sl, q0);
+    };
+    auto no_valu = [](auto) __attribute__((always_inline)) {};
 
     int sl_c = 0;  // ring slot of tile t
-    pref_q(0);
-    {  // tile 0: phase 2 without the previous tile's dV / dK
+    qf[0] = rd_q(0, 0);
+    qf[1] = rd_q(0, 1);
+    {  // tile 0: phase 3 without dK(t-1)
       const int q0 = q0_of(0);
       issue(NS - 2);
-      sd(H0{}, 0, q0, 0);
-      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // no MFMA between the chain and its reads
-      sfor<16>([&](auto gc) __attribute__((always_inline)) { sm_tail(H0{}, 0)(gc); });
-      pref_q(0);
-      sd(H1{}, 0, q0, 0);
+      ph_s(0, no_valu);
+      dp(0, q0);
+      nds = consts_of(0, 32);
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // no MFMA between dP's chains and their reads
+      sfor<16>([&](auto gc) __attribute__((always_inline)) { v3(gc); });
+      pref_t(0, false);
       wait_vm<2 * NDMA>();
       ring_barrier();
-      g_phase(H0{}, 0, sm_tail(H1{}, 0), T > 1 ? 1 % NS : -1);
+      ph_g(std::false_type{}, 0, v4, T > 1 ? 1 % NS : -1);
     }
     for (int t = 1; t < T; ++t) {
       const int sl_p = sl_c;
       sl_c = sl_c + 1 == NS ? 0 : sl_c + 1;
       const int q0 = q0_of(t);
-      issue(sl_c + NS - 2 >= NS ? sl_c - 2 : sl_c + NS - 2);
-      sd(H0{}, sl_c, q0, sl_p);
-      g_phase(H1{}, sl_p, sm_tail(H0{}, sl_c), sl_c);
-      sd(H1{}, sl_c, q0, sl_c);
-      wait_vm<2 * NDMA>();  // tile t + 1 (issued three iterations ago) landed
-      ring_barrier();
+      if constexpr (!(PR & 1)) issue(sl_c + NS - 2 >= NS ? sl_c - 2 : sl_c + NS - 2);
+      ph_s(sl_c, v1);  // with dS(t-1) k-step 1 (nds still tile t-1's)
+      dp(sl_c, q0);
+      pref_t(sl_p, true);
+      nds = consts_of(sl_c, 32);  // -delta of tile t, whose dS phases 4 and 1 compute
+      ph_g(std::true_type{}, sl_p, v3, -1);
+      pref_t(sl_c, false);
+      if constexpr (PR & 1) {
+        wait_vm<0>();
+      } else {
+        wait_vm<2 * NDMA>();  // tile t + 1 (issued three iterations ago) landed; slot t - 1 read for the last time
+      }
+      if constexpr (!(PR & 2)) ring_barrier();
       const int sl_n = sl_c + 1 == NS ? 0 : sl_c + 1;
-      g_phase(H0{}, sl_c, sm_tail(H1{}, sl_c), t + 1 < T ? sl_n : -1);
+      ph_g(std::false_type{}, sl_c, v4, t + 1 < T ? sl_n : -1);
     }
-    {  // drain: the last tile's half 1
-#pragma unroll
-      for (int i = 0; i < PF; ++i) tf[i] = rd_t(sl_c, i);
+    {  // drain: dS k-step 1 and dK of the last tile
+      sfor<16>([&](auto gc) __attribute__((always_inline)) { v1(gc); });
+      pref_t(sl_c, true);
       asm volatile("s_nop 7" ::: "memory");  // the last packs -> MFMA operand reads
-      g_phase(H1{}, sl_c, no_valu, -1);
+      ph_g(std::true_type{}, sl_c, no_valu, -1);
     }
     wait_vm<0>();  // no LDS-DMA may outlive the workgroup
   }
@@ -3912,8 +3985,24 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     rope_to_dkdv(f5);
     // dense rows: an 8-slot Q / dO ring (tiles 6 ahead; B4 S8192 backward 7.605 -> 7.544 ms in one process,
     // 7 slots 7.572); packed rows keep 6 (their key blocks often visit only a few tiles)
-    if (v6)
-      fa_bwd_dkdv6_kernel<128><<<(S + 255) / 256 * Hkv * B, 256, 0, stream>>>(a, ld);
+    // LLMT_FA_D6_PROBE (diagnostic builds, wrong results): 1 = no ring DMA in the loop, 2 = no loop barrier,
+    // 4 = no softmax VALU, 8 = no operand LDS reads
+    static const int d6p = getenv("LLMT_FA_D6_PROBE") ? atoi(getenv("LLMT_FA_D6_PROBE")) : 0;
+    const unsigned g6 = (S + 255) / 256 * Hkv * B;
+    if (v6 && d6p == 1)
+      fa_bwd_dkdv6_kernel<128, 3, 1><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 2)
+      fa_bwd_dkdv6_kernel<128, 3, 2><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 4)
+      fa_bwd_dkdv6_kernel<128, 3, 4><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 8)
+      fa_bwd_dkdv6_kernel<128, 3, 8><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 15)
+      fa_bwd_dkdv6_kernel<128, 3, 15><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 12)
+      fa_bwd_dkdv6_kernel<128, 3, 12><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6)
+      fa_bwd_dkdv6_kernel<128><<<g6, 256, 0, stream>>>(a, ld);
     else if (variant == 6 && a.rmask && !seg)
       fa_bwd_dkdv5_kernel<128, false, 8, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 6 && a.rmask)

@@ -629,9 +629,10 @@ def swiglu(gate_up: torch.Tensor, dy_t_consumer: bool = False) -> torch.Tensor:
 #          inverse rotation (no pass over dq / dk);
 #   "full" only k is rotated by the standalone kernel; the forward / dQ kernels rotate their q rows on load
 #          (the dQ kernel hands the rotated rows to the dK/dV kernel), the epilogues as "bwd";
-#   "auto" (default) "full" for D = 128, "bwd" otherwise — the faster form of each in same-process A/B
-#          (profiles/r5_rope_fused.md: Llama-3-8B fwd + bwd 10.03 / 10.13 / 10.14 ms full / bwd / off;
-#          Phi-3 packed D96 3.15 / 3.12 / 3.22 ms);
+#   "auto" (default) = "bwd": the Llama-3-8B step runs 1455.8 / 1458.6 / 1460.3 ms/step with bwd / full / off
+#          (alternating bench runs on one box, profiles/r5_rope_fused.md) — in the step the on-load rotation of
+#          "full" costs the forward and dQ kernels 8 ms/step (their per-row table reads miss L2 between the
+#          GEMMs), more than the q pass it replaces; isolated, full was ahead on the Llama shape;
 #   "off"  the standalone passes over q / k and dq / dk (A/B reference).
 _RF = os.environ.get("LLMT_ROPE_FUSED", "auto").strip().lower()
 ROPE_FUSED = ["off" if _RF in ("0", "false", "off") else (_RF if _RF in ("full", "bwd") else "auto")]
@@ -639,7 +640,7 @@ ROPE_FUSED = ["off" if _RF in ("0", "false", "off") else (_RF if _RF in ("full",
 
 def _rope_mode(D: int) -> str:
     m = ROPE_FUSED[0]
-    return ("full" if D == 128 else "bwd") if m == "auto" else m
+    return "bwd" if m == "auto" else m
 
 
 class _RopeFlashAttnFn(Function):

@@ -31,7 +31,7 @@ def fa_asm(tmp_path_factory):
 # fa_fwd4 (O^T / Q / K in a[0:255]) and fa_bwd_dkdv6 (dV^T / dK^T of 64 keys in a[0:255])
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("name", ["_ZN4llmt14fa_fwd4_kernelILi128EEEvNS_8AttnArgsE",
-                                  "_ZN4llmt19fa_bwd_dkdv6_kernelILi128ELi3EEEvNS_8AttnArgsEPKf"])
+                                  "_ZN4llmt19fa_bwd_dkdv6_kernelILi128ELi3ELi0ELb0EEEvNS_8AttnArgsEPKf"])
 def test_accumulator_registers_are_asm_owned(fa_asm, name):
     text = fa_asm
     body = re.search(rf"^{name}:(.*?)^\.Lfunc_end", text, re.S | re.M).group(1)
