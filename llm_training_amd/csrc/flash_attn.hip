@@ -2863,9 +2863,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
         constexpr int g = decltype(gc)::value, kk = g >> 1, h = g & 1;
         valu(gc);
         if constexpr (kk == 0)
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(sc[h]) : "v"(qf[0]), "v"(kf[h][0]));
+          if constexpr (PR & 64) asm volatile("" : "=&v"(sc[h]) : "v"(qf[0]), "v"(kf[h][0]));
+          else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(sc[h]) : "v"(qf[0]), "v"(kf[h][0]));
         else
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sc[h]) : "v"(qf[kk]), "v"(kf[h][kk]));
+          if constexpr (PR & 64) asm volatile("" : "+v"(sc[h]) : "v"(qf[kk]), "v"(kf[h][kk]));
+          else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sc[h]) : "v"(qf[kk]), "v"(kf[h][kk]));
         if constexpr (h == 0 && kk + 2 < NKK) qf[kk + 2] = rd_q(sl, kk + 2);
         if constexpr (DI && g >= 14) {  // -delta of the tile's rows (floats 32 ..): the dP chains' initial value
 #pragma unroll
@@ -2878,47 +2880,6 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
           constexpr int y = g - 13;
           if constexpr (y == 0) df[0] = rd_d(sl, 0);
           else vf[y - 1][0] = rd_v(y - 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    };
-    // phase 2: dP(t) of both halves || exps 0 .. 19 (from gap 2: two MFMAs behind the last S MFMA, the
-    // XDL-write -> VALU-read wait states), P k-step 0 packed; MSK: the range mask on every score first
-    auto ph_dp = [&](auto mc, int sl, int q0) __attribute__((always_inline)) {
-      constexpr bool MSK = decltype(mc)::value;
-      sfor<16>([&](auto gc) __attribute__((always_inline)) {
-        constexpr int g = decltype(gc)::value, kk = g >> 1, h = g & 1;
-        if constexpr (kk == 0)
-          if constexpr (DI)
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]), "v"(cdc));
-          else
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]));
-        else
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(dc[h]) : "v"(df[kk]), "v"(vf[h][kk]));
-        // next k-step's operands one k-step (two MFMAs) ahead: deeper would not fit the register file
-        if constexpr (h == 0 && kk + 1 < NKK) df[kk + 1] = rd_d(sl, kk + 1);
-        if constexpr (kk + 1 < NKK) vf[h][kk + 1] = rd_v(h, kk + 1);
-        if constexpr (g == 1) {  // the scores as scalars; MSK: out-of-range queries -> -inf (P = 0, dS = 0)
-          sfor<2>([&](auto hc) __attribute__((always_inline)) {
-            constexpr int hm = decltype(hc)::value;
-            if constexpr (MSK) {
-              int qlo, qhi;
-              query_interval(a, b, kw + 32 * hm + r, qlo, qhi);
-              const IdxRange rg = idx_range(qlo, qhi, q0 + 4 * hh);
-              sfor<16>([&](auto vc) __attribute__((always_inline)) {
-                constexpr int v = decltype(vc)::value, o = 8 * (v >> 2) + (v & 3);
-                pv[hm][v] = range_or_ninf<o>(sc[hm][v], rg.base, rg.span);
-              });
-            } else {
-#pragma unroll
-              for (int v = 0; v < 16; ++v) pv[hm][v] = sc[hm][v];
-            }
-          });
-        }
-        if constexpr (g >= 2 && g < 10) ex2(std::integral_constant<int, 2 * (g - 2)>{});  // exps 0 .. 15
-        if constexpr (g >= 10) {  // P k-step 0
-          pk_p(std::integral_constant<int, g - 10>{});
-          if constexpr (g >= 14) pk_p(std::integral_constant<int, g - 8>{});
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -2944,6 +2905,55 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
       if constexpr (g < 8) ds2(std::integral_constant<int, 2 * g>{});
       else pk_d(std::integral_constant<int, g - 8>{});
     };
+    // phase 2: dP(t) of both halves || exps 0 .. 19 (from gap 2: two MFMAs behind the last S MFMA, the
+    // XDL-write -> VALU-read wait states), P k-step 0 packed; MSK: the range mask on every score first
+    auto ph_dp = [&](auto mc, int sl, int q0) __attribute__((always_inline)) {
+      constexpr bool MSK = decltype(mc)::value;
+      sfor<16>([&](auto gc) __attribute__((always_inline)) {
+        constexpr int g = decltype(gc)::value, kk = g >> 1, h = g & 1;
+        if constexpr (kk == 0)
+          if constexpr (DI)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]), "v"(cdc));
+          else
+            if constexpr (PR & 64) asm volatile("" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]));
+            else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]));
+        else
+          if constexpr (PR & 64) asm volatile("" : "+v"(dc[h]) : "v"(df[kk]), "v"(vf[h][kk]));
+          else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(dc[h]) : "v"(df[kk]), "v"(vf[h][kk]));
+        // next k-step's operands one k-step (two MFMAs) ahead: deeper would not fit the register file
+        if constexpr (h == 0 && kk + 1 < NKK) df[kk + 1] = rd_d(sl, kk + 1);
+        if constexpr (kk + 1 < NKK) vf[h][kk + 1] = rd_v(h, kk + 1);
+        if constexpr (g == 1) {  // the scores as scalars; MSK: out-of-range queries -> -inf (P = 0, dS = 0)
+          sfor<2>([&](auto hc) __attribute__((always_inline)) {
+            constexpr int hm = decltype(hc)::value;
+            if constexpr (MSK) {
+              int qlo, qhi;
+              query_interval(a, b, kw + 32 * hm + r, qlo, qhi);
+              const IdxRange rg = idx_range(qlo, qhi, q0 + 4 * hh);
+              sfor<16>([&](auto vc) __attribute__((always_inline)) {
+                constexpr int v = decltype(vc)::value, o = 8 * (v >> 2) + (v & 3);
+                pv[hm][v] = range_or_ninf<o>(sc[hm][v], rg.base, rg.span);
+              });
+            } else {
+#pragma unroll
+              for (int v = 0; v < 16; ++v) pv[hm][v] = sc[hm][v];
+            }
+          });
+        }
+        if constexpr (!(PR & 16)) {
+          if constexpr (g >= 2 && g < 10) ex2(std::integral_constant<int, 2 * (g - 2)>{});  // exps 0 .. 15
+          if constexpr (g >= 10) {  // P k-step 0
+            pk_p(std::integral_constant<int, g - 10>{});
+            if constexpr (g >= 14) pk_p(std::integral_constant<int, g - 8>{});
+          }
+        }
+        if constexpr (PR & 32) {  // probe: phases 3 and 4's VALU here too
+          v3(gc);
+          v4(gc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    };
     // phases 3 / 4: dK (KQ = true: Q^T fragments, dS operands) or dV (dO^T, P) of both halves from the slot
     // `sl` (transposed fragments 0, 1 prefetched), || valu(gap); `qsl` >= 0: the next tile's first Q rows at
     // gaps 14, 15
@@ -2951,7 +2961,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
       constexpr bool KQ = decltype(kc)::value;
       sfor<16>([&](auto gc) __attribute__((always_inline)) {
         constexpr int i = decltype(gc)::value, f = i >> 1, h = i & 1, s2 = f >> 2, dt = f & 3;
-        if constexpr (KQ)
+        if constexpr (PR & 64)
+          asm volatile("" :: "v"(tf[f]), "v"(KQ ? dw[h][s2] : pw[h][s2]));
+        else if constexpr (KQ)
           asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
                        :: "i"(d6_ak(h, dt)), "i"(d6_ak(h, dt) + 15), "v"(tf[f]), "v"(dw[h][s2]));
         else
@@ -2998,11 +3010,24 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
       sl_c = sl_c + 1 == NS ? 0 : sl_c + 1;
       const int q0 = q0_of(t);
       if constexpr (!(PR & 1)) issue(sl_c + NS - 2 >= NS ? sl_c - 2 : sl_c + NS - 2);
-      ph_s(sl_c, v1);  // with dS(t-1) k-step 1 (nds still tile t-1's)
+      if constexpr (PR & 16) ph_s(sl_c, no_valu);
+      else ph_s(sl_c, v1);  // with dS(t-1) k-step 1 (nds still tile t-1's)
       dp(sl_c, q0);
       pref_t(sl_p, true);
       nds = consts_of(sl_c, 32);  // -delta of tile t, whose dS phases 4 and 1 compute
-      ph_g(std::true_type{}, sl_p, v3, -1);
+      if constexpr (PR & 16) {  // probe: every VALU of the tile beside the accumulator-destination MFMAs
+        ph_g(std::true_type{}, sl_p, [&](auto gc) __attribute__((always_inline)) {
+          constexpr int g = decltype(gc)::value;
+          v1(gc);
+          v3(gc);
+          if constexpr (g < 8) ex2(std::integral_constant<int, 2 * g>{});
+          else pk_p(std::integral_constant<int, g - 8>{});
+        }, -1);
+      } else if constexpr (PR & 32) {
+        ph_g(std::true_type{}, sl_p, no_valu, -1);
+      } else {
+        ph_g(std::true_type{}, sl_p, v3, -1);
+      }
       pref_t(sl_c, false);
       if constexpr (PR & 1) {
         wait_vm<0>();
@@ -3011,7 +3036,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const 
       }
       if constexpr (!(PR & 2)) ring_barrier();
       const int sl_n = sl_c + 1 == NS ? 0 : sl_c + 1;
-      ph_g(std::false_type{}, sl_c, v4, t + 1 < T ? sl_n : -1);
+      if constexpr (PR & 32) ph_g(std::false_type{}, sl_c, no_valu, t + 1 < T ? sl_n : -1);
+      else ph_g(std::false_type{}, sl_c, v4, t + 1 < T ? sl_n : -1);
     }
     {  // drain: dS k-step 1 and dK of the last tile
       sfor<16>([&](auto gc) __attribute__((always_inline)) { v1(gc); });
@@ -3986,7 +4012,8 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
     // dense rows: an 8-slot Q / dO ring (tiles 6 ahead; B4 S8192 backward 7.605 -> 7.544 ms in one process,
     // 7 slots 7.572); packed rows keep 6 (their key blocks often visit only a few tiles)
     // LLMT_FA_D6_PROBE (diagnostic builds, wrong results): 1 = no ring DMA in the loop, 2 = no loop barrier,
-    // 4 = no softmax VALU, 8 = no operand LDS reads
+    // 4 = no softmax VALU, 8 = no operand LDS reads, 16 = all VALU beside the accumulator-destination MFMAs,
+    // 64 = no MFMAs (profiles/r5_dkdv6.md)
     static const int d6p = getenv("LLMT_FA_D6_PROBE") ? atoi(getenv("LLMT_FA_D6_PROBE")) : 0;
     const unsigned g6 = (S + 255) / 256 * Hkv * B;
     if (v6 && d6p == 1)
@@ -4001,6 +4028,12 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       fa_bwd_dkdv6_kernel<128, 3, 15><<<g6, 256, 0, stream>>>(a, ld);
     else if (v6 && d6p == 12)
       fa_bwd_dkdv6_kernel<128, 3, 12><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 64)
+      fa_bwd_dkdv6_kernel<128, 3, 64><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 68)
+      fa_bwd_dkdv6_kernel<128, 3, 68><<<g6, 256, 0, stream>>>(a, ld);
+    else if (v6 && d6p == 16)
+      fa_bwd_dkdv6_kernel<128, 3, 16><<<g6, 256, 0, stream>>>(a, ld);
     else if (v6)
       fa_bwd_dkdv6_kernel<128><<<g6, 256, 0, stream>>>(a, ld);
     else if (variant == 6 && a.rmask && !seg)
