@@ -197,6 +197,10 @@ struct AttnArgs {
   // 1: masks from per-row index ranges (the run of a packed row, causal, window, sequence end) instead of
   // per-element segment-id compares; needs run bounds (rs / re) whenever `seg` is set
   int rmask;
+  // 1: the query-parallel / dK/dV kernels issue their first K/V (Q/dO) tile DMAs before their own row loads,
+  // so the two prologue latencies overlap instead of adding up (short packed documents: the prologue is a
+  // large share of a block); 0: rows first (A/B reference, LLMT_FA_EARLY_DMA=0)
+  int early;
   // backward: non-null -> the dQ kernel computes delta = rowsum(dO * O) itself and writes the packed per-tile
   // row constants the dK/dV kernel reads here (no separate prep pass); null -> the prep kernel ran
   float* ldw;
@@ -1099,7 +1103,8 @@ __device__ __forceinline__ void dma_tile5(const Rsrc& q, const Rsrc& d, const Rs
 __device__ __forceinline__ void dma_tile9(const Rsrc& k, const Rsrc& v, const Rsrc& sg, const char* lds, int img,
                                           const char* lseg, const int (&vk)[4], const int (&vv)[4], int vs) {
   uint32_t keep;
-  const uint32_t l0 = lds_addr(lds);
+  // (wave-uniform; readfirstlane so hipcc's divergence analysis cannot leave it in a VGPR for the "s" operand)
+  const uint32_t l0 = __builtin_amdgcn_readfirstlane(lds_addr(lds));
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %12, 0 offen lds\n\t"
@@ -1114,7 +1119,7 @@ __device__ __forceinline__ void dma_tile9(const Rsrc& k, const Rsrc& v, const Rs
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "s"(l0), "s"(img), "v"(vk[0]), "v"(vk[1]), "v"(vk[2]), "v"(vk[3]), "v"(vv[0]), "v"(vv[1]), "v"(vv[2]),
-        "v"(vv[3]), "v"(vs), "s"(k.w), "s"(v.w), "s"(sg.w), "s"(lds_addr(lseg))
+        "v"(vv[3]), "v"(vs), "s"(k.w), "s"(v.w), "s"(sg.w), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lseg)))
       : "memory");
 }
 // the same with the descriptor forced to SGPRs (a kernel under SGPR pressure may keep it in VGPRs,
@@ -1546,18 +1551,23 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
   const float sl2 = a.scale * kLog2e;
 
   bfv8 kf[NKK], vf[NKK];
+  // the block's K / V rows: loaded after the first ring tiles were issued when a.early (their latencies
+  // overlap: one workgroup per CU leaves the prologue exposed), else first
+  auto load_kv = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    kf[kk] = gload8(kp + (int64_t)min(kr, S - 1) * a.k_ss + kk * 16 + hh * 8, kr < S);
-    vf[kk] = gload8(vp + (int64_t)min(kr, S - 1) * a.v_ss + kk * 16 + hh * 8, kr < S);
-  }
+    for (int kk = 0; kk < NKK; ++kk) {
+      kf[kk] = gload8(kp + (int64_t)min(kr, S - 1) * a.k_ss + kk * 16 + hh * 8, kr < S);
+      vf[kk] = gload8(vp + (int64_t)min(kr, S - 1) * a.v_ss + kk * 16 + hh * 8, kr < S);
+    }
 #pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
-  // move K / V into the accumulator file here, with the VALU-write -> MFMA-read wait states behind them
-  // (the asm MFMAs that read them are invisible to the hazard recognizer)
+    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
+    // move K / V into the accumulator file here, with the VALU-write -> MFMA-read wait states behind them
+    // (the asm MFMAs that read them are invisible to the hazard recognizer)
 #pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+a"(kf[kk]), "+a"(vf[kk]));
-  asm volatile("s_nop 7");
+    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+a"(kf[kk]), "+a"(vf[kk]));
+    asm volatile("s_nop 7");
+  };
+  if (!a.early) load_kv();
   f32v16 dkt[NDT], dvt[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
@@ -1772,8 +1782,14 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
     };
 
     int sl_m2 = (NS - 1) * SLOT, sl_m1 = 0, sl_0 = SLOT, sl_p1 = 2 * SLOT;
+    // early: the tiles the first wait covers, then the rows (hipcc's wait for its own younger loads covers
+    // those tiles too: loads retire in order), then the rest of the ring
 #pragma unroll
-    for (int t = 0; t < NS - 1; ++t) issue(smem + t * SLOT);
+    for (int t = 0; t < 3; ++t) issue(smem + t * SLOT);
+    if (a.early) load_kv();
+#pragma unroll
+    for (int t = 3; t < NS - 1; ++t) issue(smem + t * SLOT);
+    static_assert(NS - 1 - (NS - 4) == 3, "first wait covers three tiles");
     wait_vm<NDMA * (NS - 4)>();
     ring_barrier();
 
@@ -1929,6 +1945,23 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   int klo = 0, khi = -1;
   if (!OM) key_interval(a, b, qrow, klo, khi);
 
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
+  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+  // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
+  // and past the tensor on the last row of the last head -> zeros instead of a fault
+  const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
+  const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
+  const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
+  auto issue = [&](int t) { kv_tile_dma<NW>(smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT), kv_beg + t * BN, wid,
+                                            lane, a, krs, vrs, srs); };
+  // early: tile 0 is in flight while the Q rows load (hipcc's waits for its own, younger loads then cover
+  // it too: loads retire in order)
+  if (a.early && T > 0) issue(0);
+
   bfv8 qf[NKK];
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
@@ -1947,21 +1980,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
     for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;  // running max in scaled log2 units
 
-  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
-  int kv_end = a.causal ? min(S, qs + 128) : S;
-  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
-  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
-
   if (T > 0) {
-    // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
-    // and past the tensor on the last row of the last head -> zeros instead of a fault
-    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
-    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
-    const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
-    auto issue = [&](int t) { kv_tile_dma<NW>(smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT), kv_beg + t * BN, wid,
-                                              lane, a, krs, vrs, srs); };
     // loop-invariant LDS offsets: K row reads (two 32-key halves) and V^T transposed reads
     int ro[NKK], to[NDT][2];
 #pragma unroll
@@ -1976,7 +1995,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
       }
     }
 
-    issue(0);
+    if (!a.early) issue(0);
     wait_vm<0>();
     ring_barrier();
     // the tile loop unrolled by the ring's two slots: each slot's LDS offsets are compile-time constants
@@ -3405,6 +3424,21 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   int klo = 0, khi = -1;
   if (!OM) key_interval(a, b, qrow, klo, khi);
 
+  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
+  int kv_end = a.causal ? min(S, qs + 128) : S;
+  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
+  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
+  kv_beg = max(kv_beg, qr.rs) / BN * BN;
+  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+  // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
+  // and past the tensor on the last row of the last head -> zeros instead of a fault
+  const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
+  const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
+  const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
+  auto issue = [&](int t) { kv_tile_dma<NW>(smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT), kv_beg + t * BN, wid,
+                                            lane, a, krs, vrs, srs); };
+  if (a.early && T > 0) issue(0);  // tile 0 in flight under the row loads (see fa_fwd3_kernel)
+
   bfv8 qf[NKK], df[NKK];
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) {
@@ -3450,21 +3484,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqt[dt][i] = 0.f;
 
-  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
-  int kv_end = a.causal ? min(S, qs + 128) : S;
-  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
-  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
-
   if (T > 0) {
-    // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
-    // and past the tensor on the last row of the last head -> zeros instead of a fault
-    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
-    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
-    const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
-    auto issue = [&](int t) { kv_tile_dma<NW>(smem + __builtin_amdgcn_readfirstlane((t & 1) * SLOT), kv_beg + t * BN, wid,
-                                              lane, a, krs, vrs, srs); };
     int ro[NKK], to[NDT][2];
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
@@ -3478,7 +3498,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
       }
     }
 
-    issue(0);
+    if (!a.early) issue(0);
     wait_vm<0>();
     ring_barrier();
     // the tile loop unrolled by the ring's two slots: each slot's LDS offsets are compile-time constants
@@ -3662,6 +3682,12 @@ static int range_masks() {
   return e ? atoi(e) : 1;
 }
 
+// prologue order (AttnArgs::early), read per launch for A/B (LLMT_FA_EARLY_DMA)
+static int early_dma() {
+  const char* e = getenv("LLMT_FA_EARLY_DMA");
+  return e ? atoi(e) : 1;
+}
+
 // block order of the 1-D attention grids (AttnArgs::bmajor), read per launch for A/B (LLMT_FA_BMAJOR)
 // (B4 S8192 Hq32 Hkv8: forward 2.102 -> 2.068 ms, backward 7.795 -> 7.732 ms in one process)
 static int bmajor_order() {
@@ -3762,6 +3788,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   set_dropout(a, drop_p, drop_seed);
   a.bmajor = bmajor_order();
   a.rmask = range_masks() && (seg == nullptr || a.rs != nullptr);
+  a.early = early_dma();
   dim3 grid((S + 127) / 128, Hq, B);
   // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907 (variant 0), the
   // removed one-wave-per-SIMD ring forward 1.043; 3 = fwd3 with compiler-placed row-sum adds, 2 = with the
@@ -3907,6 +3934,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   set_dropout(a, drop_p, drop_seed);
   a.bmajor = bmajor_order();
   a.rmask = range_masks() && (seg == nullptr || a.rs != nullptr);
+  a.early = early_dma();
   const bool gqa = Hq != Hkv;
   const int64_t nrows = (int64_t)B * S * Hq;
   dim3 grid((S + 127) / 128, Hq, B);
