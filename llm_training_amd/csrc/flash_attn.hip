@@ -201,6 +201,9 @@ struct AttnArgs {
   // so the two prologue latencies overlap instead of adding up (short packed documents: the prologue is a
   // large share of a block); 0: rows first (A/B reference, LLMT_FA_EARLY_DMA=0)
   int early;
+  // diagnostic probes (LLMT_FA_PROBE, wrong results by design; benchmarks/attn_block_probe.py): forward 1 = no
+  // tiles, 2 = no Q row loads, 4 = no O / LSE stores; backward 8 = no tiles in the dQ and dK/dV kernels
+  int probe;
   // backward: non-null -> the dQ kernel computes delta = rowsum(dO * O) itself and writes the packed per-tile
   // row constants the dK/dV kernel reads here (no separate prep pass); null -> the prep kernel ran
   float* ldw;
@@ -1582,7 +1585,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
   int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
   if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
   const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
-  const int T = nq * grp;
+  const int T = (a.probe & 8) ? 0 : nq * grp;
 
   if (T > 0) {
     int dq_off[2], dd_off[2];
@@ -1950,7 +1953,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
   kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+  const int T = (kv_end > kv_beg && !(a.probe & 1)) ? (kv_end - kv_beg + BN - 1) / BN : 0;
   // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
   // and past the tensor on the last row of the last head -> zeros instead of a fault
   const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
@@ -1964,7 +1967,8 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
 
   bfv8 qf[NKK];
 #pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
+  for (int kk = 0; kk < NKK; ++kk)
+    qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S && !(a.probe & 2));
   if (a.rope_q && qrow < S) {  // fused RoPE: the rows arrive unrotated
     const int p = rope_pos(a, b, qrow);
     rope_frags<NKK>(qf, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
@@ -2148,9 +2152,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
         w[4 * dt + c].y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
       }
     widen_pairs(w);
-    if (qrow < S) store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
+    if (qrow < S && !(a.probe & 4)) store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
   }
-  if (qrow < S) {
+  if (qrow < S && !(a.probe & 4)) {
     if constexpr (!WS) {
       bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
 #pragma unroll
@@ -3429,7 +3433,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
   kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
+  const int T = (kv_end > kv_beg && !(a.probe & 8)) ? (kv_end - kv_beg + BN - 1) / BN : 0;
   // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
   // and past the tensor on the last row of the last head -> zeros instead of a fault
   const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
@@ -3688,6 +3692,11 @@ static int early_dma() {
   return e ? atoi(e) : 1;
 }
 
+static int attn_probe() {
+  const char* e = getenv("LLMT_FA_PROBE");
+  return e ? atoi(e) : 0;
+}
+
 // block order of the 1-D attention grids (AttnArgs::bmajor), read per launch for A/B (LLMT_FA_BMAJOR)
 // (B4 S8192 Hq32 Hkv8: forward 2.102 -> 2.068 ms, backward 7.795 -> 7.732 ms in one process)
 static int bmajor_order() {
@@ -3789,6 +3798,7 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   a.bmajor = bmajor_order();
   a.rmask = range_masks() && (seg == nullptr || a.rs != nullptr);
   a.early = early_dma();
+  a.probe = attn_probe();
   dim3 grid((S + 127) / 128, Hq, B);
   // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907 (variant 0), the
   // removed one-wave-per-SIMD ring forward 1.043; 3 = fwd3 with compiler-placed row-sum adds, 2 = with the
@@ -3935,6 +3945,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   a.bmajor = bmajor_order();
   a.rmask = range_masks() && (seg == nullptr || a.rs != nullptr);
   a.early = early_dma();
+  a.probe = attn_probe();
   const bool gqa = Hq != Hkv;
   const int64_t nrows = (int64_t)B * S * Hq;
   dim3 grid((S + 127) / 128, Hq, B);
