@@ -279,7 +279,9 @@ class Llama(BaseModel):
         seg_info = rope_tok = None
         if device.type == "cuda" and impl in ("flash", "flash_attention_2", "hip"):
             if segment_ids is not None:
-                seg_info = F_.segment_info(segment_ids)  # run bounds, shared by every layer's attention
+                # run bounds and block orders, shared by every layer's attention
+                seg_info = F_.segment_info(segment_ids, doc_major=(self.config.num_key_value_heads ==
+                                                                   self.config.num_attention_heads))
             if F_.ROPE_FUSED[0] != "off":  # per-token RoPE table rows for the attention kernels, shared by every layer
                 rope_tok = F_.rope_token_tables(position_ids, cos, sin)
         return {"positions": position_ids, "cos": cos, "sin": sin, "segment_ids": segment_ids, "impl": impl,

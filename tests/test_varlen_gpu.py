@@ -120,8 +120,8 @@ def _fwd_bwd(q, k, v, do, seg):
 @pytest.mark.parametrize("packed", [False, True])
 def test_attention_kernel_variants_bitwise(Hq, Hkv, D, packed, monkeypatch):
     """The opt-in forward / dQ forms — MHA head chains of 2 / 4 (forward variants 5 / 6), GQA head pairs
-    on 8-wave workgroups (forward 7, dQ 3) — and the packed-block work order (against LLMT_SEG_ORDER=0)
-    compute exactly what the default kernels compute: same per-head math, only the block -> workgroup
+    on 8-wave workgroups (forward 7, dQ 3) — the packed-block work orders (LLMT_SEG_ORDER 0 / 2) and the
+    prologue issue order (LLMT_FA_EARLY_DMA=0) compute exactly what the default kernels compute: same per-head math, only the block -> workgroup
     assignment differs."""
     torch.manual_seed(0)
     B, S = 2, 1024
@@ -134,8 +134,9 @@ def test_attention_kernel_variants_bitwise(Hq, Hkv, D, packed, monkeypatch):
     forms = [("LLMT_FA_FWD_VARIANT", "5"), ("LLMT_FA_FWD_VARIANT", "6")]
     if D == 128 and Hq // Hkv % 2 == 0:
         forms += [("LLMT_FA_FWD_VARIANT", "7"), ("LLMT_FA_DQ_VARIANT", "3")]
-    if packed:
-        forms += [("LLMT_SEG_ORDER", "0")]
+    if packed:  # index order, and document-major order (the MHA default of the models)
+        forms += [("LLMT_SEG_ORDER", "0"), ("LLMT_SEG_ORDER", "2")]
+    forms += [("LLMT_FA_EARLY_DMA", "0")]  # prologue issue order: row loads before the first ring tiles
     for env, val in forms:
         monkeypatch.setenv(env, val)
         got = _fwd_bwd(q, k, v, do, seg)
