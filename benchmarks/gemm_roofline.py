@@ -1,4 +1,5 @@
-"""GEMM roofline of the Llama-3-8B training step (micro-batch 4 x 8192 = 32768 tokens, one MI355X).
+"""GEMM roofline of a training step (Llama-3-8B micro-batch 4 x 8192 = 32768 tokens by default, or
+Phi-3-mini with --model phi3-mini; one MI355X).
 
 Every forward / input-gradient / weight-gradient GEMM of the step, timed standalone on random operands
 through the framework's own dispatch (ops/fused.py: hipBLASLt with the per-shape layout choice —
@@ -28,10 +29,14 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
-H, I, V, L = 4096, 14336, 128256, 32
-QKV = 4096 + 2 * 1024
-# name -> (N out features, K in features, calls per step per GEMM kind)
-SHAPES = {"qkv": (QKV, H, L), "o": (H, H, L), "gate_up": (2 * I, H, L), "down": (H, I, L)}
+# hidden, intermediate, vocabulary, layers, qkv width
+MODELS = {"llama3-8b": (4096, 14336, 128256, 32, 4096 + 2 * 1024), "phi3-mini": (3072, 8192, 32064, 32, 3 * 3072)}
+
+
+def shapes(model):
+    H, I, V, L, QKV = MODELS[model]
+    # name -> (N out features, K in features, calls per step per GEMM kind)
+    return {"qkv": (QKV, H, L), "o": (H, H, L), "gate_up": (2 * I, H, L), "down": (H, I, L)}, H, V
 
 
 def timeit(fn, iters=10, warm=3):
@@ -52,7 +57,9 @@ def main():
     ap.add_argument("--tokens", type=int, default=32768)
     ap.add_argument("--chunk", type=int, default=8192, help="lm_head rows per GEMM (fused CE chunk)")
     ap.add_argument("--tag", default="ours")
+    ap.add_argument("--model", default="llama3-8b", choices=sorted(MODELS))
     a = ap.parse_args()
+    SHAPES, H, V = shapes(a.model)
     dev = "cuda"
     T = a.tokens
     g = torch.Generator(device=dev).manual_seed(0)
@@ -83,7 +90,7 @@ def main():
             ms = timeit(fn)
             layout = [v for k, v in F_._LAYOUT_CACHE.items() if k[0] == kind and k[1] == M and k[2] == N][-1:] \
                 if kind != "fwd" else ["nt"]
-            r = {"tag": a.tag, "gemm": name, "kind": kind, "M": M, "N": N, "K": K, "ms": round(ms, 4),
+            r = {"tag": a.tag, "model": a.model, "gemm": name, "kind": kind, "M": M, "N": N, "K": K, "ms": round(ms, 4),
                  "pflops": round(flops / ms / 1e12, 3), "calls_per_step": calls,
                  "layout": layout[0] if layout else "direct"}
             rows.append(r)
