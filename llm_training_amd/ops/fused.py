@@ -100,11 +100,11 @@ _LAYOUT_CACHE: dict[tuple, str] = {}
 #    optimizer step, so every rank runs rank 0's algorithms from the second step on (a rank whose
 #    timings were disturbed by its own collectives cannot pick a different, slower layout);
 #  * "static": the rule below (LLMT_DETERMINISTIC=1, LLMT_GEMM_LAYOUT_TUNE=0, graph capture).
-# LLMT_GEMM_LAYOUTS=table (default) | timed (ignore the table) | static.
+# LLMT_GEMM_LAYOUTS=table (default) | timed (ignore the table) | static; LLMT_GEMM_LAYOUT_TABLE=path: another table.
 _LAYOUT_SOURCE: dict[tuple, str] = {}
 _LAYOUT_MODE = os.environ.get("LLMT_GEMM_LAYOUTS", "table").strip().lower()
-_LAYOUT_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
-                                  "gemm_layouts_gfx950.json")
+_LAYOUT_TABLE_PATH = os.environ.get("LLMT_GEMM_LAYOUT_TABLE") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "gemm_layouts_gfx950.json")
 _LAYOUT_TABLE: list = [None]
 _AGREED: dict[str, str] = {}  # rank 0's choices for problems this rank has not met yet
 
@@ -232,6 +232,22 @@ def _layout(key: tuple, variants: dict, default: str, can_time: bool) -> str:
     return best
 
 
+def _sk_pairs(fns: dict) -> dict:
+    """Layout launchers taking the stream-K flag -> zero-argument launchers for :func:`_layout`. With stream-K
+    solutions allowed each layout also gets a ``/nosk`` twin restricted to the non-stream-K solutions: which
+    of the two is faster is a property of the problem (Llama-3-8B at 32768 tokens: the qkv forward 1.263 vs
+    1.128 ms, the o weight gradient 1.036 vs 0.881, the lm_head weight gradient 6.60 vs 7.00;
+    profiles/r5_gemm_streamk_ab.md), so it is timed / tabled with the layout."""
+    out = {}
+    for name, fn in fns.items():
+        if ALLOW_STREAMK[0]:
+            out[name] = (lambda f: lambda: f(True))(fn)
+            out[name + "/nosk"] = (lambda f: lambda: f(False))(fn)
+        else:
+            out[name] = (lambda f: lambda: f(False))(fn)
+    return out
+
+
 def _path(layout: str, k: int, ncols: int, *ts: torch.Tensor) -> str:
     mode = GEMM_MODES.get(layout, "blas")
     if mode == "blas" or not all(_gemm_operand_ok(t) for t in ts) or not use_native(ts[0]):
@@ -255,10 +271,22 @@ def mm_nt(x2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
     N = w.shape[0]
     y = out if out is not None else torch.empty(M, N, device=x2.device, dtype=x2.dtype)
     if path == "lt":  # column-major: y^T (N x M) = w^T (from K x N) . x^T (K x M)
-        if bias is not None and bias.is_contiguous() and bias.dtype in (torch.bfloat16, torch.float32):
-            lib().gemm_lt_bias(w, x2, y, bias, True, False, N, M, K, _ld(w), _ld(x2), N, ALLOW_STREAMK[0])
+        epi = bias is not None and bias.is_contiguous() and bias.dtype in (torch.bfloat16, torch.float32)
+
+        def nt(s):
+            if epi:
+                lib().gemm_lt_bias(w, x2, y, bias, True, False, N, M, K, _ld(w), _ld(x2), N, s)
+            else:
+                lib().gemm_lt(w, x2, y, True, False, N, M, K, _ld(w), _ld(x2), N, False, s)
+
+        sk = ALLOW_STREAMK[0]
+        if sk:
+            v = _sk_pairs({"nt": nt})
+            v[_layout(("fwd", M, N, K, _ld(w), _ld(x2), epi, sk), v, "nt", True)]()
+        else:
+            nt(False)
+        if epi:
             return y
-        lib().gemm_lt(w, x2, y, True, False, N, M, K, _ld(w), _ld(x2), N, False, ALLOW_STREAMK[0])
     else:
         lib().gemm_(x2, w, y, False, False, False)
     return y if bias is None else y.add_(bias)
@@ -292,19 +320,19 @@ def mm_nn(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
     if path == "lt" and (wt is not None or (TRANSPOSE_LAYOUTS[0] and M >= _TR_DGRAD_MIN_M and _tr_ok(dy2, w))):
         sk = ALLOW_STREAMK[0]
 
-        def tn():  # dx^T (K x M) = (w^T stored [K, N])^T-op . dy^T, both operands N-contiguous
+        def tn(s):  # dx^T (K x M) = (w^T stored [K, N])^T-op . dy^T, both operands N-contiguous
             lib().gemm_lt(wt if wt is not None else transpose(w), dy2, out, True, False, K, M, N, N,
-                          _ld(dy2), _ld(out), False, sk)
+                          _ld(dy2), _ld(out), False, s)
 
-        def nn():
-            lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, sk)
+        def nn(s):
+            lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, s)
 
         if wt is not None:  # transposed once for several chunks: TN
-            tn()
-        elif _layout(("dgrad", M, N, K, _ld(dy2), _ld(out), sk), {"tn": tn, "nn": nn}, "tn", True) == "tn":
-            tn()
+            v = _sk_pairs({"tn": tn})
+            v[_layout(("dgrad_wt", M, N, K, _ld(dy2), _ld(out), sk), v, "tn", True)]()
         else:
-            nn()
+            v = _sk_pairs({"tn": tn, "nn": nn})
+            v[_layout(("dgrad", M, N, K, _ld(dy2), _ld(out), sk), v, "tn", True)]()
     elif path == "lt":  # column-major: dx^T (K x M) = w^T (K x N) . dy^T (N x M)
         lib().gemm_lt(w, dy2, out, False, False, K, M, N, _ld(w), _ld(dy2), _ld(out), False, ALLOW_STREAMK[0])
     else:
@@ -326,42 +354,46 @@ def wgrad_into(out: torch.Tensor, dy: torch.Tensor, x: torch.Tensor, accumulate:
         sk, o2 = ALLOW_STREAMK[0], out.view(N, K)
         if dy_t is not None:
             # dy^T came with dy (the SwiGLU backward wrote both): TN, both operands token-contiguous
-            lib().gemm_lt(transpose(x), dy_t, o2, True, False, K, N, M, M, M, K, accumulate, sk)
+            def tnd(s):
+                lib().gemm_lt(transpose(x), dy_t, o2, True, False, K, N, M, M, M, K, accumulate, s)
+            v = _sk_pairs({"tn": tnd})
+            v[_layout(("wgrad_dyt", M, N, K, _ld(x), out.dtype, sk), v, "tn", not accumulate)]()
             return True
 
-        def nt():  # dW^T (K x N) = x^T (K x M) . dy (M x N), straight from the token-major operands
-            lib().gemm_lt(x, dy, o2, False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, sk)
+        def nt(s):  # dW^T (K x N) = x^T (K x M) . dy (M x N), straight from the token-major operands
+            lib().gemm_lt(x, dy, o2, False, True, K, N, M, _ld(x), _ld(dy), K, accumulate, s)
 
-        def tt():  # x^T materialised
-            lib().gemm_lt(transpose(x), dy, o2, True, True, K, N, M, M, _ld(dy), K, accumulate, sk)
+        def tt(s):  # x^T materialised
+            lib().gemm_lt(transpose(x), dy, o2, True, True, K, N, M, M, _ld(dy), K, accumulate, s)
 
-        def nn():  # dy^T materialised
-            lib().gemm_lt(x, transpose(dy), o2, False, False, K, N, M, _ld(x), M, K, accumulate, sk)
+        def nn(s):  # dy^T materialised
+            lib().gemm_lt(x, transpose(dy), o2, False, False, K, N, M, _ld(x), M, K, accumulate, s)
 
-        def tn():  # both transposed: token-contiguous operands (the layout hipBLASLt runs fastest)
-            lib().gemm_lt(transpose(x), transpose(dy), o2, True, False, K, N, M, M, M, K, accumulate, sk)
+        def tn(s):  # both transposed: token-contiguous operands (the layout hipBLASLt runs fastest)
+            lib().gemm_lt(transpose(x), transpose(dy), o2, True, False, K, N, M, M, M, K, accumulate, s)
 
-        variants = {"nt": nt, "tt": tt, "nn": nn}
+        lt = {"nt": nt, "tt": tt, "nn": nn}
         if _WGRAD_TN:
-            variants["tn"] = tn
+            lt["tn"] = tn
         if N * K <= _SPLITK_MAX_OUT and M % 256 == 0:
             # split-K along the token (contraction) dimension into 2 or 4 slices, run as one strided-batch
             # GEMM into fp32 slabs + one reduction pass: 2-4x the output tiles for outputs that fill the
             # 256 CUs in 1.5 / 3.5 waves of 256x256 tiles (qkv, down)
             def _split(a, b, ta, tb, lda, ldb, n_split):
-                def run():
+                def run(s):
                     slabs = torch.empty(n_split, N, K, device=out.device, dtype=torch.float32)
                     lib().gemm_lt_splitk(a() if callable(a) else a, b() if callable(b) else b, slabs, ta, tb,
-                                         K, N, M, lda, ldb, n_split, sk)
+                                         K, N, M, lda, ldb, n_split, s)
                     lib().splitk_reduce_(slabs, o2, accumulate)
                 return run
 
             for ns in _SPLITK:
-                variants[f"nt{ns}"] = _split(x, dy, False, True, _ld(x), _ld(dy), ns)
-                variants[f"tt{ns}"] = _split(lambda: transpose(x), dy, True, True, M, _ld(dy), ns)
-                variants[f"nn{ns}"] = _split(x, lambda: transpose(dy), False, False, _ld(x), M, ns)
+                lt[f"nt{ns}"] = _split(x, dy, False, True, _ld(x), _ld(dy), ns)
+                lt[f"tt{ns}"] = _split(lambda: transpose(x), dy, True, True, M, _ld(dy), ns)
+                lt[f"nn{ns}"] = _split(x, lambda: transpose(dy), False, False, _ld(x), M, ns)
                 if _WGRAD_TN:
-                    variants[f"tn{ns}"] = _split(lambda: transpose(x), lambda: transpose(dy), True, False, M, M, ns)
+                    lt[f"tn{ns}"] = _split(lambda: transpose(x), lambda: transpose(dy), True, False, M, M, ns)
+        variants = _sk_pairs(lt)
         if _OWN_WGRAD and M % 32 == 0 and N % 4 == 0:
             # the hand-written ping-pong GEMM (csrc/gemm.hip) reads both token-major operands directly
             # (transposed LDS reads, no materialised transposes); split into 2 / 4 contraction slices for

@@ -16,3 +16,6 @@ for w in ${WORKLOADS-pt it dpo orpo}; do
 done
 run pt_nosk LLMT_GEMM_STREAMK=0 timeout -k 10 300 python bench.py --workload pt --steps 3 --warmup 2
 run it_nosk LLMT_GEMM_STREAMK=0 timeout -k 10 300 python bench.py --workload it --steps 3 --warmup 2
+# Phi-3 IT at micro-batch 8 (the round-4 verdict's comparison point): its 32768-token problems
+run it8 timeout -k 10 300 python bench.py --workload it --micro-batch 8 --steps 3 --warmup 2
+run it8_nosk LLMT_GEMM_STREAMK=0 timeout -k 10 300 python bench.py --workload it --micro-batch 8 --steps 3 --warmup 2

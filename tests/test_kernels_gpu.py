@@ -545,7 +545,8 @@ def test_linear_bias_in_the_gemm_epilogue(monkeypatch, bias_dtype):
     calls = []
     monkeypatch.setattr(fused, "lib", lambda: _Spy(torch.ops.llmt, calls))
     y = F_.linear(x, w, b)
-    assert calls == ["gemm_lt_bias"]
+    # (several calls on first sight of the problem: the stream-K / non-stream-K solutions are timed)
+    assert calls and set(calls) == {"gemm_lt_bias"}
     assert y.dtype == torch.bfloat16
     assert _rel(y, x.float() @ w.float().t() + b.float()) < 1e-2
     dy = torch.randn_like(y)
