@@ -7,6 +7,7 @@ scripts/gpu/steps.sh \
   "verify_pt|300|python bench.py --gpus 1 --steps 20 --warmup 5" \
   "verify_ptpacked|200|python bench.py --workload pt-packed --steps 8 --warmup 3" \
   "verify_it|250|python bench.py --workload it --steps 6 --warmup 3" \
+  "verify_it8|250|python bench.py --workload it --micro-batch 8 --steps 8 --warmup 3" \
   "verify_dpo|200|python bench.py --workload dpo --steps 6 --warmup 3" \
   "verify_orpo|200|python bench.py --workload orpo --steps 6 --warmup 3" \
   "verify_prof_pt|400|bash scripts/gpu/prof_step.sh pt 3" \
