@@ -3692,6 +3692,16 @@ static int early_dma() {
   return e ? atoi(e) : 1;
 }
 
+// ring slots of the dK/dV kernel (fa_bwd_dkdv5_kernel NSL), read per launch for A/B (LLMT_FA_D5_RING): 8 for
+// D=128 (packed Llama rows, same process: 8 docs 2.900 -> 2.890 ms, 32 docs 1.546 -> 1.511 ms fwd+bwd; dense
+// unchanged), 6 for D=96 (dense 3.635 vs 3.649 ms, packed 2.183 vs 2.189; profiles/r5_dkdv_ring_ab.jsonl)
+static int d5_ring(bool seg, int D = 128) {
+  (void)seg;
+  const char* e = getenv("LLMT_FA_D5_RING");
+  if (e) return atoi(e) == 8 ? 8 : 6;
+  return D == 128 ? 8 : 6;
+}
+
 static int attn_probe() {
   const char* e = getenv("LLMT_FA_PROBE");
   return e ? atoi(e) : 0;
@@ -3990,7 +4000,9 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
         fa_bwd_dq3_kernel<96, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
       const bool f5 = dkdv_variant() == 5;
       rope_to_dkdv(f5);
-      if (dkdv_variant() == 5 && a.rmask)
+      if (dkdv_variant() == 5 && a.rmask && d5_ring(seg != nullptr, 96) == 8)
+        fa_bwd_dkdv5_kernel<96, false, 8><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
+      else if (dkdv_variant() == 5 && a.rmask)
         fa_bwd_dkdv5_kernel<96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
       else if (dkdv_variant() == 5)
         fa_bwd_dkdv5_kernel<96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
@@ -4079,7 +4091,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
       fa_bwd_dkdv5_kernel<128, false, 8, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 6 && a.rmask)
       fa_bwd_dkdv5_kernel<128, false, 6, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 5 && a.rmask && !seg)
+    else if (variant == 5 && a.rmask && d5_ring(seg != nullptr) == 8)
       fa_bwd_dkdv5_kernel<128, false, 8><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
     else if (variant == 5 && a.rmask)
       fa_bwd_dkdv5_kernel<128><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
