@@ -35,12 +35,13 @@ from ..ops.native import lib, use_native
 log = logging.getLogger("llm_training")
 
 
-def _combine(stats: torch.Tensor, group) -> torch.Tensor:
-    """All-gather the [k, n] local row statistics of every TP rank -> [tp, k, n] (one collective)."""
+def _combine(stats: torch.Tensor, group, async_op: bool = False):
+    """All-gather the [k, n] local row statistics of every TP rank -> [tp, k, n] (one collective); with
+    ``async_op`` -> (result, work): the result is valid once the work completes."""
     n = dist.get_world_size(group)
     allv = torch.empty(n * stats.numel(), dtype=stats.dtype, device=stats.device)
-    dist.all_gather_into_tensor(allv, stats.contiguous().view(-1), group=group)
-    return allv.view(n, *stats.shape)
+    work = dist.all_gather_into_tensor(allv, stats.contiguous().view(-1), group=group, async_op=async_op)
+    return (allv.view(n, *stats.shape), work) if async_op else allv.view(n, *stats.shape)
 
 
 def _local_stats(lg, lab, v0, ignore_index, native, rowsum=None):
@@ -77,8 +78,10 @@ def _local_grad(lg, lab, v0, ignore_index, lse, coef_row, coef_scalar, native):
 
 
 class _VPFusedCE(Function):
-    """Vocab-parallel fused linear + CE in one pass, memory bounded by one local logits chunk: per chunk
-    the local logits, one all-gather of their (lse, target) rows, d loss / d logits in place, dh and dW."""
+    """Vocab-parallel fused linear + CE in one pass, memory bounded by two local logits chunks: per chunk
+    the local logits, one all-gather of their (lse, target) rows, d loss / d logits in place, dh and dW.
+    The chunks are software-pipelined: chunk i+1's logits GEMM and local statistics are issued while chunk
+    i's all-gather is in flight, so the small collective does not stall the compute stream between GEMMs."""
 
     @staticmethod
     def forward(ctx, h, w_full, labels, v0, ignore_index, group, chunk, n_valid):
@@ -95,12 +98,11 @@ class _VPFusedCE(Function):
             dw_full[n_valid:].zero_()
         wt = weight_t(w, N) if need_h and native and N > chunk else None
         loss = torch.zeros((), device=h.device, dtype=torch.float32)
-        for s0 in range(0, N, chunk):
-            s1 = min(N, s0 + chunk)
+
+        def finish(s0, s1, lg, allv, work):
+            nonlocal loss
+            work.wait()
             lab = labels[s0:s1]
-            lg = mm_nt(h[s0:s1], w)
-            lse_l, tgt_l = _local_stats(lg, lab, v0, ignore_index, native)
-            allv = _combine(torch.stack([lse_l.float(), tgt_l.float()]), group)
             lse = torch.logsumexp(allv[:, 0], dim=0)
             tgt = allv[:, 1].sum(0)  # the target logit lives in exactly one rank's vocabulary window
             loss += ((lse - tgt) * valid[s0:s1]).sum()
@@ -110,7 +112,20 @@ class _VPFusedCE(Function):
                     mm_nn(lg, w, out=dh[s0:s1], wt=wt)
                 if need_w:
                     dw_add_chunk(dw, lg, h[s0:s1], s0 == 0)
+
+        pending = None
+        for s0 in range(0, N, chunk):
+            s1 = min(N, s0 + chunk)
+            lg = mm_nt(h[s0:s1], w)
+            lse_l, tgt_l = _local_stats(lg, labels[s0:s1], v0, ignore_index, native)
+            allv, work = _combine(torch.stack([lse_l.float(), tgt_l.float()]), group, async_op=True)
+            if pending is not None:
+                finish(*pending)
+            pending = (s0, s1, lg, allv, work)
             del lg
+        if pending is not None:
+            finish(*pending)
+        del pending
         ctx.save_for_backward(*(t for t in (dh, dw_full) if t is not None))
         ctx.has = (need_h, need_w)
         ctx.w = w_full
