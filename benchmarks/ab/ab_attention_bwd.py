@@ -1,13 +1,13 @@
 """In-process A/B of flash-attention backward variants (LLMT_FA_BWD_VARIANT is read on every launch):
 alternating windows of each variant on the same operands, so box-to-box clock differences cancel.
-    python benchmarks/ab_attention_bwd.py [B S Hq Hkv D] [variants, comma-separated]"""
+    python benchmarks/ab/ab_attention_bwd.py [B S Hq Hkv D] [variants, comma-separated]"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D = (int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (4, 8192, 32, 8, 128)))

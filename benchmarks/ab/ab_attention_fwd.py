@@ -1,13 +1,13 @@
 """In-process A/B of flash-attention forward variants (LLMT_FA_FWD_VARIANT is read on every launch):
 alternating windows of each variant on the same operands.
-    python benchmarks/ab_attention_fwd.py [B S Hq Hkv D] [variants, comma-separated] [env var]"""
+    python benchmarks/ab/ab_attention_fwd.py [B S Hq Hkv D] [variants, comma-separated] [env var]"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D = (int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (4, 8192, 32, 8, 128)))

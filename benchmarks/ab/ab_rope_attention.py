@@ -1,6 +1,6 @@
 """In-process A/B of RoPE fused into the attention kernels vs the standalone in-place passes
 (ops/fused.py ROPE_FUSED: bwd / full / off): forward + backward of rope_attention on one fused QKV buffer, alternating windows.
-    python benchmarks/ab_rope_attention.py [S B nq nkv D docs]
+    python benchmarks/ab/ab_rope_attention.py [S B nq nkv D docs]
 docs > 0: packed rows of that many random documents (positions restart per document)."""
 import json
 import os
@@ -8,7 +8,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 from llm_training_amd.ops.rope_utils import compute_rope_tables  # noqa: E402
 

@@ -1,14 +1,14 @@
 """Block order of packed rows (ops/fused.py segment_info, LLMT_SEG_ORDER): 1 = heaviest block first over all
 documents, 2 = document-major (a document's blocks back to back, heaviest first inside it), 0 = index order.
 Same process, alternating, fwd and fwd+bwd:
-    python benchmarks/ab_seg_order.py B S Hq Hkv D docs [equal]"""
+    python benchmarks/ab/ab_seg_order.py B S Hq Hkv D docs [equal]"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D, docs = (int(v) for v in sys.argv[1:7])

@@ -1,13 +1,13 @@
 """Compare flash-attention backward variants (LLMT_FA_BWD_VARIANT) on small shapes: per-gradient max abs
 difference against variant 4 and relative error against the fp32 reference, one JSON line per case.
-    python benchmarks/attn_variant_check.py [variant]"""
+    python benchmarks/ab/attn_variant_check.py [variant]"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 from llm_training_amd.ops import reference as ref  # noqa: E402
 

@@ -1,13 +1,13 @@
 """Compare flash-attention forward variants (LLMT_FA_FWD_VARIANT) against variant 4 and the fp32 reference
 on small shapes: output and (through the backward, which reads the forward's LSE) gradient errors, one JSON
-line per case.    python benchmarks/fwd_variant_check.py [variant]"""
+line per case.    python benchmarks/ab/fwd_variant_check.py [variant]"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 from llm_training_amd.ops import reference as ref  # noqa: E402
 

@@ -2,7 +2,7 @@
 (dense, B = N / S) and as one row of N tokens packed with equal documents of S tokens, for S = 128 .. N.
 A least-squares fit of time = blocks * c_blk + tiles * c_tile per kernel pass separates the per-block
 prologue / epilogue cost from the per-tile cost (short packed documents are dominated by the former).
-    python benchmarks/attn_block_overhead.py [N Hq Hkv D]"""
+    python benchmarks/probes/attn_block_overhead.py [N Hq Hkv D]"""
 import json
 import os
 import sys
@@ -10,7 +10,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 N, Hq, Hkv, D = (int(v) for v in (sys.argv[1:5] if len(sys.argv) > 4 else (16384, 32, 32, 96)))

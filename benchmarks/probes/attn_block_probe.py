@@ -1,14 +1,14 @@
 """Where the per-block cost of the attention kernels goes (LLMT_FA_PROBE diagnostic probes, wrong results by
 design): forward with no tiles (1), no Q loads (2), no O / LSE stores (4), combinations; backward with no
 tiles in dQ and dK/dV (8). Same process, alternating.
-    python benchmarks/attn_block_probe.py B S Hq Hkv D"""
+    python benchmarks/probes/attn_block_probe.py B S Hq Hkv D"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D = (int(v) for v in sys.argv[1:6])

@@ -1,11 +1,11 @@
 """Forward attention only, a few calls of one variant (for PMC passes):
-    rocprofv3 --pmc <counters> -- python benchmarks/attn_fwd_probe.py VARIANT [B S Hq Hkv D]"""
+    rocprofv3 --pmc <counters> -- python benchmarks/probes/attn_fwd_probe.py VARIANT [B S Hq Hkv D]"""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 os.environ["LLMT_FA_FWD_VARIANT"] = sys.argv[1]

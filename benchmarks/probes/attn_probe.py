@@ -1,11 +1,11 @@
 """Attention forward + backward at one shape, a few times (for PMC passes and per-kernel tables):
-    rocprofv3 --pmc <counters> -- python benchmarks/attn_probe.py [B S Hq Hkv D] [docs] [iters]"""
+    rocprofv3 --pmc <counters> -- python benchmarks/probes/attn_probe.py [B S Hq Hkv D] [docs] [iters]"""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D = (int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (4, 8192, 32, 8, 128)))

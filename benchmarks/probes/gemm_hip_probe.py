@@ -1,11 +1,11 @@
 """Run the hand-written gfx950 GEMM (csrc/gemm.hip) alone on one Llama-3-8B shape and layout, for PMC
-passes:   rocprofv3 --pmc <counters> -- python benchmarks/gemm_hip_probe.py [shape] [fwd|dgrad|wgrad] [T]"""
+passes:   rocprofv3 --pmc <counters> -- python benchmarks/probes/gemm_hip_probe.py [shape] [fwd|dgrad|wgrad] [T]"""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_training_amd.ops.native import lib  # noqa: E402
 
 shape = sys.argv[1] if len(sys.argv) > 1 else "gate_up"

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for sh in "8 4096 32 32 96" "16 2048 32 32 96" "8 4096 32 32 64"; do
-  timeout -k 10 120 python benchmarks/ab_attention_fwd.py $sh 3,4 >> gpurun_out/ab_chain.log 2>&1 || exit $?
+  timeout -k 10 120 python benchmarks/ab/ab_attention_fwd.py $sh 3,4 >> gpurun_out/ab_chain.log 2>&1 || exit $?
 done
 grep '^{' gpurun_out/ab_chain.log
 timeout -k 10 200 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "attn or attention or flash or varlen or phi" > gpurun_out/gt_chain.log 2>&1; tail -2 gpurun_out/gt_chain.log

@@ -8,7 +8,7 @@ for v in 5 7; do
   export LLMT_FA_BWD_VARIANT=$v
   for p in 1 2; do
     if [ $p = 1 ]; then CC=$C1; else CC=$C2; fi
-    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CC -d gpurun_out/pmc_dkdv_${v}_$p -o run -- python benchmarks/attn_probe.py > gpurun_out/pmc_dkdv_${v}_$p.log 2>&1
+    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CC -d gpurun_out/pmc_dkdv_${v}_$p -o run -- python benchmarks/probes/attn_probe.py > gpurun_out/pmc_dkdv_${v}_$p.log 2>&1
     python scripts/pmc_summary.py gpurun_out/pmc_dkdv_${v}_$p/run_results.db --match dkdv --last 2 > gpurun_out/pmc_dkdv_${v}_$p.txt
     rm -rf gpurun_out/pmc_dkdv_${v}_$p
   done

@@ -8,7 +8,7 @@ C2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INST_CYCLES_VMEM S
 for v in 4 10; do
   for pass in 1 2; do
     if [ $pass = 1 ]; then CC=$C; else CC=$C2; fi
-    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CC -d gpurun_out/pmc_fwd_${v}_$pass -o run -- python benchmarks/attn_fwd_probe.py $v > gpurun_out/pmc_fwd_${v}_$pass.log 2>&1
+    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CC -d gpurun_out/pmc_fwd_${v}_$pass -o run -- python benchmarks/probes/attn_fwd_probe.py $v > gpurun_out/pmc_fwd_${v}_$pass.log 2>&1
     python scripts/pmc_summary.py gpurun_out/pmc_fwd_${v}_$pass/run_results.db --match fa_fwd --last 2 > gpurun_out/pmc_fwd_${v}_$pass.txt
     rm -rf gpurun_out/pmc_fwd_${v}_$pass
   done
