@@ -3833,7 +3833,9 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   // block's heads have their own K/V: MHA B8 S4096 H32 D128 1.567 -> 1.391 ms, D96 1.631 -> 1.245 ms; with
   // GQA they lose (B4 S8192 Hq32 Hkv8 2.230 -> 2.507 ms; profiles/r3_attention_head_chain_ab.jsonl). In the
   // Phi-3 IT step (packed MHA) they cost 3 ms/step (688.4 / 690.3 vs 685.9 / 686.2 ms alternating on one
-  // box), so chains are opt-in: variants 5 / 6 = chains of 2 / 4; 8 = one head per workgroup.
+  // box), so chains are opt-in: variants 5 / 6 = chains of 2 / 4; 8 = one head per workgroup. Against the
+  // round-5 forward they lose standalone too (B8 S4096 H32 D96 dense 0.983 vs 1.131 / 1.241 ms, packed
+  // document-major 0.431 vs 0.752 / 1.016 ms; profiles/r4_negative_probes.jsonl).
   const int grp = Hq / Hkv;
   const int chain = variant == 5 ? (Hq % 2 == 0 ? 2 : 0) : variant == 6 ? (Hq % 4 == 0 ? 4 : 0) : 0;
   const unsigned nb1 = (unsigned)((S + 127) / 128 * Hq * B);
