@@ -406,7 +406,10 @@ def main():
     if tpl.TP_WAIT_METER is not None:
         rccl["exposed_tp_comm_ms_per_step"] = round(
             sum(a.elapsed_time(b) for a, b in tpl.TP_WAIT_METER) / args.steps, 3)
-        rccl["tp_stages"] = int(os.environ.get("LLMT_TP_STAGES", "4"))
+        # the chunk count actually used for this shard (tp_stages reduces LLMT_TP_STAGES to divide the shard)
+        # and the chunks per GEMM of every staged projection
+        rccl["tp_stages"] = tpl.tp_stages(S // pc.tp_size)
+        rccl["tp_gemm_groups"] = dict(tpl.STAGE_PLANS)
         tpl.TP_WAIT_METER = None
     el = torch.tensor([el_host], device=device, dtype=torch.float64)
     if world > 1:
@@ -423,6 +426,7 @@ def main():
         fpt += flops_per_token(cfg, S, frac) / 3  # frozen reference model: forward only
     peak_mem = torch.cuda.max_memory_allocated(device) / 2 ** 30
     import llm_training_amd.ops.fused as F_layouts
+    from llm_training_amd.ops.native import llmt_env
     if rank == 0:
         par = f"dp{pc.dp_size}" + (f"-tp{pc.tp_size}" if pc.tp_size > 1 else "")
         cfg_out = {"model": model_name if not args.layers else f"{model_name}-{args.layers}L(INVALID-debug)",
@@ -462,6 +466,8 @@ def main():
             "rccl": rccl,
             # how the GEMM layouts were chosen (shipped table / timed / rank 0's) and the hash of the choices
             "gemm_layouts": F_layouts.layout_summary(),
+            # every LLMT_* knob of the environment (kernel variants, layouts, schedules) this number ran with
+            "llmt_env": llmt_env(),
         }
         if os.environ.get("LLMT_GEMM_LAYOUT_DUMP"):
             F_layouts.dump_layouts(os.environ["LLMT_GEMM_LAYOUT_DUMP"])

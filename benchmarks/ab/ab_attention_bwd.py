@@ -1,6 +1,6 @@
-"""In-process A/B of flash-attention backward variants (LLMT_FA_BWD_VARIANT is read on every launch):
+"""In-process A/B of a per-launch flash-attention knob in the backward (LLMT_FA_* is read on every launch):
 alternating windows of each variant on the same operands, so box-to-box clock differences cancel.
-    python benchmarks/ab/ab_attention_bwd.py [B S Hq Hkv D] [variants, comma-separated]"""
+    python benchmarks/ab/ab_attention_bwd.py [B S Hq Hkv D] [values, comma-separated] [env var]"""
 import json
 import os
 import sys
@@ -11,8 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 from llm_training_amd.ops import fused as F_  # noqa: E402
 
 B, S, Hq, Hkv, D = (int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (4, 8192, 32, 8, 128)))
-variants = (sys.argv[6] if len(sys.argv) > 6 else "1,3").split(",")
-ENV = sys.argv[7] if len(sys.argv) > 7 else "LLMT_FA_BWD_VARIANT"  # or LLMT_FA_DQ_VARIANT
+variants = (sys.argv[6] if len(sys.argv) > 6 else "1,0").split(",")
+ENV = sys.argv[7] if len(sys.argv) > 7 else "LLMT_FA_EARLY_DMA"  # or LLMT_FA_BMAJOR / LLMT_FA_GENERIC
 q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)

@@ -1,6 +1,7 @@
 """Where the per-block cost of the attention kernels goes (LLMT_FA_PROBE diagnostic probes, wrong results by
 design): forward with no tiles (1), no Q loads (2), no O / LSE stores (4), combinations; backward with no
-tiles in dQ and dK/dV (8). Same process, alternating.
+tiles in dQ and dK/dV (8). Same process, alternating. Runs on the DIAGNOSTIC library (_C_diag.so, built on
+first use or by `python -m llm_training_amd._build --diag`): the production library has no probe code.
     python benchmarks/probes/attn_block_probe.py B S Hq Hkv D"""
 import json
 import os
@@ -9,7 +10,11 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+os.environ["LLMT_NATIVE_DIAG"] = "1"  # before the package loads its native library
 from llm_training_amd.ops import fused as F_  # noqa: E402
+from llm_training_amd.ops.native import lib  # noqa: E402
+
+assert lib().diag_build() == 1, "the probes need the diagnostic library"
 
 B, S, Hq, Hkv, D = (int(v) for v in sys.argv[1:6])
 q = torch.randn(B, S, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)

@@ -46,8 +46,12 @@ hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void
                                int64_t rp_sb, int64_t rp_ss, const float* rcos, const float* rsin, int64_t rP,
                                void* qrot, hipStream_t stream);
 int llmt_flash_attn_fwd_rope_inkernel(int D, float drop_p, int has_seg, int seg_runs);
+int llmt_flash_attn_bwd_generic(int D, float drop_p);
+int llmt_attn_diag_build();
 hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn, int y_mn, int out_mode, int M, int N, int K,
                      int64_t ldx, int64_t ldy, int64_t ldc, hipStream_t stream);
+hipError_t llmt_gemm_swiglu_bwd(const void* dy, const void* w, const void* gu, void* dgu, void* dgu_t, int M, int N,
+                                int K, int64_t ldx, int64_t ldy, hipStream_t stream);
 hipError_t llmt_gemm_splitk(const void* x, const void* y, float* slabs, int x_mn, int y_mn, int M, int N, int K,
                             int64_t ldx, int64_t ldy, int64_t ldc, int nsplit, hipStream_t stream);
 int64_t llmt_flash_attn_bwd_ws(int B, int S, int Hq, int D);
@@ -240,6 +244,9 @@ at::Tensor kernel_errors() {
 }
 static int* err_words() { return kernel_errors().data_ptr<int>(); }
 
+// 1 when this library is the diagnostic build (_C_diag.so, -DLLMT_DIAG: wrong-result probes compiled in)
+int64_t diag_build() { return llmt_attn_diag_build(); }
+
 void rope_(at::Tensor qkv, const at::Tensor& pos, const at::Tensor& cos_t, const at::Tensor& sin_t, int64_t nheads,
            bool inverse) {
   check_bf16_cuda(qkv, "qkv");
@@ -406,6 +413,35 @@ void gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool a_mn, bo
         "gemm");
 }
 
+// Down-projection input gradient with the SwiGLU backward fused into the GEMM epilogue (csrc/gemm.hip
+// SwiArgs): dy [M, K] @ w_down [K, N] -> dc (never stored) -> dgu [M, 2N] (and dgu^T [2N, M] when transposed)
+// from gu [M, 2N] = [gate | up].
+std::vector<at::Tensor> gemm_swiglu_bwd(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& gu, bool transposed) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(gu, "gu");
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && gu.dim() == 2, "gemm_swiglu_bwd: 2-D operands");
+  TORCH_CHECK(dy.stride(1) == 1 && w.stride(1) == 1 && gu.is_contiguous(), "gemm_swiglu_bwd: layouts");
+  const int64_t M = dy.size(0), K = dy.size(1), N = w.size(1);
+  TORCH_CHECK(w.size(0) == K && gu.size(0) == M && gu.size(1) == 2 * N, "gemm_swiglu_bwd: shapes");
+  TORCH_CHECK(K % 32 == 0 && N % 64 == 0 && M % 64 == 0, "gemm_swiglu_bwd: K % 32, N % 64, M % 64");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 30) && K < (1LL << 31), "gemm_swiglu_bwd: dimension too large");
+  const int64_t lda = row_ld(dy), ldb = row_ld(w);
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm_swiglu_bwd: leading dimensions must be 16-byte multiples");
+  TORCH_CHECK(256 * lda * 2 < 0x7fffffffLL && 256 * ldb * 2 < 0x7fffffffLL, "gemm_swiglu_bwd: leading dimension too large");
+  auto dgu = at::empty_like(gu);
+  at::Tensor dgu_t;
+  if (transposed) dgu_t = at::empty({2 * N, M}, gu.options());
+  for (const at::Tensor* t : {&dy, &w, &gu, static_cast<const at::Tensor*>(&dgu)})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "gemm_swiglu_bwd: 16-byte aligned operands");
+  if (M > 0)
+    check(llmt_gemm_swiglu_bwd(dy.data_ptr(), w.data_ptr(), gu.data_ptr(), dgu.data_ptr(),
+                               transposed ? dgu_t.data_ptr() : nullptr, (int)M, (int)N, (int)K, lda, ldb, cur_stream()),
+          "gemm_swiglu_bwd");
+  if (transposed) return {dgu, dgu_t};
+  return {dgu};
+}
+
 // slabs [nsplit, M, N] fp32 (contiguous): slab s = a . b^T over contraction slice s (layouts as gemm_)
 void gemm_splitk_(const at::Tensor& a, const at::Tensor& b, at::Tensor slabs, bool a_mn, bool b_mn) {
   check_bf16_cuda(a, "a");
@@ -547,8 +583,8 @@ void flash_attn_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& 
   auto delta = at::empty({llmt_flash_attn_bwd_ws((int)B, (int)S, (int)Hq, (int)D)}, q.options().dtype(at::kFloat));
   TORCH_CHECK(dout.strides() == o.strides(), "flash_attn_bwd: dout must share O's layout");
   at::Tensor work;  // fp32 per-q-head dK/dV partials, only needed for GQA
-  // only the generic kernels (dropout, or LLMT_FA_D96_GENERIC at D 64 / 96) reduce GQA through partials
-  if (Hq != Hkv && (dropout_p > 0 || (D != 128 && std::getenv("LLMT_FA_D96_GENERIC"))))
+  // only the generic kernels (dropout, LLMT_FA_GENERIC=1) reduce GQA through partials
+  if (Hq != Hkv && llmt_flash_attn_bwd_generic((int)D, (float)dropout_p))
     work = at::empty({2, B, S, Hq, D}, q.options().dtype(at::kFloat));
   // fused RoPE: dq / dk come back for the unrotated q / k. q holds the UNROTATED queries (k rotated) unless
   // rope_q_rotated (both rotated in memory: only the inverse rotation of the gradients is fused); qrot
@@ -586,6 +622,7 @@ TORCH_LIBRARY(llmt, m) {
       "Tensor? coef_row, Tensor? coef_scalar, bool write_grad, int vocab_total=-1, Tensor(b!)? rowsum=None) -> "
       "(Tensor, Tensor, Tensor)");
   m.def("kernel_errors() -> Tensor", &kernel_errors);
+  m.def("diag_build() -> int", &diag_build);
   m.def(
       "adamw_(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!)? pout, float lr, float b1, float b2, "
       "float eps, float wd, int step, Tensor? gscale) -> ()");
@@ -595,6 +632,7 @@ TORCH_LIBRARY(llmt, m) {
   m.def("dequant_sum_(Tensor q, Tensor scale, Tensor(a!) out, int k, bool accumulate) -> ()");
   m.def("gemm_(Tensor a, Tensor b, Tensor(a!) c, bool a_mn, bool b_mn, bool accumulate) -> ()");
   m.def("gemm_splitk_(Tensor a, Tensor b, Tensor(a!) slabs, bool a_mn, bool b_mn) -> ()");
+  m.def("gemm_swiglu_bwd(Tensor dy, Tensor w, Tensor gu, bool transposed) -> Tensor[]");
   m.def(
       "flash_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? seg, float scale, bool causal, int window, "
       "float dropout_p=0., int seed=0, Tensor? rope_pos=None, Tensor? rope_cos=None, Tensor? rope_sin=None, "
@@ -623,6 +661,7 @@ TORCH_LIBRARY_IMPL(llmt, CUDA, m) {
   m.impl("dequant_sum_", &dequant_sum_);
   m.impl("gemm_", &gemm_);
   m.impl("gemm_splitk_", &gemm_splitk_);
+  m.impl("gemm_swiglu_bwd", &gemm_swiglu_bwd);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
 }

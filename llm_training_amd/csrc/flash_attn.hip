@@ -201,8 +201,10 @@ struct AttnArgs {
   // so the two prologue latencies overlap instead of adding up (short packed documents: the prologue is a
   // large share of a block); 0: rows first (A/B reference, LLMT_FA_EARLY_DMA=0)
   int early;
-  // diagnostic probes (LLMT_FA_PROBE, wrong results by design; benchmarks/attn_block_probe.py): forward 1 = no
-  // tiles, 2 = no Q row loads, 4 = no O / LSE stores; backward 8 = no tiles in the dQ and dK/dV kernels
+  // diagnostic probes (LLMT_FA_PROBE, wrong results by design; benchmarks/probes/attn_block_probe.py): forward
+  // 1 = no tiles, 2 = no Q row loads, 4 = no O / LSE stores; backward 8 = no tiles in the dQ and dK/dV kernels.
+  // Only the diagnostic library (_C_diag.so, built with -DLLMT_DIAG) reads it; in the production library
+  // FA_PROBE is the constant 0, so no environment variable can change what the kernels compute.
   int probe;
   // backward: non-null -> the dQ kernel computes delta = rowsum(dO * O) itself and writes the packed per-tile
   // row constants the dK/dV kernel reads here (no separate prep pass); null -> the prep kernel ran
@@ -222,6 +224,12 @@ struct AttnArgs {
   bf16* qrot;
   int qr_sb, qr_ss, qr_sh;
 };
+
+#ifdef LLMT_DIAG
+#define FA_PROBE(a, m) ((a).probe & (m))
+#else
+#define FA_PROBE(a, m) 0
+#endif
 
 // ---------------------------------------------------------------------------- fused RoPE helpers
 // table row of token (b, s): through the position ids, or (rpos null) per-token tables whose row b * rp_sb +
@@ -981,8 +989,7 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 // ============================================================================ backward, D = 128 pipeline
 // The D = 64 / 96 / 128 backward (every Llama-family and Phi-3 model) is: the query-parallel dQ kernel
 // (fa_bwd_dq3_kernel, two workgroups per CU), which also computes delta and writes the packed per-row
-// constants below (fa_bwd_prep128_kernel is the separate-pass form, LLMT_FA_PREP=1), and this key-parallel
-// dK/dV kernel, built for one wave per SIMD (512 registers per lane):
+// constants below, and this key-parallel dK/dV kernel, built for one wave per SIMD (512 registers per lane):
 //  * Q / dO tiles arrive by LDS-DMA (`buffer_load ... lds`, zero-filled past the end) into a ring of NS
 //    slots, several tiles ahead, behind counted `s_waitcnt vmcnt` and a raw barrier.
 //  * one wave per SIMD issues one instruction per issue slot, so the loop is instruction-bound, not
@@ -998,59 +1005,6 @@ __global__ __launch_bounds__(256) void fa_gqa_reduce_kernel(AttnArgs a) {
 //   ld[((b*Hq + h)*nT + t)*128 + {0..31: -lse/scale | 32..63: -delta | 64..95: segment id |
 //                                  96..127: -lse*log2(e)}]
 constexpr int kLdTile = 128;
-
-// 16 lanes per row: each reads one 16-byte chunk of the row of O and of dO, so a wave instruction covers
-// four contiguous 256-byte rows (one row per lane read 64 scattered 16-byte pieces: 2.7 TB/s); the
-// partial dot products meet through three xor shuffles inside the 16-lane group.
-template <int D>
-__global__ __launch_bounds__(256) void fa_bwd_prep128_kernel(AttnArgs a, float* ld) {
-  const int nT = (a.S + 31) / 32;
-  const int64_t nrows = (int64_t)a.B * a.Hq * nT * 32;
-  const float inv_scale = 1.f / a.scale;
-  const int c = threadIdx.x & 15;
-  for (int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; row < nrows; row += (int64_t)gridDim.x * 16) {
-    const int i = (int)(row & 31);
-    const int64_t tt = row >> 5;
-    const int t = (int)(tt % nT);
-    const int64_t bh = tt / nT;
-    const int h = (int)(bh % a.Hq);
-    const int b = (int)(bh / a.Hq);
-    const int s = t * 32 + i;
-    float dl = 0.f;
-    if (s < a.S && c < D / 8) {
-      const bf16x8* op = reinterpret_cast<const bf16x8*>(a.o + (int64_t)b * a.o_sb + (int64_t)s * a.o_ss + (int64_t)h * a.o_sh);
-      const bf16x8* dp = reinterpret_cast<const bf16x8*>(a.dout + (int64_t)b * a.d_sb + (int64_t)s * a.d_ss + (int64_t)h * a.d_sh);
-      float x[8], y[8];
-      unpack8(op[c], x);
-      unpack8(dp[c], y);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dl += x[j] * y[j];
-    }
-    dl += __shfl_xor(dl, 8, 16);
-    dl += __shfl_xor(dl, 4, 16);
-    dl += __shfl_xor(dl, 2, 16);
-    dl += __shfl_xor(dl, 1, 16);
-    if (c == 0) {
-      float ls = -INFINITY, l2 = -INFINITY;
-      int sg = -1;
-      if (s < a.S) {
-        const int64_t lr = ((int64_t)b * a.Hq + h) * a.S + s;
-        ((float*)a.delta)[lr] = dl;
-        const float l = a.lse[lr];
-        ls = (l == -INFINITY) ? -INFINITY : -l * inv_scale;
-        l2 = (l == -INFINITY) ? -INFINITY : -l * kLog2e;
-        sg = a.seg ? a.seg[(int64_t)b * a.S + s] : 0;
-      } else {
-        dl = 0.f;
-      }
-      float* blk = ld + (bh * nT + t) * kLdTile;
-      blk[i] = ls;
-      blk[32 + i] = -dl;
-      reinterpret_cast<int*>(blk)[64 + i] = sg;
-      blk[96 + i] = l2;
-    }
-  }
-}
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -1168,336 +1122,13 @@ __device__ __forceinline__ void store_pairs(bf16* row, const uint2 (&w)[NG]) {
   for (int g = 0; g < NG; g += 2) *reinterpret_cast<uint4*>(row + 8 * g) = make_uint4(w[g].x, w[g].y, w[g + 1].x, w[g + 1].y);
 }
 
-// grid: ceil(S/128) * Hkv * B blocks (1-D), 4 waves x 32 keys; query tiles of 32 rows over all q heads of
-// the kv group; NS-slot LDS-DMA ring.
-// D = 96 (Phi-3) runs the same structure on 256-byte LDS rows: the DMA rows read 64 bytes past each
-// 192-byte row (never past the tensor: the descriptors end at the last row's D elements) and only the
-// first D / 16 k-steps / D / 32 output tiles are used.
-template <int V, int D = 128, bool WS = false>
-__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv128_kernel(AttnArgs a, const float* ld) {
-  constexpr int NKK = D / 16, NDT = D / 32;
-  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 2 * 256, NS = 6;
-  constexpr int NDMA = 5;  // DMA instructions per wave per tile: Q 2, dO 2, row constants 1
-  using QI = Img<128>;
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases go to M0
-  const int S = a.S, grp = a.Hq / a.Hkv;
-  int L = (int)blockIdx.x;
-  const int hk = L % a.Hkv;
-  L /= a.Hkv;
-  int b, kb;
-  block_of(a, L, (S + 127) / 128, false, b, kb);
-  const int ks = kb * 128, kw = ks + wid * 32, kr = kw + r;
-  const int nT = (S + 31) / 32;
-  const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
-  const bf16* vp = a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh;
-  const int sk = (a.seg && kr < S) ? a.seg[(int64_t)b * S + kr] : 0;
-  const float sl2 = a.scale * kLog2e;
-
-  bfv8 kf[NKK], vf[NKK];
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    kf[kk] = gload8(kp + (int64_t)min(kr, S - 1) * a.k_ss + kk * 16 + hh * 8, kr < S);
-    vf[kk] = gload8(vp + (int64_t)min(kr, S - 1) * a.v_ss + kk * 16 + hh * 8, kr < S);
-  }
-  // hipcc's load counting does not see the asm DMAs below: make it retire its own loads here
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[kk]), "+v"(vf[kk]));
-  f32v16 dkt[NDT], dvt[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      dkt[dt][i] = 0.f;
-      dvt[dt][i] = 0.f;
-    }
-
-  const RunInfo kr_run = block_run(a, b, min(ks, S - 1), min(ks + 127, S - 1));
-  const int q_beg = a.causal ? ks : max(0, kr_run.rs) / 32 * 32;  // multiple of 32
-  int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
-  if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
-  const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
-  const int T = nq * grp;
-
-  if (T > 0) {
-    // ---- DMA of the next tile (tiles past T-1 repeat the last one) into the ring. The tile sequence
-    // is walked with scalar counters. Each descriptor covers one head from row q_beg on (rows past S
-    // fall outside it and read as zeros) and is rebuilt only when the walk enters the next head; the
-    // tile's byte offset inside the head rides in the lane offsets (one VALU add per DMA instead of
-    // three 64-bit descriptor builds per tile: the old per-tile descriptors were ~90 SALU per tile
-    // in a loop that issues one instruction per cycle from its single wave per SIMD).
-    int dq_off[2], dd_off[2];
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int row = 8 * wid + 4 * n + (lane >> 4);
-      const int ch = (lane & 15) ^ QI::swz(row);
-      dq_off[n] = (row * a.q_ss + ch * 8) * 2;
-      dd_off[n] = (row * a.d_ss + ch * 8) * 2;
-    }
-    const int ld_off = ((wid & 1) * 64 + lane) * 4;
-    asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]));
-    const int64_t q_rows = S - q_beg;
-    const int64_t nrec_q = ((q_rows - 1) * a.q_ss + D) * 2, nrec_d = ((q_rows - 1) * a.d_ss + D) * 2;
-    const int64_t nrec_l = (int64_t)nq * kLdTile * 4;
-    const bf16* qh0 = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * grp) * a.q_sh + (int64_t)q_beg * a.q_ss;
-    const bf16* dh0 = a.dout + (int64_t)b * a.d_sb + (int64_t)(hk * grp) * a.d_sh + (int64_t)q_beg * a.d_ss;
-    const float* lh0 = ld + (((int64_t)b * a.Hq + hk * grp) * nT + (q_beg >> 5)) * kLdTile;
-    const int step_q = BM * a.q_ss * 2, step_d = BM * a.d_ss * 2;
-    Rsrc qrs = make_rsrc4(qh0, nrec_q), drs = make_rsrc4(dh0, nrec_d), lrs = make_rsrc4(lh0, nrec_l);
-    int iss_g = 0, iss_q = 0, iss_n = 0, toff_q = 0, toff_d = 0, toff_l = 0;
-    auto issue = [&](const char* slot) {
-      // row constants: waves 0/2 fetch floats 0..63, waves 1/3 floats 64..127 (same bytes twice)
-      const char* q0 = slot + 8 * wid * 256;
-      dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, slot + 2 * IMG + (wid & 1) * 256,
-                dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
-      if (++iss_n < T) {
-        toff_q += step_q;
-        toff_d += step_d;
-        toff_l += kLdTile * 4;
-        if (++iss_q == nq) {
-          iss_q = 0;
-          ++iss_g;
-          toff_q = toff_d = toff_l = 0;
-          qrs = make_rsrc4(qh0 + (int64_t)iss_g * a.q_sh, nrec_q);
-          drs = make_rsrc4(dh0 + (int64_t)iss_g * a.d_sh, nrec_d);
-          lrs = make_rsrc4(lh0 + (int64_t)iss_g * nT * kLdTile, nrec_l);
-        }
-      }
-    };
-    // mask state of a tile: first query row, and whether any element of it needs the compare
-    int cur_q = 0;  // tile index inside its head of the tile whose S/dP is being computed
-    const bool seg_or_window = a.seg != nullptr || a.window >= 0;
-    struct TileMask {
-      int q0;
-      bool need, m_seg;
-    };
-    auto tile_mask = [&]() {
-      TileMask m;
-      m.q0 = q_beg + cur_q * BM;
-      m.need = a.causal && kw + 31 > m.q0;
-      m.m_seg = false;
-      if (seg_or_window) {
-        m.m_seg = seg_mask(a, kr_run, m.q0, m.q0 + 31);
-        m.need = m.need || m.m_seg || (a.window >= 0 && m.q0 + 31 - a.window > kw);
-      }
-      if (++cur_q == nq) cur_q = 0;
-      return m;
-    };
-    // lane-constant LDS byte offsets inside a 32-row image, computed once and kept opaque so hipcc
-    // does not re-derive the swizzle for every read inside the loop (it did: ~5 VALU per read)
-    int ro[NKK], to[NDT][2];
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) ro[kk] = QI::roff(r, 2 * kk + hh);
-    {
-      const int g = lane >> 4, i16 = lane & 15;
-      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        to[dt][0] = QI::toff(BM, row, dt * 32 + col);
-        to[dt][1] = QI::toff(BM, row + 8, dt * 32 + col);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(ro[kk]));
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+v"(to[dt][0]), "+v"(to[dt][1]));
-    auto rows = [&](const char* slot, bfv8* qr, bfv8* dr) {
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const char* p = slot + ro[kk];  // one VGPR address; the dO image is an immediate offset away
-        qr[kk] = lds_b128(p);
-        dr[kk] = lds_b128(p + IMG);
-      }
-    };
-    // A operands of the accumulator-as-B products from tile image pair `slot`: rows 16*s2..,
-    // columns 32*dt.. of Q (dK) and dO (dV); 8 VGPR addresses per tile, everything else immediates
-    auto trA2 = [&](const char* slot, bfv8 (&tq)[2][NDT], bfv8 (&td)[2][NDT]) {
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const char* p0 = slot + to[dt][0];
-        const char* p1 = slot + to[dt][1];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const s16v4 ql = lds_tr(p0 + 4096 * s2), qh = lds_tr(p1 + 4096 * s2);
-          const s16v4 dl = lds_tr(p0 + IMG + 4096 * s2), dh = lds_tr(p1 + IMG + 4096 * s2);
-          tq[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(ql, qh, 0, 1, 2, 3, 4, 5, 6, 7));
-          td[s2][dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(dl, dh, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-      }
-    };
-    // S = Q.K^T and dP = dO.V^T of the tile in `qr` / `dr`, accumulated from zero (the MFMA's inline 0)
-    auto sdp = [&](const bfv8* qr, const bfv8* dr, f32v16& s, f32v16& d) {
-      const f32v16 z = {};
-      s = mfma32(qr[0], kf[0], z);
-      d = mfma32(dr[0], vf[0], z);
-#pragma unroll
-      for (int kk = 1; kk < NKK; ++kk) {
-        s = mfma32(qr[kk], kf[kk], s);
-        d = mfma32(dr[kk], vf[kk], d);
-      }
-    };
-    // P = exp2(S * scale * log2e - lse * log2e) and dS = P (dP - delta) of the tile in `slot` (its row
-    // constants: -lse*log2e at floats 96.., -delta at 32..; rows past S / without keys carry -inf);
-    // masked elements (diagonal / window / segment tiles only) get P = 0
-    auto softmax = [&](const char* slot, const TileMask& m, const f32v16& s, const f32v16& d, bfv8 (&pb)[2],
-                       bfv8 (&db)[2]) {
-      const float* Ls = reinterpret_cast<const float*>(slot + 2 * IMG);
-      float lq[16], nd[16];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float4 l4 = *reinterpret_cast<const float4*>(Ls + 96 + 8 * c + 4 * hh);
-        const float4 d4 = *reinterpret_cast<const float4*>(Ls + 32 + 8 * c + 4 * hh);
-        lq[4 * c] = l4.x; lq[4 * c + 1] = l4.y; lq[4 * c + 2] = l4.z; lq[4 * c + 3] = l4.w;
-        nd[4 * c] = d4.x; nd[4 * c + 1] = d4.y; nd[4 * c + 2] = d4.z; nd[4 * c + 3] = d4.w;
-      }
-      // packed fp32 math (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: two lanes' worth per instruction)
-      // wherever two neighbouring elements take the same operation: the loop issues one instruction per
-      // cycle from its single wave per SIMD, so halving the VALU count of the softmax shortens it
-      typedef float f2 __attribute__((ext_vector_type(2)));
-      float p[16];
-      const f2 sl2v = {sl2, sl2};
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        if constexpr (V == 1) {  // scalar form (A/B reference)
-          p[i] = fexp2(fmaf(s[i], sl2, lq[i]));
-          p[i + 1] = fexp2(fmaf(s[i + 1], sl2, lq[i + 1]));
-        } else {
-          const f2 sv = {s[i], s[i + 1]}, lv = {lq[i], lq[i + 1]};
-          const f2 x = __builtin_elementwise_fma(sv, sl2v, lv);
-          p[i] = fexp2(x[0]);
-          p[i + 1] = fexp2(x[1]);
-        }
-      }
-      if (m.need) {
-        const int* Sg = reinterpret_cast<const int*>(Ls + 64);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          int4 s4 = make_int4(sk, sk, sk, sk);
-          if (m.m_seg) s4 = *reinterpret_cast<const int4*>(Sg + 8 * c + 4 * hh);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int qi = m.q0 + 8 * c + 4 * hh + j;
-            bool ok = true;
-            if (a.causal) ok = ok && (kr <= qi);
-            if (a.window >= 0) ok = ok && (qi - kr <= a.window);
-            if (m.m_seg) ok = ok && ((&s4.x)[j] == sk);
-            p[4 * c + j] = ok ? p[4 * c + j] : 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const int i = 8 * s2 + j;
-          const f2 pv = {p[i], p[i + 1]}, dv = {d[i], d[i + 1]}, nv = {nd[i], nd[i + 1]};
-          f2 ds;
-          if constexpr (V == 1) {
-            ds[0] = p[i] * (d[i] + nd[i]);
-            ds[1] = p[i + 1] * (d[i + 1] + nd[i + 1]);
-          } else {
-            ds = pv * (dv + nv);
-          }
-          pb[s2][j] = (__bf16)p[i];
-          pb[s2][j + 1] = (__bf16)p[i + 1];
-          db[s2][j] = (__bf16)ds[0];
-          db[s2][j + 1] = (__bf16)ds[1];
-        }
-    };
-
-    // ring slots (byte offsets) of tiles t-2 (the DMA target of iteration t), t-1, t, t+1
-    int sl_m2 = (NS - 1) * SLOT, sl_m1 = 0, sl_0 = SLOT, sl_p1 = 2 * SLOT;
-    // prologue: tiles 0..NS-2 in flight, wait for 0..2
-#pragma unroll
-    for (int t = 0; t < NS - 1; ++t) issue(smem + t * SLOT);
-    wait_vm<NDMA * (NS - 4)>();
-    ring_barrier();
-
-    bfv8 qr[NKK], dr[NKK];
-    f32v16 sacc, dacc;
-    rows(smem, qr, dr);
-    TileMask mprev = tile_mask();
-    sdp(qr, dr, sacc, dacc);
-    rows(smem + SLOT, qr, dr);
-
-    for (int t = 1; t <= T; ++t) {
-      issue(smem + sl_m2);
-      // ---- region A: S/dP of tile t  ||  softmax of tile t-1 + its transposed reads
-      const TileMask mcur = tile_mask();
-      const char* pslot = smem + sl_m1;
-      bfv8 trd[2][NDT], trq[2][NDT];
-      trA2(pslot, trq, trd);
-      f32v16 sn, dn;
-      sdp(qr, dr, sn, dn);
-      bfv8 pb[2], db[2];
-      softmax(pslot, mprev, sacc, dacc, pb, db);
-      // ---- region B: dV/dK of tile t-1  ||  row reads of tile t+1
-      rows(smem + sl_p1, qr, dr);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          dvt[dt] = mfma32(trd[s2][dt], pb[s2], dvt[dt]);
-          dkt[dt] = mfma32(trq[s2][dt], db[s2], dkt[dt]);
-        }
-      sacc = sn;
-      dacc = dn;
-      mprev = mcur;
-      sl_m2 = sl_m1;
-      sl_m1 = sl_0;
-      sl_0 = sl_p1;
-      sl_p1 = (sl_p1 + SLOT == NS * SLOT) ? 0 : sl_p1 + SLOT;
-      wait_vm<NDMA * (NS - 4)>();
-      if constexpr (V == 3)
-        ring_barrier_nodrain();
-      else
-        ring_barrier();
-    }
-    wait_vm<0>();  // no LDS-DMA may outlive the workgroup
-  }
-
-  if constexpr (WS) {  // widened store tail (widen_pairs): 16-byte stores of dK / dV rows
-    uint2 wk[4 * NDT], wv[4 * NDT];
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int g = 4 * dt + c;
-        wk[g].x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
-        wk[g].y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
-        wv[g].x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
-        wv[g].y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
-      }
-    widen_pairs(wk);
-    widen_pairs(wv);
-    if (kr < S) {
-      store_pairs(a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh + 8 * hh, wk);
-      store_pairs(a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh + 8 * hh, wv);
-    }
-  } else if (kr < S) {
-    bf16* dkp = a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh;
-    bf16* dvp = a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int d = dt * 32 + 8 * c + 4 * hh;
-        uint2 wk, wv;
-        wk.x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
-        wk.y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
-        wv.x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
-        wv.y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
-        *reinterpret_cast<uint2*>(dkp + d) = wk;
-        *reinterpret_cast<uint2*>(dvp + d) = wv;
-      }
-  }
-}
-
 // ============================================================================ backward dK/dV, v5
-// The dK/dV pass of fa_bwd_dkdv128_kernel (same grid, ring, DMA, masks and fragment layouts) with the
-// loop rebuilt as a software pipeline for its one wave per SIMD (profiles/r4_dkdv_pipeline.md). Per
+// grid: ceil(S/128) * Hkv * B blocks (1-D), 4 waves x 32 keys; query tiles of 32 rows over all q heads of
+// the kv group through an NSL-slot LDS-DMA ring. D = 96 (Phi-3) runs the same structure on 256-byte LDS rows:
+// the DMA rows read 64 bytes past each 192-byte row (never past the tensor: the descriptors end at the last
+// row's D elements) and only the first D / 16 k-steps / D / 32 output tiles are used. The loop is a software
+// pipeline for one wave per SIMD (profiles/r4_dkdv_pipeline.md; the earlier un-pipelined kernel and the
+// 64-keys-per-wave / hand-allocated variants lost their A/Bs and were removed, profiles/r5_dkdv6.md). Per
 // iteration t (one 32-row query tile):
 //  * phase A issues the 2*NKK S / dP MFMAs of tile t; in their gaps the Q / dO row fragments of tile t
 //    arrive just in time (two k-steps ahead), and the transposed Q^T / dO^T fragments of tile t-1 and the
@@ -1585,7 +1216,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv5_kernel(AttnArgs a, const 
   int q_end = a.window >= 0 ? min(S, ks + 128 + a.window) : S;
   if (a.rs) q_end = min(q_end, a.re[(int64_t)b * S + min(ks + 127, S - 1)] + 1);
   const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
-  const int T = (a.probe & 8) ? 0 : nq * grp;
+  const int T = FA_PROBE(a, 8) ? 0 : nq * grp;
 
   if (T > 0) {
     int dq_off[2], dd_off[2];
@@ -1953,7 +1584,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
   kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = (kv_end > kv_beg && !(a.probe & 1)) ? (kv_end - kv_beg + BN - 1) / BN : 0;
+  const int T = (kv_end > kv_beg && !FA_PROBE(a, 1)) ? (kv_end - kv_beg + BN - 1) / BN : 0;
   // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
   // and past the tensor on the last row of the last head -> zeros instead of a fault
   const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
@@ -1968,7 +1599,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
   bfv8 qf[NKK];
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk)
-    qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S && !(a.probe & 2));
+    qf[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S && !FA_PROBE(a, 2));
   if (a.rope_q && qrow < S) {  // fused RoPE: the rows arrive unrotated
     const int p = rope_pos(a, b, qrow);
     rope_frags<NKK>(qf, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
@@ -2152,9 +1783,9 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
         w[4 * dt + c].y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
       }
     widen_pairs(w);
-    if (qrow < S && !(a.probe & 4)) store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
+    if (qrow < S && !FA_PROBE(a, 4)) store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
   }
-  if (qrow < S && !(a.probe & 4)) {
+  if (qrow < S && !FA_PROBE(a, 4)) {
     if constexpr (!WS) {
       bf16* op = a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh;
 #pragma unroll
@@ -2172,1212 +1803,6 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
       a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (mu + __log2f(lt)) * kLn2 : -INFINITY;
     }
   }
-}
-
-// ============================================================================ forward, D = 128, v4
-// One wave per SIMD with 64 query rows per wave (two 32-row halves that share every K and V^T fragment
-// read, so a tile's LDS reads feed twice the MFMAs of fa_fwd3_kernel), 256-row blocks of 4 waves, 64-key
-// K/V tiles by LDS-DMA into a 4-slot ring (one barrier per tile, tile t+2 in flight under tile t).
-// Register files by role, allocated by hand (cdna guide §B, the 4-wave one-wave-per-SIMD structure): the
-// accumulator file holds O^T (a[0:127]), Q (a[128:191]) and the current K tile (a[192:255]) under literal
-// register names in the asm MFMAs and asm LDS reads (hipcc's allocator moved "a"-constrained copies of
-// them between registers and spilled when it owned them); the arch VGPRs hold two 64-score sets, bf16 P,
-// the V^T fragments and the softmax state, compiler-allocated. Each tile t is two phases of 32 MFMAs:
-//  * phase A: S^T(t) = K(t) Q^T, while the softmax of tile t-1 finishes (exps of its second key half, row
-//    sums, bf16 P) and the first V^T(t-1) fragments are read;
-//  * phase B: O^T += V^T(t-1) P^T(t-1), while the softmax of tile t starts (mask on diagonal / window / end
-//    tiles, row max, defer-max decision, exps of the first key half), the rest of V^T(t-1) is read just in
-//    time and K(t+1) is read into the accumulator file.
-// A rescale (a row max growing past kThr) multiplies O^T and l after phase B, when every P at the old max
-// (tile t-1) has been added and none at the new one. Dense rows (no segment ids), D = 128, no dropout.
-#define LLMT_ACLOB "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127","a128","a129","a130","a131","a132","a133","a134","a135","a136","a137","a138","a139","a140","a141","a142","a143","a144","a145","a146","a147","a148","a149","a150","a151","a152","a153","a154","a155","a156","a157","a158","a159","a160","a161","a162","a163","a164","a165","a166","a167","a168","a169","a170","a171","a172","a173","a174","a175","a176","a177","a178","a179","a180","a181","a182","a183","a184","a185","a186","a187","a188","a189","a190","a191","a192","a193","a194","a195","a196","a197","a198","a199","a200","a201","a202","a203","a204","a205","a206","a207","a208","a209","a210","a211","a212","a213","a214","a215","a216","a217","a218","a219","a220","a221","a222","a223","a224","a225","a226","a227","a228","a229","a230","a231","a232","a233","a234","a235","a236","a237","a238","a239","a240","a241","a242","a243","a244","a245","a246","a247","a248","a249","a250","a251","a252","a253","a254","a255"
-
-template <int... Is, class F>
-__device__ __forceinline__ void sfor_seq(std::integer_sequence<int, Is...>, F&& f) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-// f(std::integral_constant<int, i>) for i = 0 .. N-1: compile-time indices for "i" asm operands
-template <int N, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-  sfor_seq(std::make_integer_sequence<int, N>{}, f);
-}
-constexpr int fa4_ao(int dt, int qh) { return (dt * 2 + qh) * 16; }  // O^T tile (d tile, query half)
-constexpr int fa4_aq(int qh, int kk) { return 128 + (qh * 8 + kk) * 4; }  // Q fragment (query half, k-step)
-constexpr int fa4_ak(int kh, int kk) { return 192 + (kh * 8 + kk) * 4; }  // K fragment (key half, k-step)
-// phase B of fa_fwd4 exponentiates the first key half's 32 scores in gaps 10 .. 31: one in gaps 10 .. 21, two
-// in gaps 22 .. 31 (score index of the gap's first exp, and how many)
-constexpr int fa4_nexp(int g) { return g < 10 ? 0 : (g < 22 ? 1 : 2); }
-constexpr int fa4_exp0(int g) { return g < 22 ? g - 10 : 12 + 2 * (g - 22); }
-
-// two floats -> packed bf16 pair, issued where it stands (hipcc lowered element-wise bf16 inserts as one
-// block of conversions in front of the first MFMA that reads them)
-__device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
-  uint32_t r;
-  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
-}
-// exp2(x) with its row-sum add one instruction behind (the trans-use wait state by placement, see fwd3)
-__device__ __forceinline__ float exp_sum(float x, float& rs) {
-  float e;
-  asm volatile("v_exp_f32 %0, %2\n\ts_nop 0\n\tv_add_f32 %1, %1, %0" : "=&v"(e), "+v"(rs) : "v"(x));
-  return e;
-}
-
-// LDS-DMA of one 64-key K/V tile (no segment ids) for fa_fwd4: this wave's 16 K and 16 V rows, 4 per
-// instruction; the per-lane byte offsets (voffset: range-checked against the descriptor, so rows past the
-// sequence end read zeros) hold the tile's first row. The leading s_nop covers descriptor words written by
-// a VALU just before (VALU write of an SGPR -> VMEM read of it: 5 wait states; hipcc does not look inside
-// the statement).
-__device__ __forceinline__ void dma_tile8(const Rsrc& k, const Rsrc& v, uint32_t lds, int img, const int (&vk)[4],
-                                          const int (&vv)[4]) {
-  uint32_t keep;
-  asm volatile(
-      "s_nop 4\n\t"
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %11, 0 offen lds\n\t"
-      "s_add_u32 m0, %1, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %7, %12, 0 offen lds\n\t"
-      "s_add_u32 m0, %1, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %11, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %8, %12, 0 offen lds\n\t"
-      "s_add_u32 m0, %1, 0x800\n\ts_nop 0\n\tbuffer_load_dwordx4 %5, %11, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %9, %12, 0 offen lds\n\t"
-      "s_add_u32 m0, %1, 0xc00\n\ts_nop 0\n\tbuffer_load_dwordx4 %6, %11, 0 offen lds\n\t"
-      "s_add_u32 m0, m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %10, %12, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(lds), "s"(img), "v"(vk[0]), "v"(vk[1]), "v"(vk[2]), "v"(vk[3]), "v"(vv[0]), "v"(vv[1]), "v"(vv[2]),
-        "v"(vv[3]), "s"(k.w), "s"(v.w)
-      : "memory", "scc");
-}
-// x if key offset o is inside the row's range (base + o <= span, unsigned: idx_range), else -inf, in place;
-// VCC only (hipcc's 64-bit compare masks for a whole masked tile ran the kernel out of scalar registers)
-template <int O>
-__device__ __forceinline__ float range_or_ninf(float x, uint32_t base, uint32_t span) {
-  uint32_t t;
-  asm("v_add_u32 %1, %c3, %2\n\tv_cmp_le_u32 vcc, %1, %4\n\tv_cndmask_b32 %0, %5, %0, vcc"
-      : "+v"(x), "=&v"(t)
-      : "v"(base), "i"(O), "v"(span), "v"(-INFINITY)
-      : "vcc");
-  return x;
-}
-// single VALU instructions for the hand-spaced softmax gaps (hipcc would pair or fuse neighbours)
-__device__ __forceinline__ float v_exp1(float x) {
-  float r;
-  asm volatile("v_exp_f32 %0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
-__device__ __forceinline__ void v_add_ip(float& acc, float x) { asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc) : "v"(x)); }
-__device__ __forceinline__ float v_fma1(float x, float c, float d) {
-  float r;
-  asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(c), "v"(d));
-  return r;
-}
-
-template <int D = 128>
-__global__ __launch_bounds__(256, 1) void fa_fwd4_kernel(AttnArgs a) {
-  static_assert(D == 128, "fa_fwd4 is the D = 128 kernel");
-  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG, NSL = 4;
-  using KI = Img<128>;
-  __shared__ __attribute__((aligned(16))) char smem[NSL * SLOT];
-
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int S = a.S, grp = a.Hq / a.Hkv;
-  const int nqb = (S + 255) / 256;
-  int L = (int)blockIdx.x;
-  const int hk = L % a.Hkv;
-  L /= a.Hkv;
-  const int h = hk * grp + L % grp;
-  L /= grp;
-  int b, mb;
-  block_of(a, L, nqb, true, b, mb);
-  const int qs = mb * 256, qw = qs + wid * 64;
-  const int qrow0 = qw + r, qrow1 = qw + 32 + r;
-  const float sl2 = a.scale * kLog2e;
-
-  // O^T = 0 and Q into the accumulator file; this statement also claims all 256 accumulator registers for
-  // the kernel descriptor (the clobbers), so hipcc neither allocates nor spills into them
-  asm volatile(
-#define Z4(n) "v_accvgpr_write_b32 a" #n ", 0\n\t"
-      Z4(0) Z4(1) Z4(2) Z4(3) Z4(4) Z4(5) Z4(6) Z4(7) Z4(8) Z4(9) Z4(10) Z4(11) Z4(12) Z4(13) Z4(14) Z4(15)
-      Z4(16) Z4(17) Z4(18) Z4(19) Z4(20) Z4(21) Z4(22) Z4(23) Z4(24) Z4(25) Z4(26) Z4(27) Z4(28) Z4(29) Z4(30)
-      Z4(31) Z4(32) Z4(33) Z4(34) Z4(35) Z4(36) Z4(37) Z4(38) Z4(39) Z4(40) Z4(41) Z4(42) Z4(43) Z4(44) Z4(45)
-      Z4(46) Z4(47) Z4(48) Z4(49) Z4(50) Z4(51) Z4(52) Z4(53) Z4(54) Z4(55) Z4(56) Z4(57) Z4(58) Z4(59) Z4(60)
-      Z4(61) Z4(62) Z4(63) Z4(64) Z4(65) Z4(66) Z4(67) Z4(68) Z4(69) Z4(70) Z4(71) Z4(72) Z4(73) Z4(74) Z4(75)
-      Z4(76) Z4(77) Z4(78) Z4(79) Z4(80) Z4(81) Z4(82) Z4(83) Z4(84) Z4(85) Z4(86) Z4(87) Z4(88) Z4(89) Z4(90)
-      Z4(91) Z4(92) Z4(93) Z4(94) Z4(95) Z4(96) Z4(97) Z4(98) Z4(99) Z4(100) Z4(101) Z4(102) Z4(103) Z4(104)
-      Z4(105) Z4(106) Z4(107) Z4(108) Z4(109) Z4(110) Z4(111) Z4(112) Z4(113) Z4(114) Z4(115) Z4(116) Z4(117)
-      Z4(118) Z4(119) Z4(120) Z4(121) Z4(122) Z4(123) Z4(124) Z4(125) Z4(126) Z4(127)
-#undef Z4
-      ::: LLMT_ACLOB);
-  {
-    const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
-    sfor<2>([&](auto qc) {
-      constexpr int qh = decltype(qc)::value;
-      const int q = qh ? qrow1 : qrow0;
-      sfor<8>([&](auto kc) {
-        constexpr int kk = decltype(kc)::value;
-        const bfv8 x = gload8(qp + (int64_t)min(q, S - 1) * a.q_ss + kk * 16 + hh * 8, q < S);
-        const u32x4 w = __builtin_bit_cast(u32x4, x);
-        asm volatile("v_accvgpr_write_b32 a%c0, %4\n\tv_accvgpr_write_b32 a%c1, %5\n\t"
-                     "v_accvgpr_write_b32 a%c2, %6\n\tv_accvgpr_write_b32 a%c3, %7"
-                     :: "i"(fa4_aq(qh, kk)), "i"(fa4_aq(qh, kk) + 1), "i"(fa4_aq(qh, kk) + 2), "i"(fa4_aq(qh, kk) + 3),
-                     "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
-      });
-    });
-  }
-  // per-row key ranges as IdxRange pieces relative to key 0 of the tile: base0 + n0 is added per tile
-  int klo0, khi0, klo1, khi1;
-  key_interval(a, b, qrow0, klo0, khi0);
-  key_interval(a, b, qrow1, klo1, khi1);
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, nm[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f};
-
-  int kv_end = a.causal ? min(S, qs + 256) : S;
-  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = kv_beg / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
-  // this wave's tiles with any visible key: [wt0, wt1] (wave-uniform)
-  int wt1 = T - 1, wt0 = 0;
-  if (a.causal) wt1 = min(wt1, (min(qw + 63, S - 1) - kv_beg) / BN);
-  if (a.window >= 0) wt0 = max(0, (qw - a.window - kv_beg) / BN);
-  if (qw >= S) wt1 = -1;
-
-  if (T > 0) {
-    const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
-    const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, ((int64_t)(S - 1) * a.v_ss + D) * 2);
-    int vk[4], vv[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int row = 16 * wid + 4 * n + (lane >> 4);
-      const int ch = (lane & 15) ^ KI::swz(row);
-      vk[n] = (row * a.k_ss + ch * 8) * 2;
-      vv[n] = (row * a.v_ss + ch * 8) * 2;
-    }
-    const uint32_t lds0 = lds_addr(smem) + 16 * wid * 256;
-    const int kstep = BN * a.k_ss * 2, vstep = BN * a.v_ss * 2;
-    auto issue = [&](int t) {
-      int kr = (kv_beg / BN + t) * kstep, vr = (kv_beg / BN + t) * vstep;
-      // opaque: otherwise hipcc keeps the per-lane offsets of every unrolled step's tile precomputed in
-      // registers (it then parked some in the accumulator file, which the asm owns)
-      asm volatile("" : "+s"(kr), "+s"(vr));
-      const int ko[4] = {vk[0] + kr, vk[1] + kr, vk[2] + kr, vk[3] + kr};
-      const int vo[4] = {vv[0] + vr, vv[1] + vr, vv[2] + vr, vv[3] + vr};
-      dma_tile8(krs, vrs, lds0 + (t & 3) * SLOT, IMG, ko, vo);
-    };
-    int ro[8], to[4][2];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) ro[kk] = lds_addr(smem) + KI::roff(r, 2 * kk + hh);
-    {
-      const int g = lane >> 4, i16 = lane & 15;
-      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        to[dt][0] = lds_addr(smem) + KI::toff(BN, row, dt * 32 + col) + IMG;
-        to[dt][1] = lds_addr(smem) + KI::toff(BN, row + 8, dt * 32 + col) + IMG;
-      }
-    }
-    // K fragments (both key halves, k-step kk) of the tile in ring slot `sl` into the accumulator file
-    auto read_k = [&](int sl, auto kc) {
-      constexpr int kk = decltype(kc)::value;
-      const int addr = ro[kk] + sl * SLOT;
-      asm volatile("ds_read_b128 a[%c0:%c1], %4\n\tds_read_b128 a[%c2:%c3], %4 offset:8192"
-                   :: "i"(fa4_ak(0, kk)), "i"(fa4_ak(0, kk) + 3), "i"(fa4_ak(1, kk)), "i"(fa4_ak(1, kk) + 3), "v"(addr)
-                   : "memory");
-    };
-    // V^T fragment (keys 32kh + 16s2 .., columns 32dt ..) of the tile in ring slot `sl`
-    auto read_v = [&](int sl, int kh, int s2, int dt) -> bfv8 {
-      const int off = sl * SLOT + 256 * (32 * kh + 16 * s2);
-      using lp = __attribute__((address_space(3))) s16v4*;
-      const s16v4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(uintptr_t)(uint32_t)(to[dt][0] + off));
-      const s16v4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(uintptr_t)(uint32_t)(to[dt][1] + off));
-      return __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-
-    // ring slot 3 holds the "previous tile" V^T of a wave's first step when that is tile 0: P = 0 there, but
-    // 0 * (stale NaN / inf bits) would not be 0 — zero it once
-#pragma unroll
-    for (int i = 0; i < IMG / (16 * 256); ++i)
-      *reinterpret_cast<uint4*>(smem + 3 * SLOT + IMG + 16 * (tid + 256 * i)) = make_uint4(0, 0, 0, 0);
-    issue(0);
-    if (T > 1) issue(1);
-    wait_vm<0>();
-    ring_barrier();
-    sfor<8>([&](auto kc) { read_k(0, kc); });
-
-    // score sets of alternate steps ([key half][query half]); the set the wave's first step finishes as "the
-    // previous tile" starts at -inf (exp -> P = 0, row sums 0), so every step runs the same two phases
-    f32v16 sA[2][2], sB[2][2];
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) sB[x >> 1][x & 1][i] = -INFINITY;
-    uint32_t pw[2][2][2][4];  // bf16 P of the previous tile: [key half][query half][k-step][pair]
-#pragma unroll
-    for (int i = 0; i < 32; ++i) (&pw[0][0][0][0])[i] = 0u;  // the wave's first step has no previous tile
-    bool resc = false;
-
-    // phase A of tile t: S^T(t) into sc || finish the softmax of tile t-1: exps of its second key half sp[1]
-    // (the first half was exponentiated, summed and converted in phase B of the previous step), their row
-    // sums, bf16 P of that half
-    auto phase_a = [&](f32v16 (&sc)[2][2], f32v16 (&sp)[2][2], int vsl, bfv8 (&vr)[16]) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K tile in the accumulator file
-      __builtin_amdgcn_sched_barrier(0);
-      float rs0 = 0.f, rs1 = 0.f;
-      sfor<32>([&](auto gc) {
-        constexpr int g = decltype(gc)::value;
-        constexpr int kk = g >> 2, kh = (g >> 1) & 1, qh = g & 1;
-        if constexpr (kk == 0)
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], 0"
-                       : "=v"(sc[kh][qh])
-                       : "i"(fa4_ak(kh, kk)), "i"(fa4_ak(kh, kk) + 3), "i"(fa4_aq(qh, kk)), "i"(fa4_aq(qh, kk) + 3));
-        else
-          asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], %0"
-                       : "+v"(sc[kh][qh])
-                       : "i"(fa4_ak(kh, kk)), "i"(fa4_ak(kh, kk) + 3), "i"(fa4_aq(qh, kk)), "i"(fa4_aq(qh, kk) + 3));
-        // the second key half's 32 scores e = 16 fq + fi, three gap-stages apart so no gap waits on its own
-        // results: gap g scales (fma) and exponentiates score g, adds score g - 2 to its row sum and packs
-        // pair (g - 4, g - 3)
-        {
-          constexpr int fq = g >> 4, fi = g & 15;
-          sp[1][fq][fi] = v_exp1(v_fma1(sp[1][fq][fi], sl2, nm[fq]));
-        }
-        if constexpr (g >= 2) {
-          constexpr int e = g - 2;
-          v_add_ip((e >> 4) ? rs1 : rs0, sp[1][e >> 4][e & 15]);
-        }
-        if constexpr (g >= 4 && (g & 1) == 0) {
-          constexpr int e = g - 4, pq = e >> 4, ei = e & 15;
-          pw[1][pq][ei >> 3][(ei & 7) >> 1] = cvt_pk(sp[1][pq][ei], sp[1][pq][ei + 1]);
-        }
-        if constexpr (g == 30) {  // the first V^T fragments of phase B
-          vr[0] = read_v(vsl, 0, 0, 0);
-          vr[1] = read_v(vsl, 0, 0, 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      // the tail: scores 30, 31 into the sum, pairs 28 and 30 (a VALU pad after the last exp)
-      asm volatile("s_nop 1");
-      v_add_ip(rs1, sp[1][1][14]);
-      v_add_ip(rs1, sp[1][1][15]);
-      pw[1][1][1][2] = cvt_pk(sp[1][1][12], sp[1][1][13]);
-      pw[1][1][1][3] = cvt_pk(sp[1][1][14], sp[1][1][15]);
-      l[0] += rs0;
-      l[1] += rs1;
-      // the asm MFMAs are invisible to hipcc's hazard recognizer: XDL write -> VALU read (and VALU write ->
-      // MFMA operand read) wait states before the next phase touches their registers
-      asm volatile("s_nop 7\n\ts_nop 7");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-
-    // phase B of tile t: O^T += V^T(t-1) P^T(t-1) || start the softmax of tile t in sc (mask, row max,
-    // defer-max decision, exps + row sums of the first key half, its bf16 P into pw[0] once the P.V MFMAs of
-    // tile t-1 no longer read that half); K(t+1) into the accumulator file (a stale slot past the last tile is
-    // read and never used). `dummy`: the drain step past the wave's last tile, whose scores are all masked.
-    // Returns the first half's row sums (added to l after a rescale)
-    auto phase_b = [&](f32v16 (&sc)[2][2], int vsl, bfv8 (&vr)[16], int t, bool dummy, float (&rsn)[2]) {
-      const int n0 = kv_beg + t * BN;
-      const bool need_mask = dummy || (a.causal && n0 + BN - 1 > qw) || (a.window >= 0 && n0 < qw + 63 - a.window) ||
-                             n0 + BN > S || qw + 63 >= S;
-      if (need_mask) {  // diagonal / window / sequence-end tiles: out-of-range keys -> -inf
-        const IdxRange r0 = dummy ? IdxRange{1u, 0u} : idx_range(klo0, khi0, n0 + 4 * hh);
-        const IdxRange r1 = dummy ? IdxRange{1u, 0u} : idx_range(klo1, khi1, n0 + 4 * hh);
-        sfor<32>([&](auto ec) {
-          constexpr int e = decltype(ec)::value, kh = e >> 4, i = e & 15;
-          constexpr int o = 32 * kh + 8 * (i >> 2) + (i & 3);
-          sc[kh][0][i] = range_or_ninf<o>(sc[kh][0][i], r0.base, r0.span);
-          sc[kh][1][i] = range_or_ninf<o>(sc[kh][1][i], r1.base, r1.span);
-        });
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      float mx[2] = {0.f, 0.f}, mxa[2] = {0.f, 0.f}, mxb[2] = {0.f, 0.f}, u1 = 0.f, u2 = 0.f, u3 = 0.f;
-      rsn[0] = rsn[1] = 0.f;
-      sfor<32>([&](auto gc) {
-        constexpr int g = decltype(gc)::value;
-        // MFMA g: V^T fragment f = g / 2 (k-step f / 4 = (key half, s2), d tile f % 4), query half g % 2
-        constexpr int f = g >> 1, ks = f >> 2, dt = f & 3, qh = g & 1;
-        {
-          const uint32_t(&pp)[4] = pw[ks >> 1][qh][ks & 1];
-          const u32x4 pb = {pp[0], pp[1], pp[2], pp[3]};
-          asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
-                       :: "i"(fa4_ao(dt, qh)), "i"(fa4_ao(dt, qh) + 15), "v"(vr[f]), "v"(pb));
-        }
-        if constexpr (qh == 0 && f + 2 < 16) {  // fragment f + 2, three MFMAs ahead of its first use
-          constexpr int f2 = f + 2, k2 = f2 >> 2;
-          vr[f2] = read_v(vsl, k2 >> 1, k2 & 1, f2 & 3);
-        }
-        if constexpr (g < 9) {  // row maxima: 32 scores per query half, 8 per gap in three independent max3,
-          // folded into two running maxima one gap later
-          if constexpr (g >= 1) {
-            constexpr int q2 = (g - 1) >> 2;
-            mxa[q2] = (((g - 1) & 3) == 0) ? vmax3(u1, u2, u2) : vmax3(mxa[q2], u1, u2);
-            mxb[q2] = (((g - 1) & 3) == 0) ? u3 : fmaxf(mxb[q2], u3);
-          }
-          if constexpr (g < 8) {
-            constexpr int q2 = g >> 2, part = g & 3, k2 = part >> 1, i0 = (part & 1) * 8;
-            u1 = vmax3(sc[k2][q2][i0], sc[k2][q2][i0 + 1], sc[k2][q2][i0 + 2]);
-            u2 = vmax3(sc[k2][q2][i0 + 3], sc[k2][q2][i0 + 4], sc[k2][q2][i0 + 5]);
-            u3 = vmax3(sc[k2][q2][i0 + 6], sc[k2][q2][i0 + 7], sc[k2][q2][i0 + 7]);
-          }
-        }
-        if constexpr (g == 9) {  // both lane halves' maxima, then the defer-max decision
-#pragma unroll
-          for (int q2 = 0; q2 < 2; ++q2) {
-            mx[q2] = fmaxf(mxa[q2], mxb[q2]);
-            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx[q2]), __float_as_uint(mx[q2]),
-                                                            false, false);
-            mx[q2] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
-          }
-          resc = __any(mx[0] > m[0] + kThr || mx[1] > m[1] + kThr);
-#pragma unroll
-          for (int q2 = 0; q2 < 2; ++q2) {
-            const float mnew = resc ? fmaxf(m[q2], mx[q2]) : m[q2];
-            alpha[q2] = (mnew == -INFINITY || mnew == m[q2]) ? 1.f : fexp2(m[q2] - mnew);
-            m[q2] = mnew;
-            nm[q2] = (mnew == -INFINITY) ? 0.f : -mnew;
-          }
-        }
-        if constexpr (g >= 10) {  // exps of the first key half: 32 scores over gaps 10 .. 31; row sums 2 gaps later
-          constexpr int n = fa4_nexp(g), e0 = fa4_exp0(g);
-          sfor<n>([&](auto jc) {
-            constexpr int s = e0 + decltype(jc)::value, sq = s >> 4, si = s & 15;
-            sc[0][sq][si] = v_exp1(v_fma1(sc[0][sq][si], sl2, nm[sq]));
-          });
-        }
-        if constexpr (g >= 12) {
-          constexpr int n = fa4_nexp(g - 2), e0 = fa4_exp0(g - 2);
-          sfor<n>([&](auto jc) {
-            constexpr int s = e0 + decltype(jc)::value, sq = s >> 4, si = s & 15;
-            v_add_ip(rsn[sq], sc[0][sq][si]);
-          });
-        }
-        // bf16 pair p = g - 18 of the first half (its exps done, tile t-1's first-half P no longer read)
-        if constexpr (g >= 18) {
-          constexpr int p = g - 18, s = 2 * p, sq = s >> 4, si = s & 15;
-          pw[0][sq][si >> 3][(si & 7) >> 1] = cvt_pk(sc[0][sq][si], sc[0][sq][si + 1]);
-        }
-        if constexpr (g >= 4 && g < 12) read_k((t + 1) & 3, std::integral_constant<int, g - 4>{});
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      asm volatile("s_nop 1");  // the last exps -> their row-sum adds and packs
-      sfor<4>([&](auto jc) {  // row sums of the last two gaps' scores (28 .. 31)
-        constexpr int s = 28 + decltype(jc)::value;
-        v_add_ip(rsn[1], sc[0][1][s - 16]);
-      });
-      pw[0][1][1][2] = cvt_pk(sc[0][1][12], sc[0][1][13]);
-      pw[0][1][1][3] = cvt_pk(sc[0][1][14], sc[0][1][15]);
-    };
-
-    // the rare rescale of O^T (a[0:127]) after phase B: every P at the old max is in it, none at the new one
-    auto rescale = [&]() {
-      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // the last P.V MFMAs' results
-      // (tile t-1's P is all in O^T: phase B issued its last P.V MFMA before this)
-      sfor<8>([&](auto tc) {
-        constexpr int tile = decltype(tc)::value, qh = tile & 1;
-        sfor<16>([&](auto ic) {
-          constexpr int reg = tile * 16 + decltype(ic)::value;
-          float x;
-          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(reg));
-          x *= alpha[qh];
-          asm volatile("v_accvgpr_write_b32 a%c1, %0" :: "v"(x), "i"(reg));
-        });
-      });
-      asm volatile("s_nop 3" ::: "memory");  // accumulator write -> MFMA C read
-      l[0] *= alpha[0];
-      l[1] *= alpha[1];
-    };
-    auto finish_step = [&]() {
-      wait_vm<0>();  // this wave's DMA of tile t + 2
-      ring_barrier();
-    };
-    // a step with nothing to compute for this wave: its share of the ring traffic only
-    auto step_idle = [&](int t) {
-      if (t + 2 < T) issue(t + 2);
-      sfor<8>([&](auto kc) { read_k((t + 1) & 3, kc); });
-      finish_step();
-    };
-    // a compute step; sc = tile t's score set, sp = tile t-1's
-    auto step = [&](f32v16 (&sc)[2][2], f32v16 (&sp)[2][2], int t) {
-      if (t + 2 < T) issue(t + 2);
-      bfv8 vr[16];
-      float rsn[2];
-      phase_a(sc, sp, (t - 1) & 3, vr);
-      phase_b(sc, (t - 1) & 3, vr, t, t > wt1, rsn);
-      if (resc) rescale();
-      l[0] += rsn[0];  // tile t's first-half row sums, at the new scale
-      l[1] += rsn[1];
-      finish_step();
-    };
-
-    int t = 0;
-    if (wt0 <= wt1) {
-      for (; t < wt0; ++t) step_idle(t);
-      // steps wt0 .. wt1 + 1 (the last one drains P.V of tile wt1), score sets alternating A, B
-      for (; t <= wt1 + 1; t += 2) {
-        step(sA, sB, t);
-        if (t + 1 <= wt1 + 1) step(sB, sA, t + 1);
-      }
-      t = wt1 + 2;
-    }
-    for (; t <= T; ++t) step_idle(t);
-  }
-  // the last asm MFMAs' results are read by the epilogue
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-
-  sfor<2>([&](auto qc) {
-    constexpr int qh = decltype(qc)::value;
-    const float lt = l[qh] + __shfl_xor(l[qh], 32, 64);
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    uint2 w[16];
-    sfor<4>([&](auto dc) {
-      constexpr int dt = decltype(dc)::value;
-      float ov[16];
-      sfor<16>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        float x;
-        asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(fa4_ao(dt, qh) + i));
-        ov[i] = x;
-      });
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        w[4 * dt + c].x = pack_bf16x2(ov[4 * c] * inv, ov[4 * c + 1] * inv);
-        w[4 * dt + c].y = pack_bf16x2(ov[4 * c + 2] * inv, ov[4 * c + 3] * inv);
-      }
-    });
-    widen_pairs(w);
-    const int q = qh ? qrow1 : qrow0;
-    if (q < S) {
-      store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)q * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
-      if (hh == 0) {
-        const float mu = (m[qh] == -INFINITY) ? 0.f : m[qh];
-        a.lse[((int64_t)b * a.Hq + h) * S + q] = lt > 0.f ? (mu + __log2f(lt)) * kLn2 : -INFINITY;
-      }
-    }
-  });
-}
-// ============================================================================ backward dK/dV, v6
-// 64 keys per wave (two 32-key halves), dV^T and dK^T of both halves in the 256 accumulator registers
-// (asm-owned, like fa_fwd4: a[0:127] dV^T, a[128:255] dK^T). Every operand fragment read from LDS (Q / dO
-// rows, Q^T / dO^T transposed) feeds the two halves' MFMAs back to back, so a tile needs 1.1 LDS reads per
-// MFMA against fa_bwd_dkdv5's 1.75, and a 256-key workgroup of 4 waves moves each Q / dO tile through the
-// LDS-DMA ring for twice the keys (cdna guide, 'Attention backward': 64 keys per wave in 256 accumulator
-// registers). The wave's K fragments stay in VGPRs (64 registers); V of the workgroup's 256 keys sits in LDS
-// (a 64 KB swizzled image, the dP operand) next to a 5-slot Q / dO ring (tiles issued 3 ahead). Per 32-row
-// query tile t, four phases of 16 MFMAs:
-//   1  S(t), both halves (one accumulation chain each, interleaved per k-step: one Q row read per pair)
-//                                          || dS(t-1) of k-step 1 and its bf16 pairs
-//   2  dP(t), both halves                  || P = exp2(S scale log2e - lse log2e) of k-step 0, bf16 pairs
-//   3  dK(t-1) from Q^T(t-1) and dS(t-1)   || P of k-step 1, bf16 pairs
-//      (ring wait + barrier: tile t+1 landed, tile t-1's slot free)
-//   4  dV(t) from dO^T(t) and P(t)         || dS(t) of k-step 0 and its bf16 pairs
-// (diagnostic probes with everything but the MFMAs and the packs removed put the MFMA floor of this loop at
-// ~55 % of its time: the softmax VALU must spread over all four phases to hide under the MFMAs)
-// The fp32 scores of both halves (S / P, dP / dS: 64 registers) live from phase 1 to phase 4; the bf16 P and
-// dS operands (32 registers) from their pack to their MFMAs. Operand reads run two to three MFMAs ahead (LDS
-// latency under load); one accumulation chain needs no interleaving for throughput (MI355X_MICROARCH: 32
-// cycles back to back on one accumulator). Dense rows only (D = 128, causal / window, no segments).
-constexpr int d6_av(int h, int dt) { return (h * 4 + dt) * 16; }        // dV^T accumulator (key half, d tile)
-constexpr int d6_ak(int h, int dt) { return 128 + (h * 4 + dt) * 16; }  // dK^T accumulator
-
-template <int D = 128, int PF = 3, int PR = 0, bool DI = false>
-__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv6_kernel(AttnArgs a, const float* ld) {
-  static_assert(D == 128, "fa_bwd_dkdv6 is the D = 128 kernel");
-  constexpr int NKK = 8, NDT = 4, NB = 16;
-  constexpr int BM = 32, IMG = BM * 256, SLOT = 2 * IMG + 512, NS = 5, NDMA = 5;
-  constexpr int VIMG = 256 * 256;  // V of the workgroup's 256 keys
-  using QI = Img<128>;
-  __shared__ __attribute__((aligned(16))) char smem[VIMG + NS * SLOT];
-  char* const ring = smem + VIMG;
-
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int S = a.S, grp = a.Hq / a.Hkv;
-  int L = (int)blockIdx.x;
-  const int hk = L % a.Hkv;
-  L /= a.Hkv;
-  int b, kb;
-  block_of(a, L, (S + 255) / 256, false, b, kb);
-  const int ks = kb * 256, kw = ks + wid * 64;
-  const int nT = (S + 31) / 32;
-  const float sl2 = a.scale * kLog2e;
-
-  // dV^T = dK^T = 0; the clobbers claim all 256 accumulator registers for the kernel descriptor, so hipcc
-  // neither allocates nor spills into them
-  asm volatile("s_nop 0" ::: LLMT_ACLOB);
-  sfor<256>([&](auto ic) __attribute__((always_inline)) { asm volatile("v_accvgpr_write_b32 a%c0, 0" :: "i"(decltype(ic)::value)); });
-
-  // the wave's K fragments (lane: key kw + 32 h + r, columns 16 kk + 8 hh ..), rows past S read as zeros
-  bfv8 kf[2][NKK];
-  {
-    const bf16* kp = a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int key = kw + 32 * h + r;
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) kf[h][kk] = gload8(kp + (int64_t)min(key, S - 1) * a.k_ss + kk * 16 + hh * 8, key < S);
-    }
-  }
-  // the block's query tiles (dense rows: the range masks' query intervals are recomputed where a tile needs them)
-  const int q_beg = a.causal ? ks : 0;
-  const int q_end = a.window >= 0 ? min(S, ks + 256 + a.window) : S;
-  const int nq = q_end > q_beg ? (q_end - q_beg + BM - 1) / BM : 0;
-  const int T = nq * grp;
-  // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(kf[0][kk]), "+v"(kf[1][kk]));
-
-  if (T > 0) {
-    // per-lane DMA offsets, recomputed per tile (a handful of VALU ops beside the MFMAs; held across the loop they
-    // cost five of the registers the pipeline needs)
-    auto dma_offs = [&](int (&dq)[2], int (&dd)[2], int& dl) __attribute__((always_inline)) {
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int row = 8 * wid + 4 * n + (lane >> 4);
-        const int ch = (lane & 15) ^ QI::swz(row);
-        dq[n] = (row * a.q_ss + ch * 8) * 2;
-        dd[n] = (row * a.d_ss + ch * 8) * 2;
-      }
-      dl = ((wid & 1) * 64 + lane) * 4;
-    };
-    const int64_t q_rows = S - q_beg;
-    const int64_t nrec_q = ((q_rows - 1) * a.q_ss + D) * 2, nrec_d = ((q_rows - 1) * a.d_ss + D) * 2;
-    const int64_t nrec_l = (int64_t)nq * kLdTile * 4;
-    const bf16* qh0 = a.q + (int64_t)b * a.q_sb + (int64_t)(hk * grp) * a.q_sh + (int64_t)q_beg * a.q_ss;
-    const bf16* dh0 = a.dout + (int64_t)b * a.d_sb + (int64_t)(hk * grp) * a.d_sh + (int64_t)q_beg * a.d_ss;
-    const float* lh0 = ld + (((int64_t)b * a.Hq + hk * grp) * nT + (q_beg >> 5)) * kLdTile;
-    const int step_q = BM * a.q_ss * 2, step_d = BM * a.d_ss * 2;
-    Rsrc qrs = make_rsrc4(qh0, nrec_q), drs = make_rsrc4(dh0, nrec_d), lrs = make_rsrc4(lh0, nrec_l);
-    int iss_g = 0, iss_q = 0, iss_n = 0, toff_q = 0, toff_d = 0, toff_l = 0;
-    // one tile's DMA into ring slot `sl`; past the last tile the last one is loaded again (every iteration
-    // issues the same number of pieces, so one counted wait fits every iteration)
-    auto issue = [&](int sl) __attribute__((always_inline)) {
-      const char* q0 = ring + sl * SLOT + 8 * wid * 256;
-      int dq_off[2], dd_off[2], ld_off;
-      dma_offs(dq_off, dd_off, ld_off);
-      asm volatile("" : "+v"(dq_off[0]), "+v"(dq_off[1]), "+v"(dd_off[0]), "+v"(dd_off[1]), "+v"(ld_off));
-      dma_tile5(qrs, drs, lrs, q0, q0 + 4 * 256, q0 + IMG, q0 + IMG + 4 * 256, ring + sl * SLOT + 2 * IMG + (wid & 1) * 256,
-                dq_off[0] + toff_q, dq_off[1] + toff_q, dd_off[0] + toff_d, dd_off[1] + toff_d, ld_off + toff_l);
-      if (++iss_n < T) {
-        toff_q += step_q;
-        toff_d += step_d;
-        toff_l += kLdTile * 4;
-        if (++iss_q == nq) {
-          iss_q = 0;
-          ++iss_g;
-          toff_q = toff_d = toff_l = 0;
-          qrs = make_rsrc4(qh0 + (int64_t)iss_g * a.q_sh, nrec_q);
-          drs = make_rsrc4(dh0 + (int64_t)iss_g * a.d_sh, nrec_d);
-          lrs = make_rsrc4(lh0 + (int64_t)iss_g * nT * kLdTile, nrec_l);
-        }
-      }
-    };
-    // tiles 0 .. NS-3, then V of the workgroup's keys (16 pieces of 4 rows per wave, swizzled like QI)
-#pragma unroll
-    for (int t = 0; t < NS - 2; ++t) issue(t);
-    {
-      const Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh + (int64_t)ks * a.v_ss,
-                                  S > ks ? ((int64_t)(S - 1 - ks) * a.v_ss + D) * 2 : 0);
-#pragma unroll
-      for (int n = 0; n < 16; ++n) {
-        const int row = 64 * wid + 4 * n + (lane >> 4);
-        const int ch = (lane & 15) ^ QI::swz(row);
-        dma16(vrs, smem + (64 * wid + 4 * n) * 256, (row * a.v_ss + ch * 8) * 2);
-      }
-    }
-    wait_vm<0>();
-    ring_barrier();
-
-    // LDS offsets: row reads of k-step kk at ro0 ^ (32 kk) (the swizzle moves 16-byte chunks within bits 4-7
-    // of the offset, disjoint from the row's bits), transposed reads of d tile dt at to0[x] ^ (64 dt)
-    const int ro0 = QI::roff(r, hh);
-    int to0[2];
-    {
-      const int g = lane >> 4, i16 = lane & 15;
-      const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
-      to0[0] = QI::toff(BM, row, col);
-      to0[1] = QI::toff(BM, row + 8, col);
-    }
-    const char* vimg = smem + 64 * wid * 256;
-    auto rd_q = [&](int sl, int kk) __attribute__((always_inline)) {
-      if constexpr (PR & 8) return kf[1][kk & 7];
-      return lds_b128(ring + sl * SLOT + (ro0 ^ (32 * kk)));
-    };
-    auto rd_d = [&](int sl, int kk) __attribute__((always_inline)) {
-      if constexpr (PR & 8) return kf[0][kk & 7];
-      return lds_b128(ring + sl * SLOT + IMG + (ro0 ^ (32 * kk)));
-    };
-    auto rd_v = [&](int h, int kk) __attribute__((always_inline)) {
-      if constexpr (PR & 8) return kf[h][(kk + 1) & 7];
-      return lds_b128(vimg + 32 * 256 * h + (ro0 ^ (32 * kk)));
-    };
-    // transposed fragment i of a dV / dK phase: i < 8 -> dO^T (dV product), else Q^T (dK); s2 = (i / 4) & 1
-    auto rd_t = [&](int sl, int i) __attribute__((always_inline)) -> bfv8 {
-      if constexpr (PR & 8) return kf[i & 1][i & 7];
-      const int s2 = (i / NDT) & 1, dt = i % NDT;
-      const char* base = ring + sl * SLOT + (i < 2 * NDT ? IMG : 0) + 4096 * s2;
-      const s16v4 lo = lds_tr(base + (to0[0] ^ (64 * dt))), hi = lds_tr(base + (to0[1] ^ (64 * dt)));
-      return __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-
-    f32v16 sc[2], dc[2];       // S and dP - delta of both key halves (the MFMA chains' accumulators)
-    f32v16 cdc;                // DI: -delta of the lane's 16 query rows, the dP chains' initial accumulator
-    const float* nds = nullptr;  // !DI: -delta of the tile whose dS is computed (LDS)
-    float pv[2][16], dsv[2][16];  // P and dS element-wise (scalars: no vector re-assembly around the updates)
-    u32x4 pw[2][2], dw[2][2];  // bf16 P / dS operands [key half][k-step]
-    const float* lqs = nullptr;  // the tile's row constants in LDS: -lse log2e (floats 96 ..), -delta (32 ..)
-    bfv8 qf[NKK], df[NKK], vf[2][NKK], tf[8];
-    auto q0_of = [&](int t) __attribute__((always_inline)) { return q_beg + (t % nq) * BM; };
-    auto need_mask = [&](int q0) __attribute__((always_inline)) {
-      return (a.causal && q0 < kw + 63) || (a.window >= 0 && q0 + 31 - kw > a.window);
-    };
-    // exp element e of a tile (k-step e >> 4, half (e >> 3) & 1, value 8 k-step + (e & 7))
-    // row constant pair of values v, v + 1 (v even): rows 8 (v >> 2) + 4 hh + (v & 3), adjacent floats
-    auto cpair = [&](const float* base, int v) __attribute__((always_inline)) {
-      return *reinterpret_cast<const float2*>(base + 8 * (v >> 2) + 4 * hh + (v & 3));
-    };
-    // exps of the element pair e, e + 1 (e even)
-    auto ex2 = [&](auto ec) __attribute__((always_inline)) {
-      constexpr int e = decltype(ec)::value, h = (e >> 3) & 1, v = 8 * (e >> 4) + (e & 7);
-      if constexpr (PR & 4) return;
-      const float2 l = cpair(lqs, v);
-      float e0, e1;
-      asm volatile("v_fma_f32 %0, %2, %4, %5\n\tv_fma_f32 %1, %3, %4, %6\n\tv_exp_f32 %0, %0\n\tv_exp_f32 %1, %1"
-                   : "=&v"(e0), "=&v"(e1)
-                   : "v"(pv[h][v]), "v"(pv[h][v + 1]), "v"(sl2), "v"(l.x), "v"(l.y));
-      pv[h][v] = e0;
-      pv[h][v + 1] = e1;
-    };
-    // dS = P (dP - delta) of the pair e, e + 1
-    auto ds2 = [&](auto ec) __attribute__((always_inline)) {
-      constexpr int e = decltype(ec)::value, h = (e >> 3) & 1, v = 8 * (e >> 4) + (e & 7);
-      if constexpr (PR & 4) {
-        dsv[h][v] = dc[h][v];
-        dsv[h][v + 1] = dc[h][v + 1];
-        return;
-      }
-      float t0, t1;
-      if constexpr (DI) {  // dc already holds dP - delta (the dP chains start from -delta, see ph_s)
-        asm volatile("v_mul_f32 %0, %2, %3\n\tv_mul_f32 %1, %4, %5"
-                     : "=&v"(t0), "=&v"(t1) : "v"(dc[h][v]), "v"(pv[h][v]), "v"(dc[h][v + 1]), "v"(pv[h][v + 1]));
-      } else {
-        const float2 n = cpair(nds, v);
-        asm volatile("v_add_f32 %0, %2, %3\n\tv_add_f32 %1, %4, %5\n\tv_mul_f32 %0, %6, %0\n\tv_mul_f32 %1, %7, %1"
-                     : "=&v"(t0), "=&v"(t1)
-                     : "v"(dc[h][v]), "v"(n.x), "v"(dc[h][v + 1]), "v"(n.y), "v"(pv[h][v]), "v"(pv[h][v + 1]));
-      }
-      dsv[h][v] = t0;
-      dsv[h][v + 1] = t1;
-    };
-    // bf16 pair w of a tile's operands (k-step w >> 3, half (w >> 2) & 1, word w & 3)
-    auto pk_p = [&](auto wc) __attribute__((always_inline)) {
-      constexpr int w = decltype(wc)::value, s2 = w >> 3, h = (w >> 2) & 1, j = w & 3, v = 8 * s2 + 2 * j;
-      pw[h][s2][j] = cvt_pk(pv[h][v], pv[h][v + 1]);
-    };
-    auto pk_d = [&](auto wc) __attribute__((always_inline)) {
-      constexpr int w = decltype(wc)::value, s2 = w >> 3, h = (w >> 2) & 1, j = w & 3, v = 8 * s2 + 2 * j;
-      dw[h][s2][j] = cvt_pk(dsv[h][v], dsv[h][v + 1]);
-    };
-    auto consts_of = [&](int sl, int off) __attribute__((always_inline)) {
-      return reinterpret_cast<const float*>(ring + sl * SLOT + 2 * IMG) + off;
-    };
-    // phase 1: S(t) of both halves (tile in slot sl; Q rows 0, 1 prefetched), the dP operands' first k-steps
-    // and -lse log2e fetched in its gaps
-    auto ph_s = [&](int sl, auto&& valu) __attribute__((always_inline)) {
-      lqs = consts_of(sl, 96);
-      sfor<16>([&](auto gc) __attribute__((always_inline)) {
-        constexpr int g = decltype(gc)::value, kk = g >> 1, h = g & 1;
-        valu(gc);
-        if constexpr (kk == 0)
-          if constexpr (PR & 64) asm volatile("" : "=&v"(sc[h]) : "v"(qf[0]), "v"(kf[h][0]));
-          else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(sc[h]) : "v"(qf[0]), "v"(kf[h][0]));
-        else
-          if constexpr (PR & 64) asm volatile("" : "+v"(sc[h]) : "v"(qf[kk]), "v"(kf[h][kk]));
-          else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sc[h]) : "v"(qf[kk]), "v"(kf[h][kk]));
-        if constexpr (h == 0 && kk + 2 < NKK) qf[kk + 2] = rd_q(sl, kk + 2);
-        if constexpr (DI && g >= 14) {  // -delta of the tile's rows (floats 32 ..): the dP chains' initial value
-#pragma unroll
-          for (int c = 2 * (g - 14); c < 2 * (g - 13); ++c) {
-            const float4 x = *reinterpret_cast<const float4*>(consts_of(sl, 32) + 8 * c + 4 * hh);
-            cdc[4 * c] = x.x; cdc[4 * c + 1] = x.y; cdc[4 * c + 2] = x.z; cdc[4 * c + 3] = x.w;
-          }
-        }
-        if constexpr (g >= 13) {  // dP operands of k-step 0: dO row, V of both halves
-          constexpr int y = g - 13;
-          if constexpr (y == 0) df[0] = rd_d(sl, 0);
-          else vf[y - 1][0] = rd_v(y - 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    };
-    // VALU of the four phases (P and dS of a tile spread over all of them; one exp pair, dS pair or two packs
-    // per gap beside the MFMA and its operand reads):
-    //   phase 1 (S(t)):        dS of tile t-1, k-step 1 (gaps 0 .. 7), its bf16 pairs (2 .. 9)
-    //   phase 2 (dP(t)):       exps 0 .. 15 (gaps 2 .. 9), P k-step 0 (10 .. 15)
-    //   phase 3 (dK(t-1)):     exps 16 .. 31 (gaps 0 .. 7), P k-step 1 (8 .. 15)
-    //   phase 4 (dV(t)):       dS k-step 0 (gaps 0 .. 7), its bf16 pairs (8 .. 15)
-    auto v1 = [&](auto gc) __attribute__((always_inline)) {
-      constexpr int g = decltype(gc)::value;
-      if constexpr (g < 8) ds2(std::integral_constant<int, 16 + 2 * g>{});
-      if constexpr (g >= 2 && g < 10) pk_d(std::integral_constant<int, g + 6>{});  // words 8 .. 15, a gap behind
-    };
-    auto v3 = [&](auto gc) __attribute__((always_inline)) {
-      constexpr int g = decltype(gc)::value;
-      if constexpr (g < 8) ex2(std::integral_constant<int, 16 + 2 * g>{});
-      else pk_p(std::integral_constant<int, g>{});
-    };
-    auto v4 = [&](auto gc) __attribute__((always_inline)) {
-      constexpr int g = decltype(gc)::value;
-      if constexpr (g < 8) ds2(std::integral_constant<int, 2 * g>{});
-      else pk_d(std::integral_constant<int, g - 8>{});
-    };
-    // phase 2: dP(t) of both halves || exps 0 .. 19 (from gap 2: two MFMAs behind the last S MFMA, the
-    // XDL-write -> VALU-read wait states), P k-step 0 packed; MSK: the range mask on every score first
-    auto ph_dp = [&](auto mc, int sl, int q0) __attribute__((always_inline)) {
-      constexpr bool MSK = decltype(mc)::value;
-      sfor<16>([&](auto gc) __attribute__((always_inline)) {
-        constexpr int g = decltype(gc)::value, kk = g >> 1, h = g & 1;
-        if constexpr (kk == 0)
-          if constexpr (DI)
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]), "v"(cdc));
-          else
-            if constexpr (PR & 64) asm volatile("" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]));
-            else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(dc[h]) : "v"(df[0]), "v"(vf[h][0]));
-        else
-          if constexpr (PR & 64) asm volatile("" : "+v"(dc[h]) : "v"(df[kk]), "v"(vf[h][kk]));
-          else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(dc[h]) : "v"(df[kk]), "v"(vf[h][kk]));
-        // next k-step's operands one k-step (two MFMAs) ahead: deeper would not fit the register file
-        if constexpr (h == 0 && kk + 1 < NKK) df[kk + 1] = rd_d(sl, kk + 1);
-        if constexpr (kk + 1 < NKK) vf[h][kk + 1] = rd_v(h, kk + 1);
-        if constexpr (g == 1) {  // the scores as scalars; MSK: out-of-range queries -> -inf (P = 0, dS = 0)
-          sfor<2>([&](auto hc) __attribute__((always_inline)) {
-            constexpr int hm = decltype(hc)::value;
-            if constexpr (MSK) {
-              int qlo, qhi;
-              query_interval(a, b, kw + 32 * hm + r, qlo, qhi);
-              const IdxRange rg = idx_range(qlo, qhi, q0 + 4 * hh);
-              sfor<16>([&](auto vc) __attribute__((always_inline)) {
-                constexpr int v = decltype(vc)::value, o = 8 * (v >> 2) + (v & 3);
-                pv[hm][v] = range_or_ninf<o>(sc[hm][v], rg.base, rg.span);
-              });
-            } else {
-#pragma unroll
-              for (int v = 0; v < 16; ++v) pv[hm][v] = sc[hm][v];
-            }
-          });
-        }
-        if constexpr (!(PR & 16)) {
-          if constexpr (g >= 2 && g < 10) ex2(std::integral_constant<int, 2 * (g - 2)>{});  // exps 0 .. 15
-          if constexpr (g >= 10) {  // P k-step 0
-            pk_p(std::integral_constant<int, g - 10>{});
-            if constexpr (g >= 14) pk_p(std::integral_constant<int, g - 8>{});
-          }
-        }
-        if constexpr (PR & 32) {  // probe: phases 3 and 4's VALU here too
-          v3(gc);
-          v4(gc);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    };
-    // phases 3 / 4: dK (KQ = true: Q^T fragments, dS operands) or dV (dO^T, P) of both halves from the slot
-    // `sl` (transposed fragments 0, 1 prefetched), || valu(gap); `qsl` >= 0: the next tile's first Q rows at
-    // gaps 14, 15
-    auto ph_g = [&](auto kc, int sl, auto&& valu, int qsl) __attribute__((always_inline)) {
-      constexpr bool KQ = decltype(kc)::value;
-      sfor<16>([&](auto gc) __attribute__((always_inline)) {
-        constexpr int i = decltype(gc)::value, f = i >> 1, h = i & 1, s2 = f >> 2, dt = f & 3;
-        if constexpr (PR & 64)
-          asm volatile("" :: "v"(tf[f]), "v"(KQ ? dw[h][s2] : pw[h][s2]));
-        else if constexpr (KQ)
-          asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
-                       :: "i"(d6_ak(h, dt)), "i"(d6_ak(h, dt) + 15), "v"(tf[f]), "v"(dw[h][s2]));
-        else
-          asm volatile("v_mfma_f32_32x32x16_bf16 a[%c0:%c1], %2, %3, a[%c0:%c1]"
-                       :: "i"(d6_av(h, dt)), "i"(d6_av(h, dt) + 15), "v"(tf[f]), "v"(pw[h][s2]));
-        if constexpr (h == 0 && f + 2 < 8) tf[f + 2] = rd_t(sl, (KQ ? 8 : 0) + f + 2);
-        valu(gc);
-        if constexpr (i >= 14) {
-          if (qsl >= 0) qf[i - 14] = rd_q(qsl, i - 14);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    };
-    auto pref_t = [&](int sl, bool kq) __attribute__((always_inline)) {
-      tf[0] = rd_t(sl, kq ? 8 : 0);
-      tf[1] = rd_t(sl, kq ? 9 : 1);
-    };
-    auto dp = [&](int sl, int q0) __attribute__((always_inline)) {
-      if (need_mask(q0))
-        ph_dp(std::true_type{}, sl, q0);
-      else
-        ph_dp(std::false_type{}, sl, q0);
-    };
-    auto no_valu = [](auto) __attribute__((always_inline)) {};
-
-    int sl_c = 0;  // ring slot of tile t
-    qf[0] = rd_q(0, 0);
-    qf[1] = rd_q(0, 1);
-    {  // tile 0: phase 3 without dK(t-1)
-      const int q0 = q0_of(0);
-      issue(NS - 2);
-      ph_s(0, no_valu);
-      dp(0, q0);
-      nds = consts_of(0, 32);
-      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // no MFMA between dP's chains and their reads
-      sfor<16>([&](auto gc) __attribute__((always_inline)) { v3(gc); });
-      pref_t(0, false);
-      wait_vm<2 * NDMA>();
-      ring_barrier();
-      ph_g(std::false_type{}, 0, v4, T > 1 ? 1 % NS : -1);
-    }
-    for (int t = 1; t < T; ++t) {
-      const int sl_p = sl_c;
-      sl_c = sl_c + 1 == NS ? 0 : sl_c + 1;
-      const int q0 = q0_of(t);
-      if constexpr (!(PR & 1)) issue(sl_c + NS - 2 >= NS ? sl_c - 2 : sl_c + NS - 2);
-      if constexpr (PR & 16) ph_s(sl_c, no_valu);
-      else ph_s(sl_c, v1);  // with dS(t-1) k-step 1 (nds still tile t-1's)
-      dp(sl_c, q0);
-      pref_t(sl_p, true);
-      nds = consts_of(sl_c, 32);  // -delta of tile t, whose dS phases 4 and 1 compute
-      if constexpr (PR & 16) {  // probe: every VALU of the tile beside the accumulator-destination MFMAs
-        ph_g(std::true_type{}, sl_p, [&](auto gc) __attribute__((always_inline)) {
-          constexpr int g = decltype(gc)::value;
-          v1(gc);
-          v3(gc);
-          if constexpr (g < 8) ex2(std::integral_constant<int, 2 * g>{});
-          else pk_p(std::integral_constant<int, g - 8>{});
-        }, -1);
-      } else if constexpr (PR & 32) {
-        ph_g(std::true_type{}, sl_p, no_valu, -1);
-      } else {
-        ph_g(std::true_type{}, sl_p, v3, -1);
-      }
-      pref_t(sl_c, false);
-      if constexpr (PR & 1) {
-        wait_vm<0>();
-      } else {
-        wait_vm<2 * NDMA>();  // tile t + 1 (issued three iterations ago) landed; slot t - 1 read for the last time
-      }
-      if constexpr (!(PR & 2)) ring_barrier();
-      const int sl_n = sl_c + 1 == NS ? 0 : sl_c + 1;
-      if constexpr (PR & 32) ph_g(std::false_type{}, sl_c, no_valu, t + 1 < T ? sl_n : -1);
-      else ph_g(std::false_type{}, sl_c, v4, t + 1 < T ? sl_n : -1);
-    }
-    {  // drain: dS k-step 1 and dK of the last tile
-      sfor<16>([&](auto gc) __attribute__((always_inline)) { v1(gc); });
-      pref_t(sl_c, true);
-      asm volatile("s_nop 7" ::: "memory");  // the last packs -> MFMA operand reads
-      ph_g(std::true_type{}, sl_c, no_valu, -1);
-    }
-    wait_vm<0>();  // no LDS-DMA may outlive the workgroup
-  }
-  // the last asm MFMAs' accumulator writes -> the reads below
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    f32v16 dkt[NDT], dvt[NDT];
-    sfor<NDT>([&](auto dc_) __attribute__((always_inline)) {
-      constexpr int dt = decltype(dc_)::value;
-      sfor<16>([&](auto ic) __attribute__((always_inline)) {
-        constexpr int i = decltype(ic)::value;
-        float x, y;
-        if (h == 0) {
-          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(d6_ak(0, dt) + i));
-          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(y) : "i"(d6_av(0, dt) + i));
-        } else {
-          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(d6_ak(1, dt) + i));
-          asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(y) : "i"(d6_av(1, dt) + i));
-        }
-        dkt[dt][i] = x;
-        dvt[dt][i] = y;
-      });
-    });
-    const int kr = kw + 32 * h + r;
-    if (a.rope_dk && kr < S) {  // fused RoPE: gradient of the unrotated k
-      const int p = rope_pos(a, b, kr);
-      rope_acc_inv<D>(dkt, a.rcos + (int64_t)p * (D / 2), a.rsin + (int64_t)p * (D / 2), hh);
-    }
-    uint2 wk[4 * NDT], wv[4 * NDT];
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int g = 4 * dt + c;
-        wk[g].x = pack_bf16x2(dkt[dt][4 * c] * a.scale, dkt[dt][4 * c + 1] * a.scale);
-        wk[g].y = pack_bf16x2(dkt[dt][4 * c + 2] * a.scale, dkt[dt][4 * c + 3] * a.scale);
-        wv[g].x = pack_bf16x2(dvt[dt][4 * c], dvt[dt][4 * c + 1]);
-        wv[g].y = pack_bf16x2(dvt[dt][4 * c + 2], dvt[dt][4 * c + 3]);
-      }
-    widen_pairs(wk);
-    widen_pairs(wv);
-    if (kr < S) {
-      store_pairs(a.dk + (int64_t)b * a.dk_sb + (int64_t)kr * a.dk_ss + (int64_t)hk * a.dk_sh + 8 * hh, wk);
-      store_pairs(a.dv + (int64_t)b * a.dv_sb + (int64_t)kr * a.dv_ss + (int64_t)hk * a.dv_sh + 8 * hh, wv);
-    }
-  }
-}
-
-#undef LLMT_ACLOB
-
-// ============================================================================ forward, head-chained
-// fa_fwd3 with NH query heads per workgroup (same batch row and query block, so the same key-tile range,
-// masks and segment runs): the NH heads' tiles form one sequence through the K/V LDS-DMA ring, so the
-// first tile of head j+1 is in flight under the last tile of head j and its Q fragments are loaded there
-// too; head j's O / LSE are written at the boundary. A block then pays the prologue (Q + first K/V tile
-// latency with nothing to hide it) once per NH heads: that fixed cost is ~6.5 tiles' worth per block,
-// the whole kernel at short sequences / packed documents (profiles/r3_attention_bwd_atomic_floor.md).
-// Grid: ceil(S/128) * (Hq / NH) * B blocks, head chains fastest, heaviest query blocks first.
-template <int D, int NH>
-__global__ __launch_bounds__(256, 2) void fa_fwd3c_kernel(AttnArgs a) {
-  constexpr int NKK = D / 16, NDT = D / 32;
-  constexpr int BN = 64, IMG = BN * 256, SLOT = 2 * IMG + 256;
-  using KI = Img<128>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
-
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int S = a.S, grp = a.Hq / a.Hkv;
-  const int nqb = (S + 127) / 128;
-  int L = (int)blockIdx.x;
-  int h0;
-  if (grp % NH == 0) {  // GQA: kv head fastest (the blocks of one XCD share a kv head's K/V in its L2)
-    const int hk = L % a.Hkv;
-    L /= a.Hkv;
-    h0 = hk * grp + (L % (grp / NH)) * NH;
-    L /= grp / NH;
-  } else {  // chains span kv heads (MHA): consecutive heads
-    const int nch = a.Hq / NH;
-    h0 = (L % nch) * NH;
-    L /= nch;
-  }
-  int b, mb;
-  block_of(a, L, nqb, true, b, mb);
-  const int qs = mb * 128, qw = qs + wid * 32, qrow = qw + r;
-  const float sl2 = a.scale * kLog2e;
-  int sq = (a.seg && qrow < S) ? a.seg[(int64_t)b * S + qrow] : -2;
-
-  auto load_q = [&](int h, bfv8 (&qd)[NKK]) {
-    const bf16* qp = a.q + (int64_t)b * a.q_sb + (int64_t)h * a.q_sh;
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) qd[kk] = gload8(qp + (int64_t)min(qrow, S - 1) * a.q_ss + kk * 16 + hh * 8, qrow < S);
-  };
-  bfv8 qf[NKK];
-  load_q(h0, qf);
-  // hipcc does not count the asm DMAs: retire its own loads before the first one is issued
-  asm volatile("" : "+v"(sq));
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
-  f32v16 ot[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
-  float m = -INFINITY, l = 0.f;
-
-  // O / LSE of head h from the running state, then the state reset for the next head
-  auto finish = [&](int h) {
-    const float lt = l + __shfl_xor(l, 32, 64);
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    uint2 w[4 * NDT];
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        w[4 * dt + c].x = pack_bf16x2(ot[dt][4 * c] * inv, ot[dt][4 * c + 1] * inv);
-        w[4 * dt + c].y = pack_bf16x2(ot[dt][4 * c + 2] * inv, ot[dt][4 * c + 3] * inv);
-      }
-    widen_pairs(w);
-    if (qrow < S) {
-      store_pairs(a.out + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * a.o_sh + 8 * hh, w);
-      if (hh == 0) {
-        const float mu = (m == -INFINITY) ? 0.f : m;
-        a.lse[((int64_t)b * a.Hq + h) * S + qrow] = lt > 0.f ? (mu + __log2f(lt)) * kLn2 : -INFINITY;
-      }
-    }
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) ot[dt][i] = 0.f;
-    m = -INFINITY;
-    l = 0.f;
-  };
-
-  const RunInfo qr = block_run(a, b, qs, min(qs + 127, S - 1));
-  int kv_end = a.causal ? min(S, qs + 128) : S;
-  if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
-  int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
-  kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = kv_end > kv_beg ? (kv_end - kv_beg + BN - 1) / BN : 0;
-
-  if (T == 0) {
-#pragma unroll
-    for (int j = 0; j < NH; ++j) finish(h0 + j);
-    return;
-  }
-  // K/V descriptors of the chain head being fetched, rebuilt when the fetch moves to the next kv head;
-  // records end with the last row's D elements (the 256-byte DMA rows of D < 128 read past a row -> zeros
-  // instead of a fault)
-  const int64_t krec = ((int64_t)(S - 1) * a.k_ss + D) * 2, vrec = ((int64_t)(S - 1) * a.v_ss + D) * 2;
-  int fhk = h0 / grp;
-  Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)fhk * a.k_sh, krec);
-  Rsrc vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)fhk * a.v_sh, vrec);
-  const Rsrc srs = make_rsrc4(a.seg ? a.seg + (int64_t)b * S : nullptr, a.seg ? (int64_t)S * 4 : 0);
-  // tile u of the chain = tile u % T of head u / T, in ring slot u & 1
-  auto issue = [&](int u, int j, int t) {
-    const char* slot = smem + __builtin_amdgcn_readfirstlane((u & 1) * SLOT);
-    const int n0 = kv_beg + t * BN;
-    int vk[4], vv[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int row = 16 * wid + 4 * n + (lane >> 4);
-      const int ch = (lane & 15) ^ KI::swz(row);
-      vk[n] = ((n0 + row) * a.k_ss + ch * 8) * 2;
-      vv[n] = ((n0 + row) * a.v_ss + ch * 8) * 2;
-    }
-    const int hk = (h0 + j) / grp;
-    if (hk != fhk) {  // wave-uniform: a new kv head (MHA, or a chain crossing a GQA group)
-      fhk = hk;
-      krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, krec);
-      vrs = make_rsrc4(a.v + (int64_t)b * a.v_sb + (int64_t)hk * a.v_sh, vrec);
-    }
-    dma_tile9(krs, vrs, srs, slot + 16 * wid * 256, IMG, slot + 2 * IMG, vk, vv, (n0 + lane) * 4);
-  };
-  int ro[NKK], to[NDT][2];
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) ro[kk] = KI::roff(r, 2 * kk + hh);
-  {
-    const int g = lane >> 4, i16 = lane & 15;
-    const int row = 4 * (g >> 1) + (i16 >> 2), col = 16 * (g & 1) + 4 * (i16 & 3);
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      to[dt][0] = KI::toff(BN, row, dt * 32 + col);
-      to[dt][1] = KI::toff(BN, row + 8, dt * 32 + col);
-    }
-  }
-
-  issue(0, 0, 0);
-  wait_vm<0>();
-  ring_barrier();
-  int j = 0, t = 0;
-  const int U = NH * T;
-  for (int u = 0; u < U; ++u) {
-    const char* slot = smem + __builtin_amdgcn_readfirstlane((u & 1) * SLOT);
-    const int n0 = kv_beg + t * BN;
-    const bool last = t == T - 1;
-    if (u + 1 < U) {
-      if (last)
-        issue(u + 1, j + 1, 0);
-      else
-        issue(u + 1, j, t + 1);
-    }
-    bfv8 fr[16];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) fr[8 * tt + kk] = lds_b128(slot + 8192 * tt + ro[kk]);
-    __builtin_amdgcn_sched_barrier(0);
-    f32v16 st[2];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) st[tt][i] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) st[tt] = mfma32(fr[8 * tt + kk], qf[kk], st[tt]);
-    }
-    // the next head's Q into the registers the S^T chain just consumed: the loads fly under the rest of
-    // the tile (softmax, P.V)
-    if (last && j + 1 < NH) load_q(h0 + j + 1, qf);
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const char* base = slot + IMG + 256 * (32 * tt + 16 * s2);
-          const s16v4 lo = lds_tr(base + to[dt][0]), hi = lds_tr(base + to[dt][1]);
-          fr[8 * tt + 4 * s2 + dt] = __builtin_bit_cast(bfv8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-    __builtin_amdgcn_sched_barrier(0);
-    const bool m_causal = a.causal && (n0 + BN - 1 > qw);
-    const bool m_window = a.window >= 0 && (n0 < qw + 31 - a.window);
-    const bool m_end = n0 + BN > S;
-    const bool m_seg = seg_mask(a, qr, n0, n0 + BN - 1);
-    if (m_causal || m_window || m_end || m_seg || qw + 31 >= S) {
-      const int* Ss = reinterpret_cast<const int*>(slot + 2 * IMG);
-      const int lim = qrow - n0 - 4 * hh, lo = qrow - a.window - n0 - 4 * hh, hi = S - 1 - n0 - 4 * hh;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          int4 sk = make_int4(sq, sq, sq, sq);
-          if (m_seg) sk = *reinterpret_cast<const int4*>(Ss + 32 * tt + 8 * c + 4 * hh);
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            const int ko = 32 * tt + 8 * c + jj;
-            bool ok = (ko <= hi) && (qrow < S);
-            if (a.causal) ok = ok && (ko <= lim);
-            if (a.window >= 0) ok = ok && (ko >= lo);
-            if (m_seg) ok = ok && ((&sk.x)[jj] == sq);
-            if (!ok) st[tt][4 * c + jj] = -INFINITY;
-          }
-        }
-    }
-    float mx0 = vmax3(st[0][0], st[0][1], st[0][2]), mx1 = vmax3(st[1][0], st[1][1], st[1][2]);
-#pragma unroll
-    for (int i = 3; i < 15; i += 2) {
-      mx0 = vmax3(mx0, st[0][i], st[0][i + 1]);
-      mx1 = vmax3(mx1, st[1][i], st[1][i + 1]);
-    }
-    float smax = vmax3(mx0, st[0][15], vmax3(mx1, st[1][15], mx1));
-    smax = fmaxf(smax, __shfl_xor(smax, 32, 64)) * sl2;
-    if (__any(smax > m + kThr)) {
-      const float mnew = fmaxf(m, smax);
-      const float alpha = (mnew == -INFINITY) ? 1.f : fexp2(m - mnew);
-      m = mnew;
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) ot[dt][i] *= alpha;
-    }
-    const float nm = (m == -INFINITY) ? 0.f : -m;
-    float rs0 = 0.f, rs1 = 0.f;
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        st[tt][i] = fexp2(fmaf(st[tt][i], sl2, nm));
-        st[tt][i + 1] = fexp2(fmaf(st[tt][i + 1], sl2, nm));
-        rs0 += st[tt][i];
-        rs1 += st[tt][i + 1];
-      }
-    l += rs0 + rs1;
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bfv8 pb = acc_as_b(st[tt], s2);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) ot[dt] = mfma32(fr[8 * tt + 4 * s2 + dt], pb, ot[dt]);
-      }
-    __builtin_amdgcn_sched_barrier(0);
-    wait_vm<0>();  // this wave's DMA of tile u + 1 (and the next head's Q loads)
-    if (last) {
-      finish(h0 + j);
-      if (j + 1 < NH) {
-        // the asm wait above retired the Q loads; this statement makes hipcc place its own wait for
-        // them here (already satisfied) instead of in front of the next tile's MFMAs, after the DMA
-#pragma unroll
-        for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
-      }
-      ++j;
-      t = 0;
-    } else {
-      ++t;
-    }
-    ring_barrier();
-  }
-  wait_vm<0>();  // the last head's O stores
 }
 
 // ============================================================================ backward dQ, D = 128, v3
@@ -3433,7 +1858,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   if (!a.causal && a.rs) kv_end = min(kv_end, a.re[(int64_t)b * S + min(qs + 127, S - 1)] + 1);
   int kv_beg = a.window >= 0 ? max(0, qs - a.window) : 0;
   kv_beg = max(kv_beg, qr.rs) / BN * BN;
-  const int T = (kv_end > kv_beg && !(a.probe & 8)) ? (kv_end - kv_beg + BN - 1) / BN : 0;
+  const int T = (kv_end > kv_beg && !FA_PROBE(a, 8)) ? (kv_end - kv_beg + BN - 1) / BN : 0;
   // records end with the last row's D elements: the 256-byte DMA rows of D < 128 read past a row,
   // and past the tensor on the last row of the last head -> zeros instead of a fault
   const Rsrc krs = make_rsrc4(a.k + (int64_t)b * a.k_sb + (int64_t)hk * a.k_sh, ((int64_t)(S - 1) * a.k_ss + D) * 2);
@@ -3657,61 +2082,41 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
 
 using namespace llmt;
 
-// GQA head pairs (two query heads per 8-wave workgroup sharing the K/V ring, fa_fwd3_kernel /
-// fa_bwd_dq3_kernel NW = 8) against one head per 4-wave workgroup, in one process
-// (profiles/r3_attention_head_pairs_ab.jsonl): B4 S8192 Hq32 Hkv8 forward 2.183 -> 2.111 ms, backward
-// 8.146 -> 7.889 ms (dQ); B2 S4096 equal; B32 S1024 forward 0.446 -> 0.486, backward 1.483 -> 1.532 (one
-// workgroup per CU exposes the per-block prologue that two independent workgroups hide). In the Llama-3-8B
-// step, though, pairs on every dense S8192 call lost 5 ms/step (1497.5 / 1498.7 vs 1492.6 / 1493.0 ms,
-// alternating runs on one box): an 8-wave workgroup waits for a whole CU's worth of free slots while the
-// optimizer stream's kernels overlap the forward. Opt-in only (forward variant 7, dQ variant 3).
-static bool pairs_pay(const int*, int) { return false; }
-
-// dK/dV kernel variant, read on every launch so one process can A/B them (LLMT_FA_BWD_VARIANT):
-//   1 = end-of-tile barrier after an LDS drain and scalar softmax (A/B reference), 3 = barrier without
-//   the drain (rows prefetched for the next tile stay in flight across it) and packed softmax. (A
-//   sched-group pinned schedule of the same loop measured 9.17 vs 8.12 ms at B4 S8192 and was removed.)
-static int dkdv_variant() {
-  const char* e = getenv("LLMT_FA_BWD_VARIANT");
-  // 4 = 3 with the widened dK / dV store tail: B32 S1024 1.496 -> 1.476 ms, B64 S512 1.058 -> 1.029 ms,
-  // S8192 unchanged, bitwise-equal gradients (profiles/r3_attention_wide_store_ab.jsonl)
-  // 5 = the software-pipelined loop (fa_bwd_dkdv5_kernel): B4 S8192 Hq32 Hkv8 backward 8.150 -> 8.017 ms in
-  // one process, bitwise-equal gradients on every checked shape (benchmarks/attn_variant_check.py)
-  return e ? atoi(e) : 5;  // 3 vs 1, in-process A/B: B4 S8192 8.117 vs 8.186 ms, bitwise-equal gradients
+// Kernel selection. One kernel family per pass and head dim (D = 64 / 96 / 128):
+//   forward  fa_fwd3_kernel      (LDS-DMA K/V ring, fused Q rotation, range masks)
+//   dQ       fa_bwd_dq3_kernel   (also computes delta and the per-tile row constants for the dK/dV pass)
+//   dK/dV    fa_bwd_dkdv5_kernel (software-pipelined, one wave per SIMD, GQA heads looped in-kernel)
+// plus the generic kernels (fa_fwd_kernel / fa_bwd_{delta,dq,dkdv}_kernel) for dropout and other head dims.
+// Losing variants of earlier rounds (one-wave-per-SIMD hand-allocated forward / dK/dV, head chains, GQA head
+// pairs, the un-pipelined dK/dV loop, the separate prep pass) were removed after their A/Bs
+// (profiles/r5_attention_fwd4.md, r5_dkdv6.md, r3_attention_head_pairs_ab.jsonl, r4_negative_probes.jsonl).
+// Knobs, read per launch (recorded by ops/native.py llmt_env() into run metadata):
+//   LLMT_FA_GENERIC=1     the generic kernels for every launch (numerics reference);
+//   LLMT_FA_RANGE_MASK=0  per-element mask compares instead of range masks (A/B reference);
+//   LLMT_FA_EARLY_DMA=0   row loads before the first ring tiles in the prologues (A/B reference);
+//   LLMT_FA_BMAJOR=0      batch-interleaved block order of dense rows (A/B reference; B4 S8192 Hq32 Hkv8 with
+//                         the default batch-major order: forward 2.102 -> 2.068 ms, backward 7.795 -> 7.732 ms).
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
+static bool generic_only() { return env_int("LLMT_FA_GENERIC", 0) == 1; }
+static int range_masks() { return env_int("LLMT_FA_RANGE_MASK", 1); }
+static int early_dma() { return env_int("LLMT_FA_EARLY_DMA", 1); }
+static int bmajor_order() { return env_int("LLMT_FA_BMAJOR", 1); }
+#ifdef LLMT_DIAG
+static int attn_probe() { return env_int("LLMT_FA_PROBE", 0); }
+#else
+static int attn_probe() { return 0; }
+#endif
 
-// range masks (AttnArgs::rmask; LLMT_FA_RANGE_MASK=0: per-element compares, the A/B reference)
-static int range_masks() {
-  const char* e = getenv("LLMT_FA_RANGE_MASK");
-  return e ? atoi(e) : 1;
-}
-
-// prologue order (AttnArgs::early), read per launch for A/B (LLMT_FA_EARLY_DMA)
-static int early_dma() {
-  const char* e = getenv("LLMT_FA_EARLY_DMA");
-  return e ? atoi(e) : 1;
-}
-
-// ring slots of the dK/dV kernel (fa_bwd_dkdv5_kernel NSL), read per launch for A/B (LLMT_FA_D5_RING): 8 for
-// D=128 (packed Llama rows, same process: 8 docs 2.900 -> 2.890 ms, 32 docs 1.546 -> 1.511 ms fwd+bwd; dense
-// unchanged), 6 for D=96 (dense 3.635 vs 3.649 ms, packed 2.183 vs 2.189; profiles/r5_dkdv_ring_ab.jsonl)
-static int d5_ring(bool seg, int D = 128) {
-  (void)seg;
-  const char* e = getenv("LLMT_FA_D5_RING");
-  if (e) return atoi(e) == 8 ? 8 : 6;
-  return D == 128 ? 8 : 6;
-}
-
-static int attn_probe() {
-  const char* e = getenv("LLMT_FA_PROBE");
-  return e ? atoi(e) : 0;
-}
-
-// block order of the 1-D attention grids (AttnArgs::bmajor), read per launch for A/B (LLMT_FA_BMAJOR)
-// (B4 S8192 Hq32 Hkv8: forward 2.102 -> 2.068 ms, backward 7.795 -> 7.732 ms in one process)
-static int bmajor_order() {
-  const char* e = getenv("LLMT_FA_BMAJOR");
-  return e ? atoi(e) : 1;
+// 1 in the diagnostic library (probes compiled in), 0 in the production one
+extern "C" int llmt_attn_diag_build() {
+#ifdef LLMT_DIAG
+  return 1;
+#else
+  return 0;
+#endif
 }
 
 static void set_dropout(AttnArgs& a, float p, uint32_t seed) {
@@ -3760,17 +2165,8 @@ static bool rope_ok(const void* rpos, const float* rcos, const float* rsin, int6
          strides32({rp_sb, rp_ss});
 }
 
-static int fwd_variant() {
-  const char* fve = getenv("LLMT_FA_FWD_VARIANT");
-  return fve ? atoi(fve) : 4;
-}
 // does the forward launch for this problem go to fa_fwd3_kernel (the kernel with the fused Q rotation)?
-static bool fwd_uses_fwd3(int D, int variant, bool drop, bool rmask, bool seg) {
-  if (drop) return false;
-  const bool chain = variant == 5 || variant == 6;
-  if (D == 64 || D == 96) return variant != 0 && !chain;
-  return !chain && !(variant == 10 && rmask && !seg) && (variant == 2 || variant == 3 || variant >= 4);
-}
+static bool fwd_uses_fwd3(int D, bool drop) { return !drop && !generic_only() && (D == 64 || D == 96 || D == 128); }
 
 extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
                                           const int* seg, int B, int S, int Hq, int Hkv, int D, int64_t q_sb,
@@ -3809,19 +2205,12 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
   a.rmask = range_masks() && (seg == nullptr || a.rs != nullptr);
   a.early = early_dma();
   a.probe = attn_probe();
-  dim3 grid((S + 127) / 128, Hq, B);
-  // B1 S8192 Hq32 Hkv8: fwd3 0.659 ms (834 TF/s; 977 TF/s at B4), fa_fwd_kernel 0.907 (variant 0), the
-  // removed one-wave-per-SIMD ring forward 1.043; 3 = fwd3 with compiler-placed row-sum adds, 2 = with the
-  // inline-asm adds (A/B reference); read per launch
-  // 4 = 3 with the widened O store tail (T21), in one process: B4 S8192 2.199 vs 2.203 ms, B32 S1024 0.429
-  // vs 0.458, B64 S512 0.314 vs 0.343 ms (the per-block cost of short sequences / packed documents),
-  // bitwise-equal output (profiles/r3_attention_wide_store_ab.jsonl)
-  const int variant = fwd_variant();  // 3 vs 2 in one process: B4 S8192 2.145 vs 2.168 ms, same output
+  const bool v3 = fwd_uses_fwd3(D, a.drop_thresh != 0);
   if (rope) {
     // fused RoPE: q holds unrotated queries (k is already rotated). fa_fwd3_kernel rotates its rows on load;
-    // every other kernel gets the rotated rows in the qrot scratch (q itself is never written)
+    // the generic kernel gets the rotated rows in the qrot scratch (q itself is never written)
     set_rope(a, rpos, rpos64, rp_sb, rp_ss, rcos, rsin, rP, qrot, D);
-    if (fwd_uses_fwd3(D, variant, a.drop_thresh != 0, a.rmask, seg != nullptr)) {
+    if (v3) {
       a.rope_q = 1;
     } else {
       if (!qrot) return hipErrorInvalidValue;
@@ -3829,74 +2218,38 @@ extern "C" hipError_t llmt_flash_attn_fwd(const void* q, const void* k, const vo
       use_qrot(a);
     }
   }
-  // head chains (fa_fwd3c: 4 query heads per workgroup, bitwise-equal output) pay standalone where a
-  // block's heads have their own K/V: MHA B8 S4096 H32 D128 1.567 -> 1.391 ms, D96 1.631 -> 1.245 ms; with
-  // GQA they lose (B4 S8192 Hq32 Hkv8 2.230 -> 2.507 ms; profiles/r3_attention_head_chain_ab.jsonl). In the
-  // Phi-3 IT step (packed MHA) they cost 3 ms/step (688.4 / 690.3 vs 685.9 / 686.2 ms alternating on one
-  // box), so chains are opt-in: variants 5 / 6 = chains of 2 / 4; 8 = one head per workgroup. Against the
-  // round-5 forward they lose standalone too (B8 S4096 H32 D96 dense 0.983 vs 1.131 / 1.241 ms, packed
-  // document-major 0.431 vs 0.752 / 1.016 ms; profiles/r4_negative_probes.jsonl).
-  const int grp = Hq / Hkv;
-  const int chain = variant == 5 ? (Hq % 2 == 0 ? 2 : 0) : variant == 6 ? (Hq % 4 == 0 ? 4 : 0) : 0;
+  const dim3 grid((S + 127) / 128, Hq, B);
+  // fa_fwd3: B1 S8192 Hq32 Hkv8 0.659 ms (834 TF/s; 977 TF/s at B4) vs 0.907 for the generic kernel;
+  // RS = 2 (rmask): permlane32 row max, asm exp / row-sum pairs (2.091 -> 2.054 ms at B4 S8192); the widened
+  // O store tail (T21) pays at short rows (B64 S512 0.343 -> 0.314 ms; profiles/r3_attention_wide_store_ab.jsonl)
   const unsigned nb1 = (unsigned)((S + 127) / 128 * Hq * B);
+#define LLMT_FWD(DD)                                                  \
+  if (!v3)                                                            \
+    fa_fwd_kernel<DD><<<grid, 256, 0, stream>>>(a);                   \
+  else if (a.rmask)                                                   \
+    fa_fwd3_kernel<DD, 2, 1><<<nb1, 256, 0, stream>>>(a);             \
+  else                                                                \
+    fa_fwd3_kernel<DD, 1, 1, 4, true><<<nb1, 256, 0, stream>>>(a);
   switch (D) {
-    case 64:  // the v3 structure on 128-byte rows (256-byte LDS pitch)
-      if (a.drop_thresh || variant == 0)
-        fa_fwd_kernel<64><<<grid, 256, 0, stream>>>(a);
-      else if (chain == 4)
-        fa_fwd3c_kernel<64, 4><<<nb1 / 4, 256, 0, stream>>>(a);
-      else if (chain == 2)
-        fa_fwd3c_kernel<64, 2><<<nb1 / 2, 256, 0, stream>>>(a);
-      else if (a.rmask)
-        fa_fwd3_kernel<64, 2, 1><<<nb1, 256, 0, stream>>>(a);
-      else
-        fa_fwd3_kernel<64, 1, 1, 4, true><<<nb1, 256, 0, stream>>>(a);
-      break;
-    case 96:  // Phi-3: the v3 structure on 192-byte rows (256-byte LDS pitch)
-      if (a.drop_thresh || variant == 0)
-        fa_fwd_kernel<96><<<grid, 256, 0, stream>>>(a);
-      else if (chain == 4)
-        fa_fwd3c_kernel<96, 4><<<nb1 / 4, 256, 0, stream>>>(a);
-      else if (chain == 2)
-        fa_fwd3c_kernel<96, 2><<<nb1 / 2, 256, 0, stream>>>(a);
-      else if (a.rmask)
-        fa_fwd3_kernel<96, 2, 1><<<nb1, 256, 0, stream>>>(a);
-      else
-        fa_fwd3_kernel<96, 1, 1, 4, true><<<nb1, 256, 0, stream>>>(a);
-      break;
-    case 128: {
-      if (a.drop_thresh)  // dropout lives in the generic kernels
-        fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
-      else if (variant == 10 && a.rmask && !seg)  // one wave per SIMD, 64 rows per wave (fa_fwd4_kernel)
-        fa_fwd4_kernel<128><<<(S + 255) / 256 * Hq * B, 256, 0, stream>>>(a);
-      else if (variant == 2)  // row sums through the inline-asm add (each behind its own wait state)
-        fa_fwd3_kernel<128><<<nb1, 256, 0, stream>>>(a);
-      else if (variant == 3)  // dwordx2 O store tail (A/B reference)
-        fa_fwd3_kernel<128, 1><<<nb1, 256, 0, stream>>>(a);
-      else if (chain == 4)
-        fa_fwd3c_kernel<128, 4><<<nb1 / 4, 256, 0, stream>>>(a);
-      else if (chain == 2)
-        fa_fwd3c_kernel<128, 2><<<nb1 / 2, 256, 0, stream>>>(a);
-      else if (grp % 2 == 0 && (variant == 7 || (variant == 4 && pairs_pay(seg, S))))  // GQA head pairs
-        fa_fwd3_kernel<128, 1, 1, 8><<<nb1 / 2, 512, 0, stream>>>(a);
-      else if (variant == 9 && a.rmask)  // compiler-placed row-sum adds, bpermute row max (A/B reference)
-        fa_fwd3_kernel<128, 1, 1><<<nb1, 256, 0, stream>>>(a);
-      else if (variant >= 4 && a.rmask)  // permlane32 row max, asm exp / row-sum pairs: 2.091 -> 2.054 ms
-        fa_fwd3_kernel<128, 2, 1><<<nb1, 256, 0, stream>>>(a);
-      else if (variant >= 4)
-        fa_fwd3_kernel<128, 1, 1, 4, true><<<nb1, 256, 0, stream>>>(a);
-      else
-        fa_fwd_kernel<128><<<grid, 256, 0, stream>>>(a);
-    } break;
+    case 64: { LLMT_FWD(64) } break;    // the v3 structure on 128-byte rows (256-byte LDS pitch)
+    case 96: { LLMT_FWD(96) } break;    // Phi-3: 192-byte rows (256-byte LDS pitch)
+    case 128: { LLMT_FWD(128) } break;
     default: return hipErrorInvalidValue;
   }
+#undef LLMT_FWD
   return hipGetLastError();
 }
 
 // 1: a forward with fused RoPE needs no qrot scratch (the launch goes to fa_fwd3_kernel)
 extern "C" int llmt_flash_attn_fwd_rope_inkernel(int D, float drop_p, int has_seg, int seg_runs) {
-  const bool rmask = range_masks() && (!has_seg || seg_runs);
-  return fwd_uses_fwd3(D, fwd_variant(), drop_p > 0.f, rmask, has_seg != 0) ? 1 : 0;
+  (void)has_seg;
+  (void)seg_runs;
+  return fwd_uses_fwd3(D, drop_p > 0.f) ? 1 : 0;
+}
+
+// 1: the backward of this problem runs the generic kernels (GQA then needs the fp32 partials workspace)
+extern "C" int llmt_flash_attn_bwd_generic(int D, float drop_p) {
+  return (drop_p > 0.f || generic_only() || !(D == 64 || D == 96 || D == 128)) ? 1 : 0;
 }
 
 // floats of the `delta` workspace llmt_flash_attn_bwd needs
@@ -3960,152 +2313,46 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
   a.probe = attn_probe();
   const bool gqa = Hq != Hkv;
   const int64_t nrows = (int64_t)B * S * Hq;
-  dim3 grid((S + 127) / 128, Hq, B);
+  const dim3 grid((S + 127) / 128, Hq, B);
   const int dgrid = stream_grid(nrows, 256);
-  static const bool small_v3 = getenv("LLMT_FA_D96_GENERIC") == nullptr;  // A/B switch for D = 64 / 96
   // fused RoPE: with qun the dQ kernel rotates its rows on load and writes them to qrot for the dK/dV
-  // kernel; the dQ / dK epilogues (dq3, dkdv5 / dkdv6) apply the inverse rotation. Other kernels: qrot by
-  // the standalone rotation, inverse passes after.
+  // kernel; the dQ / dK epilogues apply the inverse rotation. Generic kernels: qrot by the standalone
+  // rotation, inverse passes after.
   if (rope) set_rope(a, rpos, rpos64, rp_sb, rp_ss, rcos, rsin, rP, qrot, D);
-  auto rope_to_dkdv = [&](bool fused_dk) {  // after the dQ kernel: the dK/dV kernel reads qrot
-    if (!rope) return;
-    if (qun) use_qrot(a);
-    a.rope_q = a.rope_dq = 0;
-    a.rope_dk = fused_dk;
-  };
-  auto rope_finish_dk = [&](bool fused_dk) {
-    if (rope && !fused_dk) rope_launch(a, a.dk, a.dk_sb, a.dk_ss, a.dk_sh, a.dk, a.dk_sb, a.dk_ss, a.dk_sh, Hkv, D, -1.f, stream);
-  };
-  if ((D == 128 || ((D == 96 || D == 64) && small_v3)) && !a.drop_thresh) {
+  if ((D == 128 || D == 96 || D == 64) && !a.drop_thresh && !generic_only()) {
     if (rope) {
       a.rope_q = qun;
       a.rope_dq = 1;
     }
-    // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws)
+    // delta buffer = [B, Hq, S] delta, then the packed per-tile row constants (llmt_flash_attn_bwd_ws),
+    // written by the dQ kernel (its waves cover every 32-row tile of every head; the dK/dV kernel runs after
+    // it on this stream)
     float* ld = delta + nrows;
-    const int64_t nT = (S + 31) / 32;
-    // the dQ kernel computes delta and writes the row constants itself (its waves cover every 32-row tile
-    // of every head, and the dK/dV kernel runs after it on this stream); LLMT_FA_PREP=1: the separate prep
-    // pass (A/B reference, read per launch)
-    const char* pe = getenv("LLMT_FA_PREP");
-    const bool fused_prep = !(pe && atoi(pe) == 1);
-    if (fused_prep) a.ldw = ld;
-    auto prep = [&](auto d_c) {
-      if (!fused_prep)
-        fa_bwd_prep128_kernel<decltype(d_c)::value><<<stream_grid((int64_t)B * Hq * nT * 32 * 16, 256), 256, 0, stream>>>(a, ld);
-    };
-    if (D == 96) {  // Phi-3: prep, v3 dQ, ring dK/dV (GQA inside the kernel: no partial buffers)
-      prep(std::integral_constant<int, 96>{});
-      if (a.rmask)
-        fa_bwd_dq3_kernel<96, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else
-        fa_bwd_dq3_kernel<96, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      const bool f5 = dkdv_variant() == 5;
-      rope_to_dkdv(f5);
-      if (dkdv_variant() == 5 && a.rmask && d5_ring(seg != nullptr, 96) == 8)
-        fa_bwd_dkdv5_kernel<96, false, 8><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      else if (dkdv_variant() == 5 && a.rmask)
-        fa_bwd_dkdv5_kernel<96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      else if (dkdv_variant() == 5)
-        fa_bwd_dkdv5_kernel<96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      else if (dkdv_variant() >= 3)
-        fa_bwd_dkdv128_kernel<3, 96, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      else
-        fa_bwd_dkdv128_kernel<1, 96><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      rope_finish_dk(f5);
-      return hipGetLastError();
+    a.ldw = ld;
+    const unsigned gq = (unsigned)((S + 127) / 128 * Hq * B), gk = (unsigned)((S + 127) / 128 * Hkv * B);
+    // dK/dV ring: 8 slots for D = 128 (tiles 6 ahead; B4 S8192 backward 7.605 -> 7.544 ms in one process;
+    // packed 32 docs/row 1.546 -> 1.511 ms), 6 for D = 96 / 64 (dense 3.635 vs 3.649 ms;
+    // profiles/r5_dkdv_ring_ab.jsonl)
+#define LLMT_BWD3(DD, RING)                                                       \
+  if (a.rmask)                                                                    \
+    fa_bwd_dq3_kernel<DD, true, true><<<gq, 256, 0, stream>>>(a);                 \
+  else                                                                            \
+    fa_bwd_dq3_kernel<DD, true, true, 4, true><<<gq, 256, 0, stream>>>(a);        \
+  if (rope) {                                                                     \
+    if (qun) use_qrot(a);                                                         \
+    a.rope_q = a.rope_dq = 0;                                                     \
+    a.rope_dk = 1;                                                                \
+  }                                                                               \
+  if (a.rmask)                                                                    \
+    fa_bwd_dkdv5_kernel<DD, false, RING><<<gk, 256, 0, stream>>>(a, ld);          \
+  else                                                                            \
+    fa_bwd_dkdv5_kernel<DD, true><<<gk, 256, 0, stream>>>(a, ld);
+    switch (D) {
+      case 64: { LLMT_BWD3(64, 6) } break;
+      case 96: { LLMT_BWD3(96, 6) } break;
+      default: { LLMT_BWD3(128, 8) } break;
     }
-    if (D == 64) {
-      prep(std::integral_constant<int, 64>{});
-      if (a.rmask)
-        fa_bwd_dq3_kernel<64, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else
-        fa_bwd_dq3_kernel<64, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      const bool f5 = dkdv_variant() == 5;
-      rope_to_dkdv(f5);
-      if (dkdv_variant() == 5 && a.rmask)
-        fa_bwd_dkdv5_kernel<64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      else if (dkdv_variant() == 5)
-        fa_bwd_dkdv5_kernel<64, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      else if (dkdv_variant() >= 3)
-        fa_bwd_dkdv128_kernel<3, 64, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      else
-        fa_bwd_dkdv128_kernel<1, 64><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-      rope_finish_dk(f5);
-      return hipGetLastError();
-    }
-    prep(std::integral_constant<int, 128>{});
-    // dQ: B4 S8192 Hq32 Hkv8 backward 9.16 ms with dq3 vs 9.66 ms with the earlier one-wave-per-SIMD ring
-    // kernel (removed, like the 8-wave role-split dK/dV kernel: 10.81 vs 9.89 ms, and the ring forward)
-    {
-      // LLMT_FA_DQ_VARIANT=0: V reads after the whole S^T chain (A/B reference, read per launch); the
-      // default interleaves them: B4 S8192 backward 8.00 -> 7.93 ms in one process, same gradients.
-      // 1 = the dwordx2 dQ store tail; the default (2) widens it (T21): B32 S1024 backward 1.541 ->
-      // 1.522 ms, B4 S8192 unchanged, same gradients
-      const char* dqe = getenv("LLMT_FA_DQ_VARIANT");
-      const int dqv = dqe ? atoi(dqe) : 2;
-      if ((Hq / Hkv) % 2 == 0 && (dqv == 3 || (dqv == 2 && pairs_pay(seg, S))))  // GQA head pairs
-        fa_bwd_dq3_kernel<128, true, true, 8><<<(S + 127) / 128 * (Hq / 2) * B, 512, 0, stream>>>(a);
-      else if (dqv == 0)
-        fa_bwd_dq3_kernel<128, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else if (dqv == 1)
-        fa_bwd_dq3_kernel<128><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else if (dqv == 4 && a.rmask)  // asm reading the MFMA results (A/B reference)
-        fa_bwd_dq3_kernel<128, true, true, 4, false, false><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else if (a.rmask)
-        fa_bwd_dq3_kernel<128, true, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-      else
-        fa_bwd_dq3_kernel<128, true, true, 4, true><<<(S + 127) / 128 * Hq * B, 256, 0, stream>>>(a);
-    }
-    const int variant = dkdv_variant();
-    // 7 = 64 keys per wave with asm-owned accumulators (fa_bwd_dkdv6_kernel), dense rows
-    const bool v6 = variant == 7 && a.rmask && !seg;
-    const bool f5 = variant == 5 || (variant == 6 && a.rmask) || v6;
-    rope_to_dkdv(f5);
-    // dense rows: an 8-slot Q / dO ring (tiles 6 ahead; B4 S8192 backward 7.605 -> 7.544 ms in one process,
-    // 7 slots 7.572); packed rows keep 6 (their key blocks often visit only a few tiles)
-    // LLMT_FA_D6_PROBE (diagnostic builds, wrong results): 1 = no ring DMA in the loop, 2 = no loop barrier,
-    // 4 = no softmax VALU, 8 = no operand LDS reads, 16 = all VALU beside the accumulator-destination MFMAs,
-    // 64 = no MFMAs (profiles/r5_dkdv6.md)
-    static const int d6p = getenv("LLMT_FA_D6_PROBE") ? atoi(getenv("LLMT_FA_D6_PROBE")) : 0;
-    const unsigned g6 = (S + 255) / 256 * Hkv * B;
-    if (v6 && d6p == 1)
-      fa_bwd_dkdv6_kernel<128, 3, 1><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 2)
-      fa_bwd_dkdv6_kernel<128, 3, 2><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 4)
-      fa_bwd_dkdv6_kernel<128, 3, 4><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 8)
-      fa_bwd_dkdv6_kernel<128, 3, 8><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 15)
-      fa_bwd_dkdv6_kernel<128, 3, 15><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 12)
-      fa_bwd_dkdv6_kernel<128, 3, 12><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 64)
-      fa_bwd_dkdv6_kernel<128, 3, 64><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 68)
-      fa_bwd_dkdv6_kernel<128, 3, 68><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6 && d6p == 16)
-      fa_bwd_dkdv6_kernel<128, 3, 16><<<g6, 256, 0, stream>>>(a, ld);
-    else if (v6)
-      fa_bwd_dkdv6_kernel<128><<<g6, 256, 0, stream>>>(a, ld);
-    else if (variant == 6 && a.rmask && !seg)
-      fa_bwd_dkdv5_kernel<128, false, 8, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 6 && a.rmask)
-      fa_bwd_dkdv5_kernel<128, false, 6, 1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 5 && a.rmask && d5_ring(seg != nullptr) == 8)
-      fa_bwd_dkdv5_kernel<128, false, 8><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 5 && a.rmask)
-      fa_bwd_dkdv5_kernel<128><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 5)
-      fa_bwd_dkdv5_kernel<128, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 3)
-      fa_bwd_dkdv128_kernel<3><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else if (variant == 4)
-      fa_bwd_dkdv128_kernel<3, 128, true><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    else
-      fa_bwd_dkdv128_kernel<1><<<(S + 127) / 128 * Hkv * B, 256, 0, stream>>>(a, ld);
-    rope_finish_dk(f5);
+#undef LLMT_BWD3
     return hipGetLastError();
   }
   if (gqa && !work) return hipErrorInvalidValue;
@@ -4131,7 +2378,7 @@ extern "C" hipError_t llmt_flash_attn_bwd(const void* q, const void* k, const vo
 #undef LLMT_BWD
   if (rope) {
     rope_launch(a, a.out, a.dq_sb, a.dq_ss, a.dq_sh, a.out, a.dq_sb, a.dq_ss, a.dq_sh, Hq, D, -1.f, stream);
-    rope_finish_dk(false);
+    rope_launch(a, a.dk, a.dk_sb, a.dk_ss, a.dk_sh, a.dk, a.dk_sb, a.dk_ss, a.dk_sh, Hkv, D, -1.f, stream);
   }
   return hipGetLastError();
 }

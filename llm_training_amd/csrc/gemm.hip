@@ -186,6 +186,18 @@ struct GemmArgs {
   int64_t ldx, ldy, ldc;
 };
 
+// SwiGLU-backward epilogue (OUT = 4, gemm_pp_kernel): C = dc = dy . W_down is not stored; with g = gu[m, n],
+// u = gu[m, I + n] (I = N) the epilogue writes dgu[m, n] = dc u silu'(g), dgu[m, I + n] = dc silu(g) and, when
+// dgu_t is set, the same values transposed into dgu_t [2I, M] (the token-contiguous operand of the gate_up
+// weight-gradient GEMM). Replaces the standalone swiglu_bwd_tr pass (csrc/elementwise.hip), which read dc back.
+struct SwiArgs {
+  const bf16* gu;  // [M, 2N]
+  bf16* dgu;       // [M, 2N]
+  bf16* dgu_t;     // [2N, M] or null
+};
+
+__device__ __forceinline__ float g_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+
 __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   const int nbm = (M + kBM - 1) / kBM, nbn = (N + kBN - 1) / kBN, nwg = nbm * nbn;
   const int bid = blockIdx.x;
@@ -365,6 +377,132 @@ hipError_t launch(const GemmArgs& a, int out_mode, hipStream_t stream) {
   return gemm_waves() == 8 ? launch_nw<XMN, YMN, 8>(a, out_mode, stream) : launch_nw<XMN, YMN, 4>(a, out_mode, stream);
 }
 
+// ---------------------------------------------------------------- SwiGLU-backward epilogue
+// Runs after the main loop of a 256 x 256 tile, in four passes of 64 output columns (the columns of waves
+// wq = q of both row groups). Per pass, through the (now free) LDS ring:
+//   1. the owning waves write their dc accumulators as bf16 into D [256 rows][64 cols];
+//   2. all 512 threads take 2 rows x 8 columns per step (two steps): D from LDS, g / u from global (16-byte
+//      loads issued before step 1, so their latency overlaps the LDS staging), dg / du in fp32 with the
+//      swiglu_bwd_kernel math, 16-byte row-major stores of dgu, and the bf16 results as 32-bit row-pair
+//      words into the transposed images G^T / U^T [64 cols][128 row pairs];
+//   3. 16-byte stores of 8 tokens of one dgu_t row from G^T / U^T (32 threads cover a 512-byte row run).
+// The staged dc is rounded to bf16 first: the same numerics as the unfused GEMM (bf16 dc) + swiglu_bwd_tr.
+constexpr int kSwDP = 144;             // D row pitch (bytes): 128 + 16
+constexpr int kSwTW = 132;             // G^T / U^T row pitch (32-bit words): 128 + 4
+constexpr int kSwD = 256 * kSwDP;      // 36 KB
+constexpr int kSwT = 64 * kSwTW * 4;   // 33 KB each
+
+__device__ __forceinline__ void swiglu_bwd_epilogue(const GemmArgs& g, const SwiArgs& sw, gf4 (&acc)[8][4],
+                                                    char* smem, int row0, int col0, int grp, int wq, int fr, int fc,
+                                                    int tid) {
+  const int M = g.M, N = g.N;
+  const int64_t ld2 = 2 * (int64_t)N;
+  char* dimg = smem;
+  uint32_t* gt = reinterpret_cast<uint32_t*>(smem + kSwD);
+  uint32_t* ut = reinterpret_cast<uint32_t*>(smem + kSwD + kSwT);
+  const int cch = tid & 7, rp = tid >> 3;  // 8-column chunk, row pair (per step)
+  // every wave's DMAs have landed and every fragment read retired before the ring is reused
+  g_barrier();
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) {
+    const int c0 = col0 + q * 64;
+    if (c0 >= N) break;  // workgroup-uniform
+    // (2) operands of this thread's two steps, loaded first (rows 2 rp, 2 rp + 1 and + 128)
+    bf16x8 gv[2][2], uv[2][2];
+    const int n = c0 + cch * 8;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = row0 + st * 128 + 2 * rp + h;
+        if (m < M && n < N) {
+          const bf16* pr = sw.gu + (int64_t)m * ld2 + n;
+          gv[st][h] = *reinterpret_cast<const bf16x8*>(pr);
+          uv[st][h] = *reinterpret_cast<const bf16x8*>(pr + N);
+        } else {
+          gv[st][h] = bf16x8{{0u, 0u, 0u, 0u}};
+          uv[st][h] = gv[st][h];
+        }
+      }
+    // (1) the owning waves stage dc (bf16) in D
+    if (wq == q) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int r = grp * 128 + i * 16 + fr, c = jj * 16 + fc * 4;
+          uint2 w;
+          w.x = pack_bf16x2(acc[i][jj][0], acc[i][jj][1]);
+          w.y = pack_bf16x2(acc[i][jj][2], acc[i][jj][3]);
+          *reinterpret_cast<uint2*>(dimg + r * kSwDP + c * 2) = w;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      uint32_t wg[8], wu[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = st * 128 + 2 * rp + h, m = row0 + r;
+        float dcv[8], a[8], b[8], da[8], db[8];
+        unpack8(*reinterpret_cast<const bf16x8*>(dimg + r * kSwDP + cch * 16), dcv);
+        unpack8(gv[st][h], a);
+        unpack8(uv[st][h], b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // the swiglu_bwd_kernel math, element for element
+          const float sg = g_sigmoid(a[i]);
+          const float silu = a[i] * sg;
+          da[i] = dcv[i] * b[i] * sg * (1.f + a[i] * (1.f - sg));
+          db[i] = dcv[i] * silu;
+        }
+        const bf16x8 pa = pack8(da), pb = pack8(db);
+        if (m < M && n < N) {
+          bf16* drow = sw.dgu + (int64_t)m * ld2 + n;
+          *reinterpret_cast<bf16x8*>(drow) = pa;
+          *reinterpret_cast<bf16x8*>(drow + N) = pb;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t lo_g = pa.w[i] & 0xffffu, hi_g = pa.w[i] >> 16;
+          const uint32_t lo_u = pb.w[i] & 0xffffu, hi_u = pb.w[i] >> 16;
+          if (h == 0) {
+            wg[2 * i] = lo_g; wg[2 * i + 1] = hi_g;
+            wu[2 * i] = lo_u; wu[2 * i + 1] = hi_u;
+          } else {
+            wg[2 * i] |= lo_g << 16; wg[2 * i + 1] |= hi_g << 16;
+            wu[2 * i] |= lo_u << 16; wu[2 * i + 1] |= hi_u << 16;
+          }
+        }
+      }
+      if (sw.dgu_t) {
+        const int pw = st * 64 + rp;  // row-pair word index
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          gt[(cch * 8 + i) * kSwTW + pw] = wg[i];
+          ut[(cch * 8 + i) * kSwTW + pw] = wu[i];
+        }
+      }
+    }
+    __syncthreads();
+    if (sw.dgu_t) {
+      // (3) 64 columns x 32 chunks of 8 tokens per image: 4 chunks of each image per thread
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int idx = tid + 512 * k;
+        const int c = idx >> 5, ch = idx & 31;
+        const int nn = c0 + c, m = row0 + ch * 8;
+        if (nn < N && m < M) {
+          const uint4 vg = *reinterpret_cast<const uint4*>(gt + c * kSwTW + 4 * ch);
+          const uint4 vu = *reinterpret_cast<const uint4*>(ut + c * kSwTW + 4 * ch);
+          *reinterpret_cast<uint4*>(sw.dgu_t + (int64_t)nn * M + m) = vg;
+          *reinterpret_cast<uint4*>(sw.dgu_t + (int64_t)(N + nn) * M + m) = vu;
+        }
+      }
+      __syncthreads();  // the images are rewritten by the next pass
+    }
+  }
+}
+
 // ---------------------------------------------------------------- ping-pong kernel
 // The same tile (256 x 256, 8 waves as 2 (M) x 4 (N), wave tile 128 x 64, 32-deep stages in a ring of NS
 // 32-KB LDS slots filled by LDS-DMA) with the waves split into two groups that alternate roles between
@@ -381,7 +519,7 @@ hipError_t launch(const GemmArgs& a, int out_mode, hipStream_t stream) {
 // past the last stage read an empty descriptor range (zeros into slots no one reads) so the wait counts
 // stay constant. Split-K: blockIdx.y selects a contiguous slice of the stages, written as an fp32 slab.
 template <bool XMN, bool YMN, int OUT, int NS>
-__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g, int nk, int64_t slab) {
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g, int nk, int64_t slab, SwiArgs sw) {
   constexpr int AH = NS - 1;  // stages in flight ahead of the one being read
   __shared__ __attribute__((aligned(16))) char smem[NS * kSlot];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -458,6 +596,10 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g, int nk, int64_
   g_wait_vm<0>();             // no LDS-DMA outlives the workgroup
 
   const int fr = lane & 15, fc = lane >> 4;
+  if constexpr (OUT == 4) {
+    swiglu_bwd_epilogue(g, sw, acc, smem, row0, col0, grp, wq, fr, fc, tid);
+    return;
+  }
   char* cbase = reinterpret_cast<char*>(g.c) + (int64_t)blockIdx.y * slab * (OUT == 0 || OUT == 3 ? 2 : 4);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -499,15 +641,22 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g, int nk, int64_
 }
 
 template <bool XMN, bool YMN>
-hipError_t launch_pp(const GemmArgs& a, int out_mode, int ksplit, int64_t slab, hipStream_t stream) {
+hipError_t launch_pp(const GemmArgs& a, int out_mode, int ksplit, int64_t slab, hipStream_t stream,
+                     const SwiArgs& sw = SwiArgs{nullptr, nullptr, nullptr}) {
   const int64_t nwg = (int64_t)((a.M + kBM - 1) / kBM) * ((a.N + kBN - 1) / kBN);
   const int nk = a.K / kBK / ksplit;
   const dim3 grid((unsigned)nwg, (unsigned)ksplit), block(512);
   switch (out_mode) {
-    case 0: gemm_pp_kernel<XMN, YMN, 0, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
-    case 1: gemm_pp_kernel<XMN, YMN, 1, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
-    case 2: gemm_pp_kernel<XMN, YMN, 2, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
-    default: gemm_pp_kernel<XMN, YMN, 3, 5><<<grid, block, 0, stream>>>(a, nk, slab); break;
+    case 0: gemm_pp_kernel<XMN, YMN, 0, 5><<<grid, block, 0, stream>>>(a, nk, slab, sw); break;
+    case 1: gemm_pp_kernel<XMN, YMN, 1, 5><<<grid, block, 0, stream>>>(a, nk, slab, sw); break;
+    case 2: gemm_pp_kernel<XMN, YMN, 2, 5><<<grid, block, 0, stream>>>(a, nk, slab, sw); break;
+    case 3: gemm_pp_kernel<XMN, YMN, 3, 5><<<grid, block, 0, stream>>>(a, nk, slab, sw); break;
+    default:
+      if constexpr (!XMN && YMN) {  // the down-projection input gradient: dy [M, K] . W_down [K, N]
+        gemm_pp_kernel<false, true, 4, 5><<<grid, block, 0, stream>>>(a, nk, slab, sw);
+        break;
+      }
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
@@ -560,4 +709,19 @@ extern "C" hipError_t llmt_gemm_splitk(const void* x, const void* y, float* slab
   if (!x_mn && y_mn) return launch_pp<false, true>(a, 1, nsplit, slab, stream);
   if (x_mn && y_mn) return launch_pp<true, true>(a, 1, nsplit, slab, stream);
   return hipErrorInvalidValue;
+}
+
+// Down-projection input gradient with the SwiGLU backward in the epilogue (see SwiArgs): dy [M, K] (row stride
+// ldx), w_down [K, N] (row stride ldy), gu / dgu [M, 2N] contiguous, dgu_t [2N, M] or null. Preconditions
+// (checked by the binding): K % 32 == 0, N % 64 == 0, M % 64 == 0, 16-byte aligned operands.
+extern "C" hipError_t llmt_gemm_swiglu_bwd(const void* dy, const void* w, const void* gu, void* dgu, void* dgu_t, int M,
+                                           int N, int K, int64_t ldx, int64_t ldy, hipStream_t stream) {
+  using namespace llmt;
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (K <= 0 || K % kBK != 0 || N % 64 != 0 || M % 64 != 0) return hipErrorInvalidValue;
+  if (ldx % 8 || ldy % 8) return hipErrorInvalidValue;
+  if (256 * ldx * 2 >= 0x7fffffffLL || 256 * ldy * 2 >= 0x7fffffffLL) return hipErrorInvalidValue;
+  GemmArgs a{reinterpret_cast<const bf16*>(dy), reinterpret_cast<const bf16*>(w), nullptr, M, N, K, ldx, ldy, 0};
+  SwiArgs sw{reinterpret_cast<const bf16*>(gu), reinterpret_cast<bf16*>(dgu), reinterpret_cast<bf16*>(dgu_t)};
+  return launch_pp<false, true>(a, 4, 1, 0, stream, sw);
 }

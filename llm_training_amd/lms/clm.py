@@ -40,7 +40,8 @@ class CLM(BaseLM):
                 n = x.shape[0]
                 if mt.shape[0] < n * pc.tp_size:  # sequence right-padded to a TP multiple: no noise on pads
                     mt = torch.nn.functional.pad(mt, (0, 0, 0, n * pc.tp_size - mt.shape[0]))
-                mt = mt[pc.tp_rank * n:(pc.tp_rank + 1) * n]
+                from ..parallel.tensor_parallel import shard_seq_local
+                mt = shard_seq_local(mt, pc.tp_rank, pc.tp_size)  # this rank's rows (chunked sequence layout)
             noise = torch.empty_like(x).uniform_(-1, 1) * mt.unsqueeze(-1) * mag.view(1, -1, 1)
             return x + noise.detach()
 

@@ -454,9 +454,10 @@ def _patch_mlp(m: nn.Module) -> bool:
         # (Liger's LigerSwiGLUMLP); gate / up weights live in one fused parameter (no per-call concat)
         if _fuse_gate_up(m):
             def forward(_m, x):
-                from ..ops.fused import linear, swiglu
-                c = swiglu(linear(x, _m.gate_up_weight), dy_t_consumer=True)
-                return linear(c, _m.down_proj.weight, _m.down_proj.bias)
+                from ..ops.fused import linear, swiglu_down
+                # down_proj's input-gradient GEMM carries the SwiGLU backward in its epilogue
+                return swiglu_down(linear(x, _m.gate_up_weight), _m.down_proj.weight, _m.down_proj.bias,
+                                   dy_t_consumer=True)
         else:  # biased projections: concatenated per call
             def forward(_m, x):
                 from ..ops.fused import swiglu
@@ -467,9 +468,9 @@ def _patch_mlp(m: nn.Module) -> bool:
                 return _m.down_proj(swiglu(torch.nn.functional.linear(x, w, b)))
     elif hasattr(m, "gate_up_proj") and hasattr(m, "down_proj"):  # Phi-3: fused [gate | up] projection
         def forward(_m, x):
-            from ..ops.fused import linear, swiglu
+            from ..ops.fused import linear, swiglu_down
             gu = linear(x, _m.gate_up_proj.weight, _m.gate_up_proj.bias)
-            return linear(swiglu(gu, dy_t_consumer=True), _m.down_proj.weight, _m.down_proj.bias)
+            return swiglu_down(gu, _m.down_proj.weight, _m.down_proj.bias, dy_t_consumer=True)
     else:
         return False
     _bind(m, forward)

@@ -144,7 +144,11 @@ class LlamaMLP(nn.Module):
             gu = tpl.ag_linear(h, self.gate_up_proj.weight, self.gate_up_proj.bias, sp_group)
             return tpl.linear_rs(F_.swiglu(gu), self.down_proj.weight, self.down_proj.bias, sp_group)
         gu = self.gate_up_proj(h)
-        return self.down_proj(F_.swiglu(gu, dy_t_consumer=isinstance(self.gate_up_proj, Linear)))
+        consumer = isinstance(self.gate_up_proj, Linear)
+        if isinstance(self.down_proj, Linear):
+            # the down projection's input-gradient GEMM carries the SwiGLU backward in its epilogue
+            return F_.swiglu_down(gu, self.down_proj.weight, self.down_proj.bias, dy_t_consumer=consumer)
+        return self.down_proj(F_.swiglu(gu, dy_t_consumer=consumer))
 
 
 class LlamaDecoderLayer(nn.Module):

@@ -113,13 +113,28 @@ def layout_key_str(key: tuple) -> str:
     return "|".join(str(x).replace("torch.", "") for x in key)
 
 
+def _device_arch() -> str | None:
+    try:
+        return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+    except Exception:  # no GPU / no HIP device properties
+        return None
+
+
 def _layout_table() -> dict:
+    """The shipped layout table, only on the architecture it was measured on (its ``arch`` field, default
+    gfx950): on another GPU the timed first-sight choice is used instead of choices tuned elsewhere."""
     if _LAYOUT_TABLE[0] is None:
         tbl = {}
         if _LAYOUT_MODE == "table" and os.path.exists(_LAYOUT_TABLE_PATH):
             import json
             with open(_LAYOUT_TABLE_PATH) as f:
-                tbl = json.load(f).get("layouts", {})
+                doc = json.load(f)
+            arch = _device_arch()
+            if arch is None or arch == doc.get("arch", "gfx950"):
+                tbl = doc.get("layouts", {})
+            else:
+                log.info("GEMM layout table measured on %s, device is %s: timing layouts instead",
+                         doc.get("arch", "gfx950"), arch)
         _LAYOUT_TABLE[0] = tbl
     return _LAYOUT_TABLE[0]
 
@@ -183,8 +198,9 @@ def dump_layouts(path: str) -> None:
     """Write the choices of this process as a table in the shipped format (tuning/gemm_layouts_gfx950.json)."""
     import json
     with open(path, "w") as f:
-        json.dump({"layouts": {layout_key_str(k): v for k, v in sorted(_LAYOUT_CACHE.items(), key=lambda kv:
-                                                                      layout_key_str(kv[0]))}}, f, indent=1)
+        json.dump({"arch": _device_arch() or "gfx950",
+                   "layouts": {layout_key_str(k): v for k, v in sorted(_LAYOUT_CACHE.items(), key=lambda kv:
+                                                                       layout_key_str(kv[0]))}}, f, indent=1)
 
 
 # largest weight-gradient output (elements) offered the split-K candidates (fp32 slabs: 8 bytes / element)
@@ -643,6 +659,65 @@ class _SwiGLUFn(Function):
             _DY_T[dgu.data_ptr()] = dgu_t
             return dgu, None
         return lib().swiglu_bwd(gu, dc), None
+
+
+# The down projection's input gradient with the SwiGLU backward in its epilogue (csrc/gemm.hip SwiArgs, the
+# hand-written ping-pong GEMM): dc = dy @ W_down is never written; the epilogue reads gate / up of its tile and
+# writes dgu (and dgu^T for the TN gate_up weight gradient). LLMT_SWIGLU_GEMM=0 runs hipBLASLt + the separate
+# swiglu_bwd_tr pass instead (A/B reference).
+SWIGLU_GEMM = [os.environ.get("LLMT_SWIGLU_GEMM", "1").strip().lower() not in ("0", "false", "off")]
+
+
+class _SwiGLUDownFn(Function):
+    """y = swiglu(gu) @ W_down^T (+ b): the SwiGLU forward and the down projection, with the backward's input
+    gradient GEMM and SwiGLU backward fused (one kernel)."""
+
+    @staticmethod
+    def forward(ctx, gu, w, b, dy_t_consumer):
+        gu = gu.contiguous()
+        c = lib().swiglu_fwd(gu)
+        ctx.save_for_backward(gu, c)
+        ctx.w, ctx.has_bias, ctx.dy_t_consumer = w, b is not None, dy_t_consumer
+        return mm_nt(c.reshape(-1, c.shape[-1]), w, bias=b).view(*c.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        gu, c = ctx.saved_tensors
+        w = ctx.w
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.stride(-1) != 1 or (dy2.size(0) > 1 and dy2.stride(0) % 8):
+            dy2 = dy2.contiguous()
+        I2 = gu.shape[-1]
+        T = gu.numel() // I2
+        _DY_T.clear()
+        dgu = dw = db = None
+        if ctx.needs_input_grad[0]:
+            on = FUSED_DY_T[0] if FUSED_DY_T[0] is not None else I2 // 2 >= DY_T_MIN_I
+            tr = (on and ctx.dy_t_consumer and TRANSPOSE_LAYOUTS[0] and T >= _TR_WGRAD_MIN_M
+                  and GEMM_MODES.get("wgrad") == "lt")
+            outs = lib().gemm_swiglu_bwd(dy2, w, gu.view(T, I2), tr)
+            dgu = outs[0].view(gu.shape)
+            if tr:
+                _DY_T[dgu.data_ptr()] = outs[1]
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad_mm(w, dy2.t(), c.reshape(-1, c.shape[-1]))
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dgu, dw, db, None
+
+
+def swiglu_down(gate_up: torch.Tensor, w_down: torch.Tensor, b_down: torch.Tensor | None = None,
+                dy_t_consumer: bool = False) -> torch.Tensor:
+    """down_proj(silu(gate) * up) for a fused [..., 2I] gate_up buffer: on bf16 GPU tensors of fitting shapes
+    (tokens and I multiples of 64, H of 32) one autograd node whose backward runs the fused GEMM + SwiGLU
+    backward kernel; otherwise ``linear(swiglu(gate_up), w_down, b_down)``."""
+    I2 = gate_up.shape[-1]
+    T = gate_up.numel() // max(1, I2)
+    if (SWIGLU_GEMM[0] and use_native(gate_up) and GEMM_MODES.get("dgrad") != "blas" and T % 64 == 0 and T > 0
+            and (I2 // 2) % 64 == 0 and w_down.shape[1] == I2 // 2 and w_down.shape[0] % 32 == 0
+            and _gemm_operand_ok(w_down)):
+        return _SwiGLUDownFn.apply(gate_up, w_down, b_down, bool(dy_t_consumer))
+    return linear(swiglu(gate_up, dy_t_consumer), w_down, b_down)
 
 
 def swiglu(gate_up: torch.Tensor, dy_t_consumer: bool = False) -> torch.Tensor:

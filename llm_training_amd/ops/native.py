@@ -16,7 +16,31 @@ import torch
 _LOCK = threading.Lock()
 _LOADED: bool | None = None
 _ERR: Exception | None = None
-LIB_PATH = Path(__file__).resolve().parent.parent / "_C.so"
+# LLMT_NATIVE_DIAG=1 loads the diagnostic build (_C_diag.so: the wrong-result probes of benchmarks/probes/
+# compiled in, `python -m llm_training_amd._build --diag`) instead of the production library
+DIAG = os.environ.get("LLMT_NATIVE_DIAG", "0") == "1"
+LIB_PATH = Path(__file__).resolve().parent.parent / ("_C_diag.so" if DIAG else "_C.so")
+# environment variables that make kernels compute wrong results on purpose (diagnostic probes); only the
+# diagnostic library reads them, and a production run refuses to start while one is set
+PROBE_VARS = ("LLMT_FA_PROBE", "LLMT_FA_D6_PROBE")
+
+
+def check_probe_env(environ=None) -> None:
+    """Raise if a diagnostic probe variable is set for a production (non-diagnostic) run."""
+    env = os.environ if environ is None else environ
+    bad = [k for k in PROBE_VARS if env.get(k, "") not in ("", "0")]
+    if bad and not DIAG:
+        raise RuntimeError(
+            f"{', '.join(bad)} select wrong-result diagnostic probes; they are only honoured by the diagnostic "
+            "library (LLMT_NATIVE_DIAG=1, built by `python -m llm_training_amd._build --diag`). Unset them for "
+            "training runs.")
+
+
+def llmt_env(environ=None) -> dict:
+    """Every LLMT_* variable of the environment (kernel / layout / schedule knobs): recorded with each run
+    (bench JSON ``llmt_env``, trainer run metadata) so a result can be traced to the knobs it ran with."""
+    env = os.environ if environ is None else environ
+    return {k: env[k] for k in sorted(env) if k.startswith("LLMT_")}
 
 
 def _load() -> bool:
@@ -25,12 +49,18 @@ def _load() -> bool:
         if _LOADED is not None:
             return _LOADED
         try:
+            check_probe_env()
             if not LIB_PATH.exists() and os.environ.get("LLMT_AUTOBUILD", "1") == "1":
                 from .. import _build
 
-                _build.build()
+                _build.build(diag=DIAG)
             torch.ops.load_library(str(LIB_PATH))
             _LOADED = True
+        except RuntimeError as e:
+            if "diagnostic probes" in str(e):
+                raise
+            _ERR = e
+            _LOADED = False
         except Exception as e:  # pragma: no cover - exercised on broken installs only
             _ERR = e
             _LOADED = False

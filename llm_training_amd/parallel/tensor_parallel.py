@@ -15,24 +15,32 @@ residual stream sharded on the sequence dim. The reference expresses it with DTe
 With SP the collectives next to the projection GEMMs are pipelined with the GEMMs (``ag_linear`` /
 ``linear_rs``, used by the decoder layers) as a staged collective matmul sized for MI355X's xGMI: every
 GPU of a node has a direct link to each of the other seven, so one RCCL all-gather / reduce-scatter keeps
-all seven links busy, while a peer-by-peer ring of P2P transfers would move each step over a single link
-(and P2P operations on one communicator run one after another on its stream). Each rank's sequence shard
-is therefore cut into ``m`` sub-chunks (``LLMT_TP_STAGES``, default 4) and each collective into ``m``
-full-mesh collectives of one sub-chunk each, issued together on the communicator's stream; the compute
-stream waits only for the stage it is about to use:
+all seven links busy, while a peer-by-peer ring of P2P transfers would move each step over a single link.
+Each collective is therefore cut into ``m`` full-mesh collectives (``LLMT_TP_STAGES``, default 4),
+issued together on the communicator's stream; the compute stream waits only for the chunks it is about
+to use.
 
-- ``ag_linear``  (q/k/v, gate/up), forward: all-gather stage j+1 is in flight while the GEMMs of stage j's
-  rows (one per source rank, written straight into their rows of the output) run; backward: the input
-  gradient of stage j (one GEMM per destination rank) is reduce-scattered while stage j+1's is computed,
-  and the weight gradient accumulates per (stage, rank) block beside them.
-- ``linear_rs``  (o, down), forward: the output rows of stage j are reduce-scattered while stage j+1's are
-  computed; backward: the staged all-gather of the output gradient feeds the input-gradient GEMMs stage by
-  stage, as in ``ag_linear``'s forward.
+**Chunked sequence layout.** The sequence shard of rank d is not one contiguous run of S/n positions
+but m chunks: with S = m * n * cm, rank d holds positions j * n * cm + d * cm + [0, cm) for j = 0..m-1.
+Then the all-gather of chunk j from every rank is global rows [j n cm, (j+1) n cm) in sequence order,
+and a reduce-scatter of such a block lands chunk j on every rank: the gathered tensor IS the sequence,
+every stage reads or writes one contiguous row block, and a projection needs no per-rank GEMMs and no
+reordering copy. The layout is a permutation of the tokens over the ranks; RMSNorm, the residual stream
+and the embedding are per-token and do not care, and attention / the loss only ever see gathered
+(sequence-ordered) tensors. Every collective of this module uses it (``seq_chunks`` of the sequence).
 
-Gathered tensors are kept stage-major ([m, n, S/(n m), ...]): each stage's all-gather writes one
-contiguous block, and every GEMM reads or writes a contiguous row block of it, so no reordering copy is
-made. The compute stream's waits are metered when ``TP_WAIT_METER`` holds a list (bench.py reports the
-exposed tensor-parallel communication per step from it).
+- ``ag_linear``  (q/k/v, gate/up), forward: the chunk all-gathers run while earlier chunks' rows are
+  multiplied; backward: the input gradient of a group of chunks is reduce-scattered while the next group's
+  is computed. The weight gradient is ONE GEMM over the gathered input and the full output gradient.
+- ``linear_rs``  (o, down), forward: the output rows of a group are reduce-scattered while the next
+  group's are computed; backward: the chunked all-gather of the output gradient feeds the input-gradient
+  GEMMs group by group, and again one weight-gradient GEMM.
+
+GEMM granularity: consecutive chunks are grouped so that each GEMM fills the chip with at least
+``LLMT_TP_GEMM_TILES`` (default 512 = two waves of 256 CUs) output tiles of 256 x 256; a projection whose
+chunk already does runs one GEMM per chunk (benchmarks/bench_tp_gemms.py). The compute stream's waits are
+metered when ``TP_WAIT_METER`` holds a list (bench.py reports the exposed tensor-parallel communication
+per step from it); ``STAGE_PLANS`` records the group sizes each projection ran with.
 """
 from __future__ import annotations
 
@@ -47,25 +55,60 @@ def _ws(group) -> int:
     return dist.get_world_size(group) if group is not None else 1
 
 
+def tp_stages(rows: int) -> int:
+    """Chunks of a sequence shard of ``rows`` rows: LLMT_TP_STAGES (default 4), reduced to divide it."""
+    m = max(1, int(os.environ.get("LLMT_TP_STAGES", "4")))
+    while rows % m:
+        m -= 1
+    return m
+
+
 def all_gather_seq(x: torch.Tensor, group) -> torch.Tensor:
+    """Sequence shard [c, ...] (chunked layout, module doc) -> the sequence [n c, ...] in order."""
     n = _ws(group)
     if n == 1:
         return x
     x = x.contiguous()
-    out = torch.empty((x.shape[0] * n, *x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x, group=group)
-    return out
+    c = x.shape[0]
+    m = tp_stages(c)
+    cm = c // m
+    out = torch.empty((m, n * cm, *x.shape[1:]), dtype=x.dtype, device=x.device)
+    for j in range(m):
+        dist.all_gather_into_tensor(out[j], x[j * cm:(j + 1) * cm], group=group)
+    return out.view(m * n * cm, *x.shape[1:])
 
 
 def reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
+    """The sequence [S, ...] (partial sums) -> this rank's shard [S / n, ...] in the chunked layout."""
     n = _ws(group)
     if n == 1:
         return x
     x = x.contiguous()
     assert x.shape[0] % n == 0, "sequence length must be divisible by the tensor-parallel size"
-    out = torch.empty((x.shape[0] // n, *x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.reduce_scatter_tensor(out, x, group=group)
+    c = x.shape[0] // n
+    m = tp_stages(c)
+    cm = c // m
+    out = torch.empty((c, *x.shape[1:]), dtype=x.dtype, device=x.device)
+    for j in range(m):
+        dist.reduce_scatter_tensor(out[j * cm:(j + 1) * cm], x[j * n * cm:(j + 1) * n * cm], group=group)
     return out
+
+
+def shard_seq_local(x: torch.Tensor, rank: int, n: int) -> torch.Tensor:
+    """This rank's chunked-layout shard of a full sequence (no communication)."""
+    c = x.shape[0] // n
+    m = tp_stages(c)
+    cm = c // m
+    return x.view(m, n, cm, *x.shape[1:])[:, rank].reshape(c, *x.shape[1:])
+
+
+def unshard_seq_local(shards: list[torch.Tensor]) -> torch.Tensor:
+    """Inverse of :func:`shard_seq_local` given every rank's shard (in rank order)."""
+    n, c = len(shards), shards[0].shape[0]
+    m = tp_stages(c)
+    cm = c // m
+    parts = [s.view(m, cm, *s.shape[1:]) for s in shards]
+    return torch.stack(parts, 1).reshape(n * c, *shards[0].shape[1:])
 
 
 class _GatherSeq(Function):
@@ -91,15 +134,12 @@ class _ScatterSeq(Function):
 
 
 class _SplitSeq(Function):
-    """Take this rank's sequence shard (no communication); bwd all-gathers."""
+    """Take this rank's sequence shard (chunked layout; no communication); bwd all-gathers."""
 
     @staticmethod
     def forward(ctx, x, group):
         ctx.group = group
-        n = _ws(group)
-        r = dist.get_rank(group)
-        c = x.shape[0] // n
-        return x[r * c:(r + 1) * c].contiguous()
+        return shard_seq_local(x, dist.get_rank(group), _ws(group)).contiguous()
 
     @staticmethod
     def backward(ctx, g):
@@ -157,6 +197,8 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
 
 # compute-stream stalls on tensor-parallel collectives: a list of (start, end) CUDA events, or None
 TP_WAIT_METER: list | None = None
+# chunk-group sizes each staged projection ran with: "ag:<N>" / "rs:<N>" -> [chunks per GEMM, ...]
+STAGE_PLANS: dict[str, list[int]] = {}
 
 
 def _tp_wait(work) -> None:
@@ -171,12 +213,21 @@ def _tp_wait(work) -> None:
         work.wait()
 
 
-def tp_stages(rows: int) -> int:
-    """Pipeline stages for a sequence shard of ``rows`` rows: LLMT_TP_STAGES (default 4), reduced to divide it."""
-    m = max(1, int(os.environ.get("LLMT_TP_STAGES", "4")))
-    while rows % m:
-        m -= 1
-    return m
+def gemm_groups(m: int, chunk_rows: int, ncols: int) -> list[tuple[int, int]]:
+    """Consecutive chunk ranges [j0, j1) of the m chunks, one GEMM each: the smallest group size dividing m
+    whose GEMM ([g * chunk_rows, ncols] output) has at least LLMT_TP_GEMM_TILES 256 x 256 tiles."""
+    want = max(1, int(os.environ.get("LLMT_TP_GEMM_TILES", "512")))
+    tiles = -(-chunk_rows // 256) * -(-ncols // 256)
+    g = m
+    for d in range(1, m + 1):
+        if m % d == 0 and d * tiles >= want:
+            g = d
+            break
+    return [(j, j + g) for j in range(0, m, g)]
+
+
+def _plan(key: str, groups) -> None:
+    STAGE_PLANS[key] = [j1 - j0 for j0, j1 in groups]
 
 
 class _AGLinear(Function):
@@ -191,48 +242,53 @@ class _AGLinear(Function):
         m = tp_stages(c)
         cm = c // m
         tail = x.shape[1:]
-        full = torch.empty((m, n, cm, *tail), dtype=x.dtype, device=x.device)  # stage-major gathered input
-        works = [dist.all_gather_into_tensor(full[j].view(n * cm, *tail), x[j * cm:(j + 1) * cm], group=group,
+        per = n * cm  # sequence positions per chunk of the gathered input
+        full = torch.empty((m * per, *tail), dtype=x.dtype, device=x.device)  # the gathered input, in order
+        works = [dist.all_gather_into_tensor(full[j * per:(j + 1) * per], x[j * cm:(j + 1) * cm], group=group,
                                              async_op=True) for j in range(m)]
-        y = torch.empty((c * n, *tail[:-1], w.shape[0]), dtype=x.dtype, device=x.device)
-        y5 = y.view(n, m, cm, *tail[:-1], w.shape[0])
-        for j in range(m):
-            _tp_wait(works[j])
-            for d in range(n):  # rows of source rank d, stage j -> their place in the output
-                mm_nt(_rows(full[j, d]), w, out=_rows(y5[d, j]), bias=b)
+        y = torch.empty((m * per, *tail[:-1], w.shape[0]), dtype=x.dtype, device=x.device)
+        rows = per * (x[0, ..., 0].numel())
+        groups = gemm_groups(m, rows, w.shape[0])
+        _plan(f"ag:{w.shape[0]}", groups)
+        for j0, j1 in groups:
+            for j in range(j0, j1):
+                _tp_wait(works[j])
+            mm_nt(_rows(full[j0 * per:j1 * per]), w, out=_rows(y[j0 * per:j1 * per]), bias=b)
         ctx.save_for_backward(full)
-        ctx.w, ctx.group, ctx.has_bias, ctx.m = w, group, b is not None, m
+        ctx.w, ctx.group, ctx.has_bias, ctx.m, ctx.n = w, group, b is not None, m, n
         return y
 
     @staticmethod
     def backward(ctx, dy):
         from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn
         (full,) = ctx.saved_tensors
-        w, group, m = ctx.w, ctx.group, ctx.m
-        n, cm = full.shape[1], full.shape[2]
-        tail = full.shape[3:]
+        w, group, m, n = ctx.w, ctx.group, ctx.m, ctx.n
+        per = full.shape[0] // m
+        cm = per // n
+        tail = full.shape[1:]
         dy = dy.contiguous()
-        dy5 = dy.view(n, m, cm, *dy.shape[1:])
         dx = dw = db = None
-        works = []
+        works, parts = [], []
         if ctx.needs_input_grad[0]:
             dx = torch.empty((m * cm, *tail), dtype=full.dtype, device=full.device)
-            for j in range(m):  # stage j's input gradient is reduce-scattered while stage j+1's is computed
-                part = torch.empty((n, cm, *tail), dtype=full.dtype, device=full.device)
-                for d in range(n):
-                    mm_nn(_rows(dy5[d, j]), w, out=_rows(part[d]))
-                works.append(dist.reduce_scatter_tensor(dx[j * cm:(j + 1) * cm], part.view(n * cm, *tail), group=group,
-                                                        async_op=True))
+            rows = per * (full[0, ..., 0].numel())
+            for j0, j1 in gemm_groups(m, rows, w.shape[1]):
+                # this group's input gradient is reduce-scattered chunk by chunk while the next one's is computed
+                part = torch.empty(((j1 - j0) * per, *tail), dtype=full.dtype, device=full.device)
+                mm_nn(_rows(dy[j0 * per:j1 * per]), w, out=_rows(part))
+                for j in range(j0, j1):
+                    works.append(dist.reduce_scatter_tensor(dx[j * cm:(j + 1) * cm],
+                                                            part[(j - j0) * per:(j - j0 + 1) * per], group=group,
+                                                            async_op=True))
+                parts.append(part)
         if ctx.needs_input_grad[1]:
-            # the weight gradient per (stage, rank) block, accumulated, under the last reduce-scatters
-            for j in range(m):
-                for d in range(n):
-                    r = _wgrad_mm(w, _rows(dy5[d, j]).t(), _rows(full[j, d]))
-                    dw = r if dw is None else (dw + r if r is not None else dw)
+            # one weight-gradient GEMM over the whole gathered input, under the last reduce-scatters
+            dw = _wgrad_mm(w, _rows(dy).t(), _rows(full))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _rows(dy).sum(0)
         for wk in works:
             _tp_wait(wk)
+        del parts
         drop_dy_t()  # a SwiGLU-produced dy^T is only used by the plain linear path
         return dx, dw, db, None
 
@@ -249,15 +305,19 @@ class _LinearRS(Function):
         c = x.shape[0] // n
         m = tp_stages(c)
         cm = c // m
-        x5 = x.view(n, m, cm, *x.shape[1:])
-        y = torch.empty((c, *x.shape[1:-1], w.shape[0]), dtype=x.dtype, device=x.device)
+        per = n * cm
+        N = w.shape[0]
+        y = torch.empty((c, *x.shape[1:-1], N), dtype=x.dtype, device=x.device)
+        rows = per * (x[0, ..., 0].numel())
+        groups = gemm_groups(m, rows, N)
+        _plan(f"rs:{N}", groups)
         works, parts = [], []
-        for j in range(m):  # stage j's rows are reduce-scattered while stage j+1's are computed
-            part = torch.empty((n, cm, *x.shape[1:-1], w.shape[0]), dtype=x.dtype, device=x.device)
-            for d in range(n):
-                mm_nt(_rows(x5[d, j]), w, out=_rows(part[d]))
-            works.append(dist.reduce_scatter_tensor(y[j * cm:(j + 1) * cm], part.view(n * cm, *part.shape[2:]),
-                                                    group=group, async_op=True))
+        for j0, j1 in groups:  # a group's output rows are reduce-scattered while the next group's are computed
+            part = torch.empty(((j1 - j0) * per, *x.shape[1:-1], N), dtype=x.dtype, device=x.device)
+            mm_nt(_rows(x[j0 * per:j1 * per]), w, out=_rows(part))
+            for j in range(j0, j1):
+                works.append(dist.reduce_scatter_tensor(y[j * cm:(j + 1) * cm], part[(j - j0) * per:(j - j0 + 1) * per],
+                                                        group=group, async_op=True))
             parts.append(part)
         for wk in works:
             _tp_wait(wk)
@@ -277,22 +337,21 @@ class _LinearRS(Function):
         dy = dy.contiguous()
         c = dy.shape[0]
         cm = c // m
-        x5 = x.view(n, m, cm, *x.shape[1:])
-        full = torch.empty((m, n, cm, *dy.shape[1:]), dtype=dy.dtype, device=dy.device)  # stage-major dy
-        works = [dist.all_gather_into_tensor(full[j].view(n * cm, *dy.shape[1:]), dy[j * cm:(j + 1) * cm],
-                                             group=group, async_op=True) for j in range(m)]
+        per = n * cm
+        full = torch.empty((m * per, *dy.shape[1:]), dtype=dy.dtype, device=dy.device)  # the gathered dy, in order
+        works = [dist.all_gather_into_tensor(full[j * per:(j + 1) * per], dy[j * cm:(j + 1) * cm], group=group,
+                                             async_op=True) for j in range(m)]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            dx5 = dx.view(n, m, cm, *x.shape[1:])
-        for j in range(m):
-            _tp_wait(works[j])
-            for d in range(n):
-                if ctx.needs_input_grad[0]:
-                    mm_nn(_rows(full[j, d]), w, out=_rows(dx5[d, j]))
-                if ctx.needs_input_grad[1]:
-                    r = _wgrad_mm(w, _rows(full[j, d]).t(), _rows(x5[d, j]))
-                    dw = r if dw is None else (dw + r if r is not None else dw)
+        rows = per * (x[0, ..., 0].numel())
+        for j0, j1 in gemm_groups(m, rows, w.shape[1]):
+            for j in range(j0, j1):
+                _tp_wait(works[j])
+            if ctx.needs_input_grad[0]:
+                mm_nn(_rows(full[j0 * per:j1 * per]), w, out=_rows(dx[j0 * per:j1 * per]))
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad_mm(w, _rows(full).t(), _rows(x))  # one weight-gradient GEMM
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _rows(dy).sum(0)
         drop_dy_t()  # a SwiGLU-produced dy^T is only used by the plain linear path

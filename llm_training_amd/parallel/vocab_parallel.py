@@ -234,7 +234,10 @@ def _keep_budget(budget, h: torch.Tensor) -> int:
         return int(budget)
     cap = 8 << 30
     if h.is_cuda:
+        # free in the driver PLUS what the caching allocator holds reserved but unused: after warm-up the
+        # allocator owns most of HBM, and the driver's free alone would shrink the budget step after step
         free, _ = torch.cuda.mem_get_info(h.device)
+        free += torch.cuda.memory_reserved(h.device) - torch.cuda.memory_allocated(h.device)
         cap = min(cap, free // 4)
     return cap
 

@@ -348,9 +348,13 @@ class Trainer:
         kernels: ``precision: 32-true`` / ``16-*`` on a GPU runs the torch reference ops for every fused op
         (reference FSDP2Precision runs fp32 / fp16 through the same Liger / flash-attn kernels instead,
         fsdp2_precision.py:19-21,92-96), which is announced here once rather than left silent."""
-        from ..ops.native import compute_path
+        from ..ops.native import DIAG, check_probe_env, compute_path, llmt_env
+        # wrong-result diagnostic probes are refused for training runs (unless the diagnostic library is
+        # loaded on purpose), and every kernel / layout knob the run sees is recorded with it
+        check_probe_env()
         path = compute_path(device.type, self.param_dtype)
-        meta = {"device": device.type, "precision": str(self.precision), "compute_kernels": path}
+        meta = {"device": device.type, "precision": str(self.precision), "compute_kernels": path,
+                "llmt_env": llmt_env(), "native_lib": "diag" if DIAG else "production"}
         if device.type == "cuda" and path != "hip":
             logger.warning("precision %r on the GPU: the fused ops (attention, RMSNorm, SwiGLU, RoPE, loss, "
                            "AdamW) run the torch reference ops, not the bf16 HIP kernels (run_meta "

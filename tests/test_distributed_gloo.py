@@ -102,8 +102,7 @@ def test_zero_stages_match_single_process(stage, offload):
 
 
 def _tp_worker(rank, world, tp, cfg_kw, full0, global_batches, stages=None):
-    if stages is not None:
-        os.environ["LLMT_TP_STAGES"] = str(stages)
+    _tp_env(stages)
     from llm_training_amd.models.llama import Llama
     from llm_training_amd.parallel.context import ParallelContext
     pc = ParallelContext.create("auto", tp, "cpu")
@@ -221,24 +220,81 @@ def test_tensor_sequence_parallel_matches_single_process(world, tp, overlap):
             assert torch.allclose(out[r]["params"][k], v, atol=atol, rtol=1e-4), (r, k)
 
 
-@pytest.mark.parametrize("tp,stages", [(8, None), (8, 1), (4, 2), (4, 1)])
+def _grads_of_one_backward(m, ids):
+    """Loss and full (TP-unsharded) parameter gradients of one forward + backward, no optimizer."""
+    import torch.distributed as dist
+
+    from llm_training_amd.lms.clm import CLM
+    lm = CLM({"model": None})
+    lm.model = m
+    lm.train()
+    loss, _, _ = lm.training_step({"input_ids": ids, "labels": ids})
+    loss.backward()
+    loss = loss.detach()
+    for p in m.parameters():
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        if m.pc.tp and getattr(p, "tp_replicated", False):  # sequence-sharded partial sums (norm weights)
+            dist.all_reduce(g, group=m.pc.tp_group)
+        p.data = g.detach().clone()
+    sd = m.gather_full_state_dict() if m.pc.tp else {k: v.detach().clone() for k, v in m.state_dict().items()}
+    return float(loss), sd
+
+
+def _tp_env(stages):
+    """stages: None (defaults), m, or (m, gemm_tiles): LLMT_TP_STAGES / LLMT_TP_GEMM_TILES for this rank."""
+    if stages is None:
+        return
+    m, tiles = stages if isinstance(stages, tuple) else (stages, None)
+    os.environ["LLMT_TP_STAGES"] = str(m)
+    if tiles is not None:
+        os.environ["LLMT_TP_GEMM_TILES"] = str(tiles)
+
+
+def _tp_grad_worker(rank, world, tp, cfg_kw, full0, ids, stages=None):
+    _tp_env(stages)
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    pc = ParallelContext.create("auto", tp, "cpu")
+    m = Llama(tiny_llama_cfg(**cfg_kw), pc, dtype=torch.float32)
+    m.load_full_state_dict(full0)
+    loss, grads = _grads_of_one_backward(m, ids)
+    return {"loss": loss, "grads": grads}
+
+
+@pytest.mark.parametrize("tp,stages", [(8, None), (8, 1), (8, (4, 2)), (4, 2), (4, (4, 1)), (4, 1), (2, None),
+                                       (2, (8, 1))])
 def test_tensor_parallel_staged_collective_matmul_tp4_tp8(tp, stages):
     """The staged collective matmul (ag_linear / linear_rs: each collective cut into LLMT_TP_STAGES full-mesh
-    pieces pipelined with the per-rank GEMMs) at the reference's TP=8 example degree and at tp 4: losses
-    and parameters equal one process, with the default stage count (sub-chunks of 2 / 1 rows here), 2 stages
-    and the unstaged form (1)."""
+    chunks of the chunked sequence layout, grouped into chip-sized GEMMs, one weight-gradient GEMM) at the
+    reference's TP=8 example degree, tp 4 and tp 2, with the default chunk count, 2 / 4 / 8 chunks, the
+    unstaged form (1) and GEMM groups of 1 / 2 chunks (LLMT_TP_GEMM_TILES; the tiny shapes otherwise run one
+    GEMM over all chunks): the loss and EVERY parameter gradient of one backward equal one process to fp32
+    summation-order noise (a wrong row of the chunk -> rank mapping would show here in full), then after
+    two AdamW steps the losses agree and the parameters agree in bulk."""
     cfg_kw = dict(vocab_size=130, num_attention_heads=8, num_key_value_heads=8, hidden_size=64,
                   intermediate_size=128)
     gb = _batches(130, STEPS, B=2, S=32)
     full0, ref, ref_losses = _single_reference(cfg_kw, gb)
+    from llm_training_amd.models.llama import Llama
+    from llm_training_amd.parallel.context import ParallelContext
+    m1 = Llama(tiny_llama_cfg(**cfg_kw), ParallelContext.single(), dtype=torch.float32)
+    m1.load_full_state_dict(full0)
+    ref_loss1, ref_grads = _grads_of_one_backward(m1, gb[0])
+    outg = run_gloo(_tp_grad_worker, tp, (tp, cfg_kw, full0, gb[0], stages), timeout=400)
+    for r in range(tp):
+        assert abs(outg[r]["loss"] - ref_loss1) < 1e-6, (r, outg[r]["loss"], ref_loss1)
+        for k, v in ref_grads.items():
+            got = outg[r]["grads"][k]
+            scale = float(v.abs().max()) + 1e-12
+            assert float((got - v).abs().max()) <= 1e-5 * scale + 1e-9, (r, k, float((got - v).abs().max()), scale)
     out = run_gloo(_tp_worker, tp, (tp, cfg_kw, full0, gb, stages), timeout=400)
     for r in range(tp):
         assert max(abs(a - b) for a, b in zip(out[r]["losses"], ref_losses)) < 1e-5, (r, out[r]["losses"], ref_losses)
         for k, v in ref.items():
             d = (out[r]["params"][k] - v).abs()
-            # AdamW turns fp32 summation-order noise on near-zero gradients into small parameter differences
-            # on a few elements (see the test above); the bulk must agree tightly
-            assert float(d.max()) < 3e-3 and float(d.mean()) < 2e-5, (r, k, float(d.max()), float(d.mean()))
+            # AdamW (lr 1e-2, 2 steps) turns fp32 summation-order noise on near-zero gradients into parameter
+            # moves of up to ~lr per step on single elements; the gradients are checked tightly above
+            assert float(d.max()) < 2.5e-2 and float(d.mean()) < 2e-5, (r, k, float(d.max()), float(d.mean()))
 
 
 def _vp_worker(rank, world, h, w, labels, chunk, vocab, keep):

@@ -368,12 +368,13 @@ _DKDV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", ["4", "5"])
+@pytest.mark.parametrize("variant", ["default", "generic"])
 @pytest.mark.parametrize("case", range(len(_DKDV_CASES) + 2))
 def test_flash_attention_dkdv_variant(monkeypatch, variant, case):
-    """The dK/dV kernel variants selected by LLMT_FA_BWD_VARIANT against the fp32 oracle: causal / not,
-    windows, GQA, D 64 / 96 / 128, several ring wraps, packed segments."""
-    monkeypatch.setenv("LLMT_FA_BWD_VARIANT", variant)
+    """The default (fa_bwd_dq3 + fa_bwd_dkdv5) and the generic backward kernels (LLMT_FA_GENERIC=1) against
+    the fp32 oracle: causal / not, windows, GQA, D 64 / 96 / 128, several ring wraps, packed segments."""
+    if variant == "generic":
+        monkeypatch.setenv("LLMT_FA_GENERIC", "1")
     if case < len(_DKDV_CASES):
         _attn_case(**_DKDV_CASES[case])
         return

@@ -108,9 +108,7 @@ def test_rope_fused_leaves_queries_unrotated():
     assert torch.equal(qkv[:, :, nq + nkv:], ref[:, :, nq + nkv:])
 
 
-@pytest.mark.parametrize("env", [("LLMT_FA_FWD_VARIANT", "0"), ("LLMT_FA_FWD_VARIANT", "10"),
-                                 ("LLMT_FA_FWD_VARIANT", "6"), ("LLMT_FA_BWD_VARIANT", "3"),
-                                 ("LLMT_FA_BWD_VARIANT", "7")])
+@pytest.mark.parametrize("env", [("LLMT_FA_GENERIC", "1"), ("LLMT_FA_RANGE_MASK", "0"), ("LLMT_FA_EARLY_DMA", "0")])
 @pytest.mark.parametrize("mode", ["bwd", "full"])
 def test_rope_fused_fallback_paths(env, mode, monkeypatch):
     # launch paths without the in-kernel rotation: the dispatcher rotates into the scratch copy / runs the

@@ -265,7 +265,39 @@ def test_run_meta_reaches_the_logger(tmp_path):
                 enable_checkpointing=False)
     t.fit(_lm(), _dm())
     hp = json.load(open(tmp_path / "r" / "hparams.json"))
-    assert hp["run_meta"] == {"device": "cpu", "precision": "32-true", "compute_kernels": "torch-reference"}
+    meta = hp["run_meta"]
+    assert {k: meta[k] for k in ("device", "precision", "compute_kernels")} == {
+        "device": "cpu", "precision": "32-true", "compute_kernels": "torch-reference"}
+    assert meta["native_lib"] == "production"
+    assert isinstance(meta["llmt_env"], dict) and all(k.startswith("LLMT_") for k in meta["llmt_env"])
+
+
+def test_run_meta_records_llmt_knobs(tmp_path, monkeypatch):
+    """Every LLMT_* knob of the environment is recorded with the run (bench JSON and Trainer run_meta)."""
+    import json
+    monkeypatch.setenv("LLMT_FA_BMAJOR", "0")
+    monkeypatch.setenv("LLMT_TP_STAGES", "2")
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=1, seed=1, logger=JSONLLogger(str(tmp_path), "r"),
+                enable_checkpointing=False)
+    t.fit(_lm(), _dm())
+    env = json.load(open(tmp_path / "r" / "hparams.json"))["run_meta"]["llmt_env"]
+    assert env["LLMT_FA_BMAJOR"] == "0" and env["LLMT_TP_STAGES"] == "2"
+
+
+@pytest.mark.parametrize("var", ["LLMT_FA_PROBE", "LLMT_FA_D6_PROBE"])
+def test_trainer_refuses_wrong_result_probes(tmp_path, monkeypatch, var):
+    """A diagnostic probe variable (kernels that compute wrong results on purpose) makes a training run
+    refuse to start with the production library; the native loader refuses it too."""
+    from llm_training_amd.ops import native
+    monkeypatch.setenv(var, "1")
+    t = Trainer(strategy="ddp", precision="32-true", max_steps=1, seed=1, enable_checkpointing=False,
+                default_root_dir=str(tmp_path))
+    with pytest.raises(RuntimeError, match="diagnostic probes"):
+        t.fit(_lm(), _dm())
+    with pytest.raises(RuntimeError, match="diagnostic probes"):
+        native.check_probe_env()
+    monkeypatch.setenv(var, "0")
+    native.check_probe_env()  # "0" = off
 
 
 def test_use_native_counts_reference_ops_on_gpu(monkeypatch):
