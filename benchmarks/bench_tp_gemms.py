@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--tp", default="2,8")
     ap.add_argument("--shapes", default="8192x4,131072x1")
     args = ap.parse_args()
-    from llm_training_amd.ops.fused import mm_nn, mm_nt, wgrad_into
+    from llm_training_amd.ops.fused import mm_nn, mm_nt, weight_t, wgrad_into
     from llm_training_amd.parallel.tensor_parallel import gemm_groups, tp_stages
     dev = "cuda"
     for tp in (int(t) for t in args.tp.split(",")):
@@ -78,9 +78,10 @@ def main():
                     for j0, j1 in gf:
                         mm_nt(x[j0 * rc:j1 * rc], w, out=y[j0 * rc:j1 * rc])
 
-                def dgrad_staged():
+                def dgrad_staged():  # one W^T shared by the groups, as tensor_parallel does
+                    wt = weight_t(w, T)
                     for j0, j1 in gd:
-                        mm_nn(dy[j0 * rc:j1 * rc], w, out=dx[j0 * rc:j1 * rc])
+                        mm_nn(dy[j0 * rc:j1 * rc], w, out=dx[j0 * rc:j1 * rc], wt=wt)
 
                 def wgrad_one():
                     wgrad_into(gw, dy, x, False)

@@ -37,8 +37,11 @@ and the embedding are per-token and do not care, and attention / the loss only e
   GEMMs group by group, and again one weight-gradient GEMM.
 
 GEMM granularity: consecutive chunks are grouped so that each GEMM fills the chip with at least
-``LLMT_TP_GEMM_TILES`` (default 512 = two waves of 256 CUs) output tiles of 256 x 256; a projection whose
-chunk already does runs one GEMM per chunk (benchmarks/bench_tp_gemms.py). The compute stream's waits are
+``LLMT_TP_GEMM_TILES`` (default 1024 = four waves of 256 CUs) output tiles of 256 x 256; a projection whose
+chunk already does runs one GEMM per chunk. The input-gradient GEMMs of all groups share one W^T (the TN
+layout hipBLASLt runs fastest). On one GPU the staged sequences run within 0-7 % of the single unstaged GEMM
+of the same FLOPs, against up to 5x for the per-(chunk, rank) GEMMs of round 5
+(benchmarks/bench_tp_gemms.py, profiles/r6_tp_gemms.md). The compute stream's waits are
 metered when ``TP_WAIT_METER`` holds a list (bench.py reports the exposed tensor-parallel communication
 per step from it); ``STAGE_PLANS`` records the group sizes each projection ran with.
 """
@@ -215,8 +218,9 @@ def _tp_wait(work) -> None:
 
 def gemm_groups(m: int, chunk_rows: int, ncols: int) -> list[tuple[int, int]]:
     """Consecutive chunk ranges [j0, j1) of the m chunks, one GEMM each: the smallest group size dividing m
-    whose GEMM ([g * chunk_rows, ncols] output) has at least LLMT_TP_GEMM_TILES 256 x 256 tiles."""
-    want = max(1, int(os.environ.get("LLMT_TP_GEMM_TILES", "512")))
+    whose GEMM ([g * chunk_rows, ncols] output) has at least LLMT_TP_GEMM_TILES (default 1024) 256 x 256
+    tiles."""
+    want = max(1, int(os.environ.get("LLMT_TP_GEMM_TILES", "1024")))
     tiles = -(-chunk_rows // 256) * -(-ncols // 256)
     g = m
     for d in range(1, m + 1):
@@ -260,7 +264,7 @@ class _AGLinear(Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn
+        from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn, weight_t
         (full,) = ctx.saved_tensors
         w, group, m, n = ctx.w, ctx.group, ctx.m, ctx.n
         per = full.shape[0] // m
@@ -272,10 +276,11 @@ class _AGLinear(Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty((m * cm, *tail), dtype=full.dtype, device=full.device)
             rows = per * (full[0, ..., 0].numel())
+            wt = weight_t(w, m * rows)  # W^T once for every group's TN input-gradient GEMM (or None)
             for j0, j1 in gemm_groups(m, rows, w.shape[1]):
                 # this group's input gradient is reduce-scattered chunk by chunk while the next one's is computed
                 part = torch.empty(((j1 - j0) * per, *tail), dtype=full.dtype, device=full.device)
-                mm_nn(_rows(dy[j0 * per:j1 * per]), w, out=_rows(part))
+                mm_nn(_rows(dy[j0 * per:j1 * per]), w, out=_rows(part), wt=wt)
                 for j in range(j0, j1):
                     works.append(dist.reduce_scatter_tensor(dx[j * cm:(j + 1) * cm],
                                                             part[(j - j0) * per:(j - j0 + 1) * per], group=group,
@@ -330,7 +335,7 @@ class _LinearRS(Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn
+        from ..ops.fused import _wgrad_mm, drop_dy_t, mm_nn, weight_t
         (x,) = ctx.saved_tensors
         w, group, m = ctx.w, ctx.group, ctx.m
         n = _ws(group)
@@ -345,11 +350,12 @@ class _LinearRS(Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
         rows = per * (x[0, ..., 0].numel())
+        wt = weight_t(w, m * rows) if ctx.needs_input_grad[0] else None
         for j0, j1 in gemm_groups(m, rows, w.shape[1]):
             for j in range(j0, j1):
                 _tp_wait(works[j])
             if ctx.needs_input_grad[0]:
-                mm_nn(_rows(full[j0 * per:j1 * per]), w, out=_rows(dx[j0 * per:j1 * per]))
+                mm_nn(_rows(full[j0 * per:j1 * per]), w, out=_rows(dx[j0 * per:j1 * per]), wt=wt)
         if ctx.needs_input_grad[1]:
             dw = _wgrad_mm(w, _rows(full).t(), _rows(x))  # one weight-gradient GEMM
         if ctx.has_bias and ctx.needs_input_grad[2]:
