@@ -48,7 +48,26 @@ struct Choice {
   hipblasLtMatmulAlgo_t algo;
   int rank;
   float ms;
+  int gsu;  // 0: the solution as it is (hipblasLtMatmul); > 0: run through hipblaslt_ext::Gemm with GemmTuning splitK
 };
+
+// Split-K counts (hipBLASLt "GSU": the solution splits the contraction itself and reduces the partial tiles in
+// the library, no fp32 slabs of ours) tried beside every timed candidate whose output has fewer than
+// kGsuMaxTiles 256 x 256 tiles: the weight gradients of the projections fill the 256 CUs in 1-4 waves of tiles
+// over a 32768-token contraction. LLMT_GEMM_GSU = comma-separated counts ("" or 0: off).
+const std::vector<int> kGsu = [] {
+  std::vector<int> v;
+  const char* e = std::getenv("LLMT_GEMM_GSU");
+  std::string t = e ? e : "";
+  std::stringstream ss(t);
+  std::string item;
+  while (std::getline(ss, item, ',')) {
+    const int x = std::atoi(item.c_str());
+    if (x > 1) v.push_back(x);
+  }
+  return v;
+}();
+constexpr int64_t kGsuMaxTiles = 1024;
 
 struct State {
   std::mutex mu;
@@ -199,11 +218,12 @@ void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool t
       got = std::min(got, kCandidates);
     }
     TORCH_CHECK(got > 0, "gemm_lt: no hipBLASLt solution for ", key);
-    Choice best{res[0].algo, 0, -1.f};
+    Choice best{res[0].algo, 0, -1.f, 0};
     auto pre = s.preset.find(key);
+    const bool gsu_try = !kGsu.empty() && batch == 1 && ((m + 255) / 256) * ((n + 255) / 256) < kGsuMaxTiles;
     if (pre != s.preset.end() && pre->second < got) {
-      best = Choice{res[pre->second].algo, pre->second, 0.f};
-    } else if ((s.tune || !streamk) && got > 1) {  // non-stream-K candidates are always timed
+      best = Choice{res[pre->second].algo, pre->second, 0.f, 0};
+    } else if ((s.tune || !streamk || gsu_try) && (got > 1 || gsu_try)) {  // non-stream-K candidates are always timed
       // time every candidate on the live operands; the output goes to a scratch tensor so an
       // accumulating call (beta = 1) is not disturbed
       auto scratch = at::empty_like(C);
@@ -226,12 +246,43 @@ void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool t
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, e0, e1);
         ms /= kReps;
-        if (best.ms < 0.f || ms < best.ms) best = Choice{res[i].algo, i, ms};
+        if (best.ms < 0.f || ms < best.ms) best = Choice{res[i].algo, i, ms, 0};
+        if (!gsu_try) continue;
+        for (int gs : kGsu) {  // the same solution with the library's own split-K
+          hipblaslt_ext::Gemm eg(h, d.op, &alpha, A.data_ptr(), d.a, B.data_ptr(), d.b, &beta, scratch.data_ptr(), d.c,
+                                 scratch.data_ptr(), d.c);
+          hipblaslt_ext::GemmTuning tun;
+          tun.setSplitK((uint16_t)gs);
+          size_t wsz = 0;
+          if (eg.isAlgoSupported(res[i].algo, tun, wsz) != HIPBLAS_STATUS_SUCCESS || wsz > kWorkspace) continue;
+          if (eg.initialize(res[i].algo, tun, ws.data_ptr(), false, stream) != HIPBLAS_STATUS_SUCCESS) continue;
+          if (eg.run(stream) != HIPBLAS_STATUS_SUCCESS) continue;  // warm-up
+          (void)hipEventRecord(e0, stream);
+          for (int r = 0; r < kReps; ++r) (void)eg.run(stream);
+          (void)hipEventRecord(e1, stream);
+          (void)hipEventSynchronize(e1);
+          float gms = 0.f;
+          (void)hipEventElapsedTime(&gms, e0, e1);
+          gms /= kReps;
+          if (gms < best.ms) best = Choice{res[i].algo, i, gms, gs};
+        }
       }
       (void)hipEventDestroy(e0);
       (void)hipEventDestroy(e1);
     }
     it = s.cache.emplace(key, best).first;
+  }
+  if (it->second.gsu > 0) {  // the library's split-K form of the chosen solution
+    hipblaslt_ext::Gemm eg(h, d.op, &alpha, A.data_ptr(), d.a, B.data_ptr(), d.b, &beta, C.data_ptr(), d.c,
+                           C.data_ptr(), d.c);
+    hipblaslt_ext::GemmTuning tun;
+    tun.setSplitK((uint16_t)it->second.gsu);
+    size_t wsz = 0;
+    hipblasLtMatmulAlgo_t algo = it->second.algo;
+    LT_CHECK(eg.isAlgoSupported(algo, tun, wsz));
+    LT_CHECK(eg.initialize(algo, tun, ws.data_ptr(), false, stream));
+    LT_CHECK(eg.run(stream));
+    return;
   }
   LT_CHECK(hipblasLtMatmul(h, d.op, &alpha, A.data_ptr(), d.a, B.data_ptr(), d.b, &beta, C.data_ptr(), d.c,
                            C.data_ptr(), d.c, &it->second.algo, ws.data_ptr(), kWorkspace, stream));
@@ -261,7 +312,7 @@ std::string gemm_lt_export() {
   for (auto& kv : s.cache) {
     hipblasLtMatmulAlgo_t a = kv.second.algo;
     o << kv.first << " " << kv.second.rank << " " << kv.second.ms << " "
-      << hipblaslt_ext::getKernelNameFromAlgo(s.handles.begin()->second, a) << "\n";
+      << hipblaslt_ext::getKernelNameFromAlgo(s.handles.begin()->second, a) << " gsu" << kv.second.gsu << "\n";
   }
   return o.str();
 }
