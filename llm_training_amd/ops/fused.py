@@ -663,9 +663,12 @@ class _SwiGLUFn(Function):
 
 # The down projection's input gradient with the SwiGLU backward in its epilogue (csrc/gemm.hip SwiArgs, the
 # hand-written ping-pong GEMM): dc = dy @ W_down is never written; the epilogue reads gate / up of its tile and
-# writes dgu (and dgu^T for the TN gate_up weight gradient). LLMT_SWIGLU_GEMM=0 runs hipBLASLt + the separate
-# swiglu_bwd_tr pass instead (A/B reference).
-SWIGLU_GEMM = [os.environ.get("LLMT_SWIGLU_GEMM", "1").strip().lower() not in ("0", "false", "off")]
+# writes dgu (and dgu^T for the TN gate_up weight gradient). Opt-in (LLMT_SWIGLU_GEMM=1): in alternating
+# same-box step runs it LOST to hipBLASLt + the separate swiglu_bwd_tr pass — Llama-3-8B PT 1511.3 / 1509.9 /
+# 1512.0 vs 1509.6 / 1508.9 / 1509.7 ms, Phi-3-mini IT 1342.7 / 1343.9 vs 1332.2 / 1338.1 ms
+# (profiles/r6_swiglu_gemm.md): the own GEMM is 0.58 ms behind hipBLASLt on this problem, more than the
+# dc round trip it saves, and the epilogue's 5.6 GB move at HBM rate with every CU in its epilogue at once.
+SWIGLU_GEMM = [os.environ.get("LLMT_SWIGLU_GEMM", "0").strip().lower() in ("1", "true", "on")]
 
 
 class _SwiGLUDownFn(Function):
