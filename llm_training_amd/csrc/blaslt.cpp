@@ -73,7 +73,7 @@ struct State {
   std::mutex mu;
   std::map<int, hipblasLtHandle_t> handles;
   std::map<std::string, Choice> cache;
-  std::map<std::string, int> preset;  // imported winners: key -> heuristic rank
+  std::map<std::string, std::pair<int, int>> preset;  // imported winners: key -> (heuristic rank, GSU split)
   // Timing the candidates is opt-in (LLMT_GEMM_TUNE=1): on the Llama-3-8B shapes the heuristic's first
   // choice won every problem (benchmarks/bench_gemm_paths.py), and timing ~15 problems x 24 candidates
   // costs seconds of start-up.
@@ -221,8 +221,8 @@ void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool t
     Choice best{res[0].algo, 0, -1.f, 0};
     auto pre = s.preset.find(key);
     const bool gsu_try = !kGsu.empty() && batch == 1 && ((m + 255) / 256) * ((n + 255) / 256) < kGsuMaxTiles;
-    if (pre != s.preset.end() && pre->second < got) {
-      best = Choice{res[pre->second].algo, pre->second, 0.f, 0};
+    if (pre != s.preset.end() && pre->second.first < got) {
+      best = Choice{res[pre->second.first].algo, pre->second.first, 0.f, pre->second.second};
     } else if ((s.tune || !streamk || gsu_try) && (got > 1 || gsu_try)) {  // non-stream-K candidates are always timed
       // time every candidate on the live operands; the output goes to a scratch tensor so an
       // accumulating call (beta = 1) is not disturbed
@@ -317,23 +317,48 @@ std::string gemm_lt_export() {
   return o.str();
 }
 
+// parses "key rank [ms kernel gsuN]" lines (gemm_lt_export's format) into the preset map; with `replace`, a
+// cached choice of this process that differs is dropped, so the next call of that problem re-resolves to the
+// imported one. Returns the number of lines read (replace = false) or of cached choices replaced.
+int64_t read_presets(State& s, const std::string& text, bool replace) {
+  std::istringstream in(text);
+  std::string line;
+  int64_t n = 0, replaced = 0;
+  while (std::getline(in, line)) {
+    std::istringstream ls(line);
+    std::string key, ms, name, g;
+    int rank;
+    if (!(ls >> key >> rank)) continue;
+    int gsu = 0;
+    if (ls >> ms >> name >> g && g.rfind("gsu", 0) == 0) gsu = std::atoi(g.c_str() + 3);
+    s.preset[key] = {rank, gsu};
+    ++n;
+    if (!replace) continue;
+    auto it = s.cache.find(key);
+    if (it != s.cache.end() && (it->second.rank != rank || it->second.gsu != gsu)) {
+      s.cache.erase(it);
+      ++replaced;
+    }
+  }
+  return replace ? replaced : n;
+}
+
 int64_t gemm_lt_import(const std::string& text, bool tune_unknown) {
   auto& s = st();
   std::lock_guard<std::mutex> lock(s.mu);
-  std::istringstream in(text);
-  std::string line;
-  int64_t n = 0;
-  while (std::getline(in, line)) {
-    std::istringstream ls(line);
-    std::string key;
-    int rank;
-    if (ls >> key >> rank) {
-      s.preset[key] = rank;
-      ++n;
-    }
-  }
+  const int64_t n = read_presets(s, text, false);
   s.tune = tune_unknown;
   return n;
+}
+
+// Adopt another process's solution choices (rank 0's, broadcast by ops.fused.agree_layouts): every rank then
+// runs the same hipBLASLt kernel per problem instead of the one its own first-sight timing picked (the
+// non-stream-K candidates are timed per rank at dp > 1, under that rank's collectives). Problems not met yet
+// take the adopted choice on first sight. Returns the number of this process's choices replaced.
+int64_t gemm_lt_adopt(const std::string& text) {
+  auto& s = st();
+  std::lock_guard<std::mutex> lock(s.mu);
+  return read_presets(s, text, true);
 }
 
 }  // namespace
@@ -350,6 +375,7 @@ TORCH_LIBRARY_FRAGMENT(llmt, m) {
       "int ldb, int ldc, bool streamk=True) -> ()");
   m.def("gemm_lt_export() -> str", &gemm_lt_export);
   m.def("gemm_lt_import(str text, bool tune_unknown) -> int", &gemm_lt_import);
+  m.def("gemm_lt_adopt(str text) -> int", &gemm_lt_adopt);
 }
 
 TORCH_LIBRARY_IMPL(llmt, CUDA, m) {

@@ -26,7 +26,7 @@ import torch
 from torch.autograd import Function
 
 from . import reference as ref
-from .native import lib, use_native
+from .native import available as native_available, lib, use_native
 
 log = logging.getLogger("llm_training.ops")
 
@@ -166,9 +166,18 @@ def agree_layouts(group=None) -> int:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) <= 1:
         return 0
-    obj = [{layout_key_str(k): v for k, v in _LAYOUT_CACHE.items()} if dist.get_rank() == 0 else None]
+    # rank 0's hipBLASLt solution choices travel with its layouts: below stream-K (dp > 1 / tp > 1) each rank
+    # times the library's candidates on first sight, under its own collectives, and could keep a different
+    # kernel for the same problem (csrc/blaslt.cpp gemm_lt_adopt)
+    lt = native_available() and torch.cuda.is_available()
+    mine = {layout_key_str(k): v for k, v in _LAYOUT_CACHE.items()}
+    obj = [(mine, lib().gemm_lt_export() if lt else "") if dist.get_rank() == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=group)
-    theirs = obj[0] or {}
+    theirs, lt_text = obj[0] or ({}, "")
+    if lt and lt_text and dist.get_rank() != 0:
+        n = lib().gemm_lt_adopt(lt_text)
+        if n:
+            log.info("hipBLASLt: %d solution choice(s) replaced by rank 0's", n)
     changed = 0
     for k in list(_LAYOUT_CACHE):
         c = theirs.get(layout_key_str(k))

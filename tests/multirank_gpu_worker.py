@@ -94,9 +94,14 @@ def main():
         eng.wait_params()
         sd = m.gather_full_state_dict() if pc.tp else {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
     torch.cuda.synchronize()
+    # every rank's hipBLASLt solution per problem (key -> "rank gsuN"): rank 0's after agree_layouts
+    from llm_training_amd.ops.native import lib
+    mine = {ln.split()[0]: ln.split()[1] + " " + ln.split()[-1] for ln in lib().gemm_lt_export().splitlines()}
+    every = [None] * dist.get_world_size()
+    dist.all_gather_object(every, mine)
     if dist.get_rank() == 0:
         torch.save({"losses": losses, "params": {k: v.float().cpu() for k, v in sd.items()},
-                    "grad_norm": float(eng.grad_norm)}, out)
+                    "grad_norm": float(eng.grad_norm), "lt_choices": every}, out)
     dist.barrier()
     dist.destroy_process_group()
 

@@ -624,6 +624,31 @@ def test_gemm_lt_tuned_layouts(layout, out):
     assert "_acc" in lib().gemm_lt_export() or layout != "tn" or not out.endswith("acc")
 
 
+def test_gemm_lt_adopt_replaces_choice():
+    """csrc/blaslt.cpp gemm_lt_adopt (rank 0's choices broadcast by ops.fused.agree_layouts): a cached
+    non-stream-K solution of this process is replaced by the adopted heuristic rank, the next call runs it
+    (same result within GEMM reordering) and the export reports it."""
+    torch.manual_seed(0)
+    M, N, K = 1536, 640, 768  # a problem no other test uses: its cache entry starts here
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    # column-major c^T (N x M) = b (from K x N, op T) . a^T (K x M): the forward layout, non-stream-K (timed)
+    lib().gemm_lt(b, a, c, True, False, N, M, K, K, K, N, False, False)
+    want = a.float() @ b.float().t()
+    assert _rel(c, want) < 1e-2
+    line = next(l for l in lib().gemm_lt_export().splitlines() if l.startswith(f"tn_{N}_{M}_{K}_") and "_nosk" in l)
+    key, rank = line.split()[:2]
+    other = 1 if int(rank) == 0 else 0
+    assert lib().gemm_lt_adopt(f"{key} {other} 0 adopted gsu0\n") == 1
+    assert lib().gemm_lt_adopt(f"{key} {other} 0 adopted gsu0\n") == 0  # not cached yet: preset only
+    c.zero_()
+    lib().gemm_lt(b, a, c, True, False, N, M, K, K, K, N, False, False)
+    assert _rel(c, want) < 1e-2
+    now = next(l for l in lib().gemm_lt_export().splitlines() if l.startswith(key + " "))
+    assert int(now.split()[1]) == other
+
+
 @pytest.mark.parametrize("D,Hq,Hkv,segs", [(128, 4, 2, False), (64, 2, 2, True), (128, 2, 2, True)])
 def test_flash_attention_dropout_matches_oracle(D, Hq, Hkv, segs):
     """Attention dropout inside the HIP kernels (generic fwd / dQ / dK-dV kernels): the keep mask is a

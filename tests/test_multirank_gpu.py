@@ -60,6 +60,10 @@ def test_two_ranks_on_one_gpu_match_single_process(reference, mode):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-4000:]
     got = torch.load(out, weights_only=True)
+    # rank 1 runs rank 0's hipBLASLt solutions (ops.fused.agree_layouts -> gemm_lt_adopt)
+    r0, r1 = got["lt_choices"]
+    common = set(r0) & set(r1)
+    assert common and all(r0[k] == r1[k] for k in common), {k: (r0[k], r1[k]) for k in common if r0[k] != r1[k]}
     # dp: the mean of the two half-batch losses is the full-batch loss (equal token counts); bf16 kernels
     for a, b in zip(got["losses"], ref_losses):
         assert abs(a - b) < 2e-2 * abs(b), (mode, got["losses"], ref_losses)
