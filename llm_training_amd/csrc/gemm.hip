@@ -7,20 +7,18 @@
 //   dgrad    dx = dy . W    : X = dy [T, N]  K-major,   Y = W [N, K]   MN-major (contraction = W's rows)
 //   wgrad    dW = dy^T . x  : X = dy [T, N]  MN-major,  Y = x [T, K]   MN-major (contraction = tokens)
 //
-// The projections and the lm_head of the models are these GEMMs. Two kernels: the
-// two-group ping-pong kernel (gemm_pp_kernel, default; 1.23-1.28 PF/s on the Llama-3-8B shapes at 32768
-// tokens) and the single-group ring kernel below (LLMT_GEMM_KERNEL=ring; 1.10-1.16). hipBLASLt reaches
-// 1.41-1.61 on the forward layout, so the framework uses these only as timed weight-gradient candidates
-// (profiles/r3_gemm_pingpong.md).
+// The projections and the lm_head of the models are these GEMMs. The kernel is the
+// two-group ping-pong kernel gemm_pp_kernel (1.23-1.28 PF/s on the Llama-3-8B shapes at 32768 tokens; a
+// single-group ring kernel, 1.10-1.16, was removed in round 6). hipBLASLt reaches 1.41-1.61 on the forward
+// layout, so the framework uses this kernel as a timed weight-gradient candidate (it reads both token-major
+// operands without transposes) and for the opt-in SwiGLU-backward epilogue (profiles/r3_gemm_pingpong.md,
+// profiles/r6_gemm_pmc.md).
 //
-// Ring kernel structure (one 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N), 256 x 256 output tile):
+// Operand staging:
 //  * K advances in 32-deep stages. Each stage's X and Y tiles (16 KB each) arrive by LDS-DMA
-//    (`buffer_load_dwordx4 ... lds`, one 1-KB piece per wave-instruction) into a ring of kNS LDS slots,
-//    kNS-1 stages ahead of the MFMAs, behind a counted `s_waitcnt vmcnt` and ONE raw barrier per stage:
-//    the loads never drain inside the loop.
-//  * fragments are software-pipelined one stage ahead: after the barrier that publishes stage t+1 the
-//    wave issues its LDS reads of stage t+1, then runs the 32 MFMAs of stage t on the registers read one
-//    iteration earlier, so LDS latency and the DMA issue hide under the MFMAs.
+//    (`buffer_load_dwordx4 ... lds`, one 1-KB piece per wave-instruction) into a ring of LDS slots, several
+//    stages ahead of the MFMAs, behind a counted `s_waitcnt vmcnt` and raw barriers: the loads never drain
+//    inside the loop.
 //  * LDS images are lane-linear (the DMA writes base + 16 * lane); bank conflicts are removed by
 //    permuting the SOURCE address and reading through the same involution:
 //      K-major image [256 rows][32 k] (64-B rows): 16-B chunk c of row r at chunk c ^ (-(r >> 2) & 3);
@@ -48,7 +46,7 @@ typedef short gs4 __attribute__((ext_vector_type(4)));
 typedef float gf4 __attribute__((ext_vector_type(4)));
 typedef unsigned int gu4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 256, kBN = 256, kBK = 32, kNS = 5;
+constexpr int kBM = 256, kBN = 256, kBK = 32;
 constexpr int kImg = kBM * kBK * 2;  // 16 KB: one operand's image of one stage
 constexpr int kSlot = 2 * kImg;      // X image + Y image
 constexpr int kPieces = 2 * kBM * kBK * 2 / 1024;  // 1-KB DMA pieces per stage (both operands)
@@ -90,20 +88,6 @@ __device__ __forceinline__ void g_dma16(const GRsrc& r, uint32_t lds_base, int v
 template <int N>
 __device__ __forceinline__ void g_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// wait until at most `stages` later stages' DMAs of this wave (D per stage) are outstanding
-template <int D>
-__device__ __forceinline__ void g_wait_stages(int stages) {
-  static_assert(kNS - 2 <= 3 && 3 * D <= 63, "extend the switch / vmcnt range");
-  if (stages >= 3)
-    g_wait_vm<3 * D>();
-  else if (stages == 2)
-    g_wait_vm<2 * D>();
-  else if (stages == 1)
-    g_wait_vm<D>();
-  else
-    g_wait_vm<0>();
 }
 
 // This wave's LDS reads retired, then a barrier that leaves the DMA ring in flight (no vmcnt(0)). The
@@ -211,170 +195,6 @@ __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   const int in = wg - g * per;
   tm = first + in % gsz;
   tn = in / gsz;
-}
-
-// OUT: 0 = bf16 store, 1 = fp32 store, 2 = fp32 accumulate, 3 = bf16 accumulate (C = bf16(C + X.Y^T))
-// NW: waves per workgroup, as 2 (M) x NW/2 (N); wave tile 128 x (512 / NW): NW = 8 -> 128 x 64 (two
-// waves per SIMD), NW = 4 -> 128 x 128 (one wave per SIMD, 256 accumulators in AGPRs, half the LDS
-// fragment traffic per MFMA).
-template <bool XMN, bool YMN, int OUT, int NW>
-__global__ __launch_bounds__(NW * 64) void gemm_kernel(GemmArgs g) {
-  constexpr int WTN = 512 / NW, NJ = WTN / 16, DMA = kPieces / NW;
-  __shared__ __attribute__((aligned(16))) char smem[kNS * kSlot];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases live in SGPRs
-  int tm, tn;
-  tile_coords(g.M, g.N, tm, tn);
-  const int row0 = tm * kBM, col0 = tn * kBN;
-
-  Opnd<XMN, NW> X;
-  Opnd<YMN, NW> Y;
-  if constexpr (!XMN)
-    X.init(g.x, g.ldx, g.M, g.K, row0, w, lane);
-  else
-    X.init(g.x, g.ldx, g.K, g.M, row0, w, lane);
-  if constexpr (!YMN)
-    Y.init(g.y, g.ldy, g.N, g.K, col0, w, lane);
-  else
-    Y.init(g.y, g.ldy, g.K, g.N, col0, w, lane);
-  const uint32_t lbase = g_lds(smem);
-
-  auto issue = [&](int t, int slot) {
-    const uint32_t s = lbase + (uint32_t)(slot * kSlot);
-    const GRsrc rx = X.rsrc(t), ry = Y.rsrc(t);
-#pragma unroll
-    for (int i = 0; i < 16 / NW; ++i) g_dma16(rx, s + (w + NW * i) * 1024, X.off[i]);
-#pragma unroll
-    for (int i = 0; i < 16 / NW; ++i) g_dma16(ry, s + kImg + (w + NW * i) * 1024, Y.off[i]);
-  };
-
-  const int wm = w / (NW / 2), wn = w % (NW / 2);
-  struct Frags {
-    gbf8 y[NJ];  // MFMA A operand: output columns
-    gbf8 x[8];  // MFMA B operand: output rows
-  };
-  auto read_frags = [&](Frags& f, const char* slot) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) f.y[j] = Y.frag(slot + kImg, wn * WTN + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) f.x[i] = X.frag(slot, wm * 128 + i * 16, lane);
-  };
-
-  gf4 acc[8][NJ];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = gf4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const Frags& f) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.y[j], f.x[i], acc[i][j], 0, 0, 0);
-  };
-
-  const int nk = g.K / kBK;
-  // prologue: stages 0 .. kNS-2 in flight, stage 0's fragments in registers
-#pragma unroll
-  for (int s = 0; s < kNS - 1; ++s)
-    if (s < nk) issue(s, s);
-  g_wait_stages<DMA>(min(nk - 1, kNS - 2));
-  g_barrier();
-  Frags f0, f1;
-  read_frags(f0, smem);
-
-  int slot_next = 1;         // slot of stage t+1
-  int slot_issue = kNS - 1;  // slot of stage t+kNS-1 (= the slot stage t-1 used)
-  // Iteration t: publish stage t+1 (its reads of the previous slot user retired before this barrier),
-  // refill the ring with stage t+kNS-1, read stage t+1's fragments, MFMA stage t.
-  // (every body reads the next stage unconditionally, so hipcc's lgkmcnt ladder before the MFMAs counts
-  // the just-issued reads as outstanding; the last stage is peeled off below)
-  auto body = [&](int t, Frags& cur, Frags& nxt) {
-    g_wait_stages<DMA>(min(nk - 1, t + kNS - 2) - (t + 1));
-    g_barrier();
-    if (t + kNS - 1 < nk) issue(t + kNS - 1, slot_issue);
-    read_frags(nxt, smem + slot_next * kSlot);
-    slot_next = slot_next + 1 == kNS ? 0 : slot_next + 1;
-    slot_issue = slot_issue + 1 == kNS ? 0 : slot_issue + 1;
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs (and the register budget flat)
-    mma(cur);
-  };
-  int t = 0;
-  for (; t + 2 < nk; t += 2) {
-    body(t, f0, f1);
-    body(t + 1, f1, f0);
-  }
-  if (t + 1 < nk) {  // two stages left
-    body(t, f0, f1);
-    f0 = f1;
-  }
-  mma(f0);
-
-  // epilogue: lane holds C[m][n .. n+3], m = row (lane & 15) of m-tile i, n = 4 * (lane >> 4) of n-tile j
-  const int fr = lane & 15, fc = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = row0 + wm * 128 + i * 16 + fr;
-    if (m >= g.M) continue;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = col0 + wn * WTN + j * 16 + fc * 4;
-      if (n >= g.N) continue;
-      const gf4 v = acc[i][j];
-      if constexpr (OUT == 0 || OUT == 3) {
-        uint2* p = reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(g.c) + (int64_t)m * g.ldc + n);
-        float a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
-        if constexpr (OUT == 3) {
-          const uint2 o = *p;
-          a0 += bf16_lo(o.x);
-          a1 += bf16_hi(o.x);
-          a2 += bf16_lo(o.y);
-          a3 += bf16_hi(o.y);
-        }
-        uint2 o;
-        o.x = pack_bf16x2(a0, a1);
-        o.y = pack_bf16x2(a2, a3);
-        *p = o;
-      } else {
-        float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.c) + (int64_t)m * g.ldc + n);
-        float4 o = make_float4(v[0], v[1], v[2], v[3]);
-        if constexpr (OUT == 2) {
-          const float4 c = *p;
-          o.x += c.x;
-          o.y += c.y;
-          o.z += c.z;
-          o.w += c.w;
-        }
-        *p = o;
-      }
-    }
-  }
-}
-
-template <bool XMN, bool YMN, int NW>
-hipError_t launch_nw(const GemmArgs& a, int out_mode, hipStream_t stream) {
-  const int64_t nwg = (int64_t)((a.M + kBM - 1) / kBM) * ((a.N + kBN - 1) / kBN);
-  const dim3 grid((unsigned)nwg), block(NW * 64);
-  switch (out_mode) {
-    case 0: gemm_kernel<XMN, YMN, 0, NW><<<grid, block, 0, stream>>>(a); break;
-    case 1: gemm_kernel<XMN, YMN, 1, NW><<<grid, block, 0, stream>>>(a); break;
-    case 2: gemm_kernel<XMN, YMN, 2, NW><<<grid, block, 0, stream>>>(a); break;
-    default: gemm_kernel<XMN, YMN, 3, NW><<<grid, block, 0, stream>>>(a); break;
-  }
-  return hipGetLastError();
-}
-
-// LLMT_GEMM_WAVES=4|8 (read once): workgroup shape, see gemm_kernel
-inline int gemm_waves() {
-  static const int nw = [] {
-    const char* e = getenv("LLMT_GEMM_WAVES");
-    return (e && atoi(e) == 8) ? 8 : 4;
-  }();
-  return nw;
-}
-
-template <bool XMN, bool YMN>
-hipError_t launch(const GemmArgs& a, int out_mode, hipStream_t stream) {
-  return gemm_waves() == 8 ? launch_nw<XMN, YMN, 8>(a, out_mode, stream) : launch_nw<XMN, YMN, 4>(a, out_mode, stream);
 }
 
 // ---------------------------------------------------------------- SwiGLU-backward epilogue
@@ -518,6 +338,8 @@ __device__ __forceinline__ void swiglu_bwd_epilogue(const GemmArgs& g, const Swi
 // a stage is read only after every wave's pieces of it were waited for before an earlier barrier. DMAs
 // past the last stage read an empty descriptor range (zeros into slots no one reads) so the wait counts
 // stay constant. Split-K: blockIdx.y selects a contiguous slice of the stages, written as an fp32 slab.
+// OUT: 0 = bf16 store, 1 = fp32 store (split-K slab), 2 = fp32 accumulate, 3 = bf16 accumulate
+// (C = bf16(C + X.Y^T)), 4 = SwiGLU-backward epilogue (no C)
 template <bool XMN, bool YMN, int OUT, int NS>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g, int nk, int64_t slab, SwiArgs sw) {
   constexpr int AH = NS - 1;  // stages in flight ahead of the one being read
@@ -661,12 +483,6 @@ hipError_t launch_pp(const GemmArgs& a, int out_mode, int ksplit, int64_t slab, 
   return hipGetLastError();
 }
 
-// LLMT_GEMM_KERNEL=ring selects the single-group ring kernel above (read per call, for A/B runs)
-inline bool use_pp() {
-  const char* e = getenv("LLMT_GEMM_KERNEL");
-  return !(e && strcmp(e, "ring") == 0);
-}
-
 }  // namespace
 }  // namespace llmt
 
@@ -681,15 +497,9 @@ extern "C" hipError_t llmt_gemm(const void* x, const void* y, void* c, int x_mn,
   if (ldx % 8 || ldy % 8 || ldc % 4) return hipErrorInvalidValue;
   if (256 * ldx * 2 >= 0x7fffffffLL || 256 * ldy * 2 >= 0x7fffffffLL) return hipErrorInvalidValue;
   GemmArgs a{reinterpret_cast<const bf16*>(x), reinterpret_cast<const bf16*>(y), c, M, N, K, ldx, ldy, ldc};
-  if (use_pp()) {
-    if (!x_mn && !y_mn) return launch_pp<false, false>(a, out_mode, 1, 0, stream);
-    if (!x_mn && y_mn) return launch_pp<false, true>(a, out_mode, 1, 0, stream);
-    if (x_mn && y_mn) return launch_pp<true, true>(a, out_mode, 1, 0, stream);
-    return hipErrorInvalidValue;
-  }
-  if (!x_mn && !y_mn) return launch<false, false>(a, out_mode, stream);
-  if (!x_mn && y_mn) return launch<false, true>(a, out_mode, stream);
-  if (x_mn && y_mn) return launch<true, true>(a, out_mode, stream);
+  if (!x_mn && !y_mn) return launch_pp<false, false>(a, out_mode, 1, 0, stream);
+  if (!x_mn && y_mn) return launch_pp<false, true>(a, out_mode, 1, 0, stream);
+  if (x_mn && y_mn) return launch_pp<true, true>(a, out_mode, 1, 0, stream);
   return hipErrorInvalidValue;  // X MN-major with Y K-major: no linear-layer GEMM has this layout
 }
 

@@ -59,7 +59,7 @@ def _kernel_meta(text):
 # (The per-element-mask forms for segment ids without run bounds and the generic dropout kernels carry SGPR
 # spills into VGPR lanes, and the generic D=128 forward a small scratch frame: off the hot path.)
 _HOT = re.compile(r"fa_fwd3_kernelILi\d+ELi2ELi1E|fa_bwd_dq3_kernelILi\d+ELb1ELb1ELi4ELb0E|fa_bwd_dkdv5_kernelILi\d+ELb0E|"
-                  r"gemm_pp_kernel|gemm_kernel")
+                  r"gemm_pp_kernel")
 
 
 @pytest.mark.parametrize("which", ["fa", "gemm"])

@@ -410,14 +410,11 @@ def test_rope_attention_fused_matches_reference():
 
 
 # ----------------------------------------------------------------------------- GEMM (csrc/gemm.hip)
-@pytest.mark.parametrize("kernel", ["pp", "ring"])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("out", ["bf16", "bf16_acc", "fp32", "fp32_acc"])
 @pytest.mark.parametrize("M,N,K", [(520, 776, 352), (64, 128, 32), (8, 264, 96), (1024, 512, 4096)])
-def test_gemm_layouts(layout, out, M, N, K, kernel, monkeypatch):
-    # nt = forward (x . W^T), nn = dgrad (dy . W), tn = wgrad (dy^T . x); partial tiles on every edge.
-    # pp = the two-group ping-pong kernel (default), ring = the single-group ring kernel
-    monkeypatch.setenv("LLMT_GEMM_KERNEL", kernel)
+def test_gemm_layouts(layout, out, M, N, K):
+    # nt = forward (x . W^T), nn = dgrad (dy . W), tn = wgrad (dy^T . x); partial tiles on every edge
     torch.manual_seed(0)
     xb = torch.randn(M, K, device=DEV).bfloat16()
     yb = torch.randn(N, K, device=DEV).bfloat16()
