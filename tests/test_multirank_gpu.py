@@ -49,17 +49,29 @@ def reference(tmp_path_factory):
     return d, losses, params
 
 
-@pytest.mark.parametrize("mode", ["dp2_z2", "dp2_z3", "tp2"])
+MODES = ["dp2_z2", "dp2_z3", "tp2", "tp2_stages1"]
+
+
+def _run_worker(d, mode):
+    """Run the two-rank worker once per mode (cached in the module's tmp dir). tp2_stages1: tp2 with the
+    sequence collectives and GEMMs unstaged (LLMT_TP_STAGES=1)."""
+    out = d / f"{mode}.pt"
+    if not out.exists():
+        env = dict(os.environ, FULL0=str(d / "full0.pt"), PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+        if mode == "tp2_stages1":
+            env["LLMT_TP_STAGES"] = "1"
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(29600 + MODES.index(mode)),
+               os.path.join(ROOT, "tests", "multirank_gpu_worker.py"), mode.split("_stages")[0], str(out)]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
+        assert r.returncode == 0, r.stderr[-4000:]
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_two_ranks_on_one_gpu_match_single_process(reference, mode):
     d, ref_losses, ref_params = reference
-    out = d / f"{mode}.pt"
-    env = dict(os.environ, FULL0=str(d / "full0.pt"), PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(29600 + ["dp2_z2", "dp2_z3", "tp2"].index(mode)),
-           os.path.join(ROOT, "tests", "multirank_gpu_worker.py"), mode, str(out)]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0, r.stderr[-4000:]
-    got = torch.load(out, weights_only=True)
+    got = _run_worker(d, mode)
     # rank 1 runs rank 0's hipBLASLt solutions (ops.fused.agree_layouts -> gemm_lt_adopt)
     r0, r1 = got["lt_choices"]
     common = set(r0) & set(r1)
@@ -72,6 +84,22 @@ def test_two_ranks_on_one_gpu_match_single_process(reference, mode):
         num += (got["params"][k] - v).norm().item() ** 2
         den += v.norm().item() ** 2
     assert (num / den) ** 0.5 < 5e-3, mode
+
+
+def test_tp_stages_do_not_change_the_bf16_training(reference):
+    """The staged collective matmul (4 sequence chunks, grouped GEMMs, one weight-gradient GEMM over the whole
+    gathered operands) trains like the unstaged form in bf16 on the GPU: the weight gradients are one GEMM in
+    both, so no per-chunk bf16 rounding accumulates (round-5 advice)."""
+    d = reference[0]
+    a, b = _run_worker(d, "tp2"), _run_worker(d, "tp2_stages1")
+    for x, y in zip(a["losses"], b["losses"]):
+        assert abs(x - y) < 2e-3 * abs(y), (a["losses"], b["losses"])
+    assert abs(a["grad_norm"] - b["grad_norm"]) < 1e-2 * b["grad_norm"]
+    num = den = 0.0
+    for k, v in b["params"].items():
+        num += (a["params"][k] - v).norm().item() ** 2
+        den += v.norm().item() ** 2
+    assert (num / den) ** 0.5 < 1e-3
 
 
 def test_bench_two_ranks_through_the_launcher(tmp_path):
