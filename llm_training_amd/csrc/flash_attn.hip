@@ -206,8 +206,8 @@ struct AttnArgs {
   // Only the diagnostic library (_C_diag.so, built with -DLLMT_DIAG) reads it; in the production library
   // FA_PROBE is the constant 0, so no environment variable can change what the kernels compute.
   int probe;
-  // backward: non-null -> the dQ kernel computes delta = rowsum(dO * O) itself and writes the packed per-tile
-  // row constants the dK/dV kernel reads here (no separate prep pass); null -> the prep kernel ran
+  // backward (dq3 / dkdv5, always set): the dQ kernel computes delta = rowsum(dO * O) itself and writes the
+  // packed per-tile row constants the dK/dV kernel reads here (no separate prep pass)
   float* ldw;
   // RoPE fused into the kernels (ops/fused.py _RopeFlashAttnFn; the reference applies it as its own op,
   // src/llm_training/ops/rope_op.py:10-20 <- models/llama/llama_model.py:553). Token (b, s) sits at position
@@ -1812,7 +1812,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_fwd3_kernel(AttnArgs a) {
 // (the forward's LSE: no online max), then batched K^T transposed reads -> dQ^T += K^T . dS^T.
 // dQ = scale * sum; the row constants come straight from lse / delta. delta = rowsum(O * dO) is computed
 // here from the wave's own O and dO rows (and written, with -lse/scale, the segment ids and -lse*log2e, as
-// the ld tiles the dK/dV kernel reads next); with LLMT_FA_PREP=1 it comes from the prep kernel instead.
+// the ld tiles the dK/dV kernel reads next).
 // NW = 8: two query heads of one kv group per workgroup sharing the K/V ring (as fa_fwd3_kernel)
 // dS = P (dP - delta) with P = exp2(x): the exp, the subtraction and the product as three single-lane VALU
 // instructions in one asm block (the product reads the exp result one instruction later: its trans-use wait
@@ -1883,7 +1883,7 @@ __global__ __launch_bounds__(NW * 64, 2) void fa_bwd_dq3_kernel(AttnArgs a) {
   if (a.ldw) {
     // the backward prep fused in: delta = rowsum(dO * O) from this lane's half row (64 of D elements, the
     // other half in lane r + 32), then the row constants of this wave's 32-row tile for the dK/dV kernel
-    // (fa_bwd_prep128_kernel's layout: -lse / scale, -delta, segment id, -lse * log2e)
+    // (per 32-row tile: -lse / scale, -delta, segment id, -lse * log2e)
     const bf16* opr = a.o + (int64_t)b * a.o_sb + (int64_t)h * a.o_sh + (int64_t)min(qrow, S - 1) * a.o_ss;
     float dl = 0.f;
 #pragma unroll
