@@ -69,6 +69,17 @@ const std::vector<int> kGsu = [] {
 }();
 constexpr int64_t kGsuMaxTiles = 1024;
 
+// Problems restricted to non-stream-K solutions (dp > 1 / tp > 1, and the layout table's "/nosk" twins) take
+// the heuristic's first non-stream-K solution (default), or time their candidates on first sight
+// (LLMT_GEMM_NOSK_TIME=1). Alternating step runs on one box: the multi-GPU schedule on one GPU (every GEMM
+// non-stream-K) 1462.0 / 1462.3 / 1466.7 ms heuristic vs 1461.9 / 1464.7 / 1463.8 timed, the one-GPU step
+// 1451.5 / 1451.2 vs 1453.3 / 1453.7 (profiles/r6_nosk_time_ab.jsonl): the same speed, and the heuristic's
+// choice is the same on every rank by construction, with no first-sight timing under collectives.
+const bool kTimeNoSk = [] {
+  const char* e = std::getenv("LLMT_GEMM_NOSK_TIME");
+  return e && e[0] == '1';
+}();
+
 struct State {
   std::mutex mu;
   std::map<int, hipblasLtHandle_t> handles;
@@ -223,7 +234,7 @@ void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool t
     const bool gsu_try = !kGsu.empty() && batch == 1 && ((m + 255) / 256) * ((n + 255) / 256) < kGsuMaxTiles;
     if (pre != s.preset.end() && pre->second.first < got) {
       best = Choice{res[pre->second.first].algo, pre->second.first, 0.f, pre->second.second};
-    } else if ((s.tune || !streamk || gsu_try) && (got > 1 || gsu_try)) {  // non-stream-K candidates are always timed
+    } else if ((s.tune || (!streamk && kTimeNoSk) || gsu_try) && (got > 1 || gsu_try)) {
       // time every candidate on the live operands; the output goes to a scratch tensor so an
       // accumulating call (beta = 1) is not disturbed
       auto scratch = at::empty_like(C);

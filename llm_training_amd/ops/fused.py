@@ -166,8 +166,8 @@ def agree_layouts(group=None) -> int:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) <= 1:
         return 0
-    # rank 0's hipBLASLt solution choices travel with its layouts: below stream-K (dp > 1 / tp > 1) each rank
-    # times the library's candidates on first sight, under its own collectives, and could keep a different
+    # rank 0's hipBLASLt solution choices travel with its layouts: a rank that timed a problem's candidates
+    # (LLMT_GEMM_TUNE / LLMT_GEMM_NOSK_TIME / LLMT_GEMM_GSU), under its own collectives, could keep a different
     # kernel for the same problem (csrc/blaslt.cpp gemm_lt_adopt)
     lt = native_available() and torch.cuda.is_available()
     mine = {layout_key_str(k): v for k, v in _LAYOUT_CACHE.items()}
