@@ -139,14 +139,19 @@ def _layout_table() -> dict:
     return _LAYOUT_TABLE[0]
 
 
+# interleaved timing rounds per layout decision (LLMT_GEMM_LAYOUT_ROUNDS; more rounds time the candidates
+# under a longer, more sustained load, as the step runs them)
+_LAYOUT_ROUNDS = max(1, int(os.environ.get("LLMT_GEMM_LAYOUT_ROUNDS", "2")))
+
+
 def _time_variants(variants: dict) -> dict:
     """Milliseconds per call of each variant on the current stream (host-synchronising)."""
     for fn in variants.values():
         fn()  # warm-up (and hipBLASLt's own solution choice for the problem)
-    # two interleaved rounds of 2 runs per variant, the faster round kept: a clock or power swing during
-    # one variant's window cannot decide the choice on its own
+    # interleaved rounds of 2 runs per variant, the faster round kept: a clock or power swing during one
+    # variant's window cannot decide the choice on its own
     times = {name: float("inf") for name in variants}
-    for _ in range(2):
+    for _ in range(_LAYOUT_ROUNDS):
         for name, fn in variants.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
