@@ -471,6 +471,10 @@ def main():
         }
         if os.environ.get("LLMT_GEMM_LAYOUT_DUMP"):
             F_layouts.dump_layouts(os.environ["LLMT_GEMM_LAYOUT_DUMP"])
+        if os.environ.get("LLMT_GEMM_LT_EXPORT"):  # hipBLASLt's solution per problem ("key rank ms name gsuN")
+            from llm_training_amd.ops.native import lib as _lib
+            with open(os.environ["LLMT_GEMM_LT_EXPORT"], "w") as f:
+                f.write(_lib().gemm_lt_export())
         print(json.dumps(out), flush=True)
     wd.arm("shutdown")
     if dist.is_initialized():

@@ -69,6 +69,13 @@ const std::vector<int> kGsu = [] {
 }();
 constexpr int64_t kGsuMaxTiles = 1024;
 
+// interleaved timing rounds per timed problem (LLMT_GEMM_TUNE_ROUNDS, default 1)
+const int kTuneRounds = [] {
+  const char* e = std::getenv("LLMT_GEMM_TUNE_ROUNDS");
+  const int v = e ? std::atoi(e) : 1;
+  return v > 0 ? v : 1;
+}();
+
 // Problems restricted to non-stream-K solutions (dp > 1 / tp > 1, and the layout table's "/nosk" twins) take
 // the heuristic's first non-stream-K solution (default), or time their candidates on first sight
 // (LLMT_GEMM_NOSK_TIME=1). Alternating step runs on one box: the multi-GPU schedule on one GPU (every GEMM
@@ -242,23 +249,31 @@ void gemm_lt_impl(const at::Tensor& A, const at::Tensor& B, at::Tensor C, bool t
       hipEvent_t e0, e1;
       (void)hipEventCreate(&e0);
       (void)hipEventCreate(&e1);
-      for (int i = 0; i < got; ++i) {
-        if (res[i].state != HIPBLAS_STATUS_SUCCESS) continue;
-        auto run = [&]() {
-          return hipblasLtMatmul(h, d.op, &alpha, A.data_ptr(), d.a, B.data_ptr(), d.b, &beta, scratch.data_ptr(),
-                                 d.c, scratch.data_ptr(), d.c, &res[i].algo, ws.data_ptr(), kWorkspace, stream);
-        };
-        if (run() != HIPBLAS_STATUS_SUCCESS) continue;  // warm-up; skips solutions that fail to launch
-        (void)hipEventRecord(e0, stream);
-        constexpr int kReps = 3;
-        for (int r = 0; r < kReps; ++r) run();
-        (void)hipEventRecord(e1, stream);
-        (void)hipEventSynchronize(e1);
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        ms /= kReps;
-        if (best.ms < 0.f || ms < best.ms) best = Choice{res[i].algo, i, ms, 0};
-        if (!gsu_try) continue;
+      constexpr int kReps = 3;
+      auto run_i = [&](int i) {
+        return hipblasLtMatmul(h, d.op, &alpha, A.data_ptr(), d.a, B.data_ptr(), d.b, &beta, scratch.data_ptr(), d.c,
+                               scratch.data_ptr(), d.c, &res[i].algo, ws.data_ptr(), kWorkspace, stream);
+      };
+      // kTuneRounds interleaved rounds of kReps runs per candidate, summed: more rounds time the candidates
+      // under a longer, sustained load instead of one burst each
+      std::vector<int> ok;
+      for (int i = 0; i < got; ++i)
+        if (res[i].state == HIPBLAS_STATUS_SUCCESS && run_i(i) == HIPBLAS_STATUS_SUCCESS) ok.push_back(i);  // warm-up
+      std::vector<float> tot(got, 0.f);
+      for (int rnd = 0; rnd < kTuneRounds; ++rnd)
+        for (int i : ok) {
+          (void)hipEventRecord(e0, stream);
+          for (int r = 0; r < kReps; ++r) run_i(i);
+          (void)hipEventRecord(e1, stream);
+          (void)hipEventSynchronize(e1);
+          float ms = 0.f;
+          (void)hipEventElapsedTime(&ms, e0, e1);
+          tot[i] += ms / kReps / kTuneRounds;
+        }
+      for (int i : ok)
+        if (best.ms < 0.f || tot[i] < best.ms) best = Choice{res[i].algo, i, tot[i], 0};
+      for (int i : ok) {
+        if (!gsu_try) break;
         for (int gs : kGsu) {  // the same solution with the library's own split-K
           hipblaslt_ext::Gemm eg(h, d.op, &alpha, A.data_ptr(), d.a, B.data_ptr(), d.b, &beta, scratch.data_ptr(), d.c,
                                  scratch.data_ptr(), d.c);
