@@ -268,6 +268,13 @@ static int rope_kind() {
   return rope_rows() ? 1 : 0;
 }
 
+// rows of one row-blocked launch: grid.y holds at most 65535, so T is split into equal launches (65536 tokens:
+// two of 32768, not 65535 + a one-row launch)
+static int64_t rows_per_launch(int64_t T) {
+  const int64_t n = (T + 65534) / 65535;
+  return (T + n - 1) / n;
+}
+
 // LLMT_EW_ROWS=0 selects the flat grid-stride SwiGLU kernels (read per call, for A/B runs)
 static bool ew_rows(int64_t T) {
   const char* e = getenv("LLMT_EW_ROWS");
@@ -279,8 +286,9 @@ extern "C" hipError_t llmt_swiglu_fwd(const void* gu, void* c, int64_t T, int I,
   const int64_t n8 = T * (I / 8);
   if (n8 == 0) return hipSuccess;
   if (ew_rows(T)) {
-    for (int64_t t0 = 0; t0 < T; t0 += 65535) {  // grid.y limit
-      const int64_t nt = T - t0 < 65535 ? T - t0 : 65535;
+    const int64_t rows = rows_per_launch(T);
+    for (int64_t t0 = 0; t0 < T; t0 += rows) {
+      const int64_t nt = T - t0 < rows ? T - t0 : rows;
       swiglu_fwd_rows_kernel<<<dim3((I / 8 + 255) / 256, (unsigned)nt), 256, 0, stream>>>(
           (const bf16x8*)gu + t0 * (I / 4), (bf16x8*)c + t0 * (I / 8), I / 8);
     }
@@ -296,8 +304,9 @@ extern "C" hipError_t llmt_swiglu_bwd(const void* gu, const void* dc, void* dgu,
   const int64_t n8 = T * (I / 8);
   if (n8 == 0) return hipSuccess;
   if (ew_rows(T)) {
-    for (int64_t t0 = 0; t0 < T; t0 += 65535) {
-      const int64_t nt = T - t0 < 65535 ? T - t0 : 65535;
+    const int64_t rows = rows_per_launch(T);
+    for (int64_t t0 = 0; t0 < T; t0 += rows) {
+      const int64_t nt = T - t0 < rows ? T - t0 : rows;
       swiglu_bwd_rows_kernel<<<dim3((I / 8 + 255) / 256, (unsigned)nt), 256, 0, stream>>>(
           (const bf16x8*)gu + t0 * (I / 4), (const bf16x8*)dc + t0 * (I / 8), (bf16x8*)dgu + t0 * (I / 4), I / 8);
     }

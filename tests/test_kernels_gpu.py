@@ -66,6 +66,27 @@ def test_swiglu(I):
     assert _rel(gu.grad, gr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("T", [65536, 131071 + 300])
+def test_swiglu_rows_split_over_launches(T, monkeypatch):
+    """The row-blocked SwiGLU kernels split T > 65535 rows (grid.y) into equal launches: forward and backward
+    bitwise equal to the flat grid-stride kernels (LLMT_EW_ROWS=0)."""
+    torch.manual_seed(0)
+    I = 64
+    gu = torch.randn(T, 2 * I, device=DEV, dtype=torch.bfloat16)
+    dc = torch.randn(T, I, device=DEV, dtype=torch.bfloat16)
+
+    def run():
+        g = gu.clone().requires_grad_(True)
+        c = F_.swiglu(g)
+        c.backward(dc)
+        return c.detach(), g.grad
+
+    rows = run()
+    monkeypatch.setenv("LLMT_EW_ROWS", "0")
+    flat = run()
+    assert torch.equal(rows[0], flat[0]) and torch.equal(rows[1], flat[1])
+
+
 @pytest.mark.parametrize("D", [64, 96, 128])
 def test_rope_inplace_roundtrip(D):
     torch.manual_seed(0)
