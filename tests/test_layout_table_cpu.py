@@ -41,3 +41,13 @@ def test_table_entries_name_offered_candidates():
         assert re.fullmatch(_VALID[kind], val), (key, val)
         if val.endswith("/nosk"):  # a non-stream-K twin is offered only when stream-K is allowed
             assert key.endswith("|True"), (key, val)
+
+
+def test_table_loaded_only_on_its_arch(monkeypatch):
+    """ops/fused.py loads the shipped table only on the architecture it was measured on (its `arch` field); on
+    another GPU the layouts are timed on first sight instead (round-5 advice). No device (CPU) loads it."""
+    from llm_training_amd.ops import fused as F_
+    for arch, expect in (("gfx950", True), ("gfx942", False), (None, True)):
+        monkeypatch.setattr(F_, "_device_arch", lambda a=arch: a)
+        monkeypatch.setattr(F_, "_LAYOUT_TABLE", [None])
+        assert bool(F_._layout_table()) == expect, arch
