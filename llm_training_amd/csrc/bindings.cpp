@@ -16,7 +16,7 @@
 extern "C" {
 hipError_t llmt_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* res_out, float* rstd,
                             int T, int H, float eps, hipStream_t stream);
-int llmt_rmsnorm_bwd_nblocks(int T);
+int llmt_rmsnorm_bwd_nblocks(int T, int H);
 hipError_t llmt_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres,
                             void* dx, float* dw_part, void* dw, int dw_is_fp32, int accumulate, int T, int H,
                             hipStream_t stream);
@@ -155,10 +155,13 @@ std::tuple<at::Tensor, at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::T
     }
     dwp = dw.data_ptr();
   }
-  const int nblk = llmt_rmsnorm_bwd_nblocks((int)T);
-  auto part = at::empty({compute_dw ? (int64_t)nblk * H : H}, x.options().dtype(at::kFloat));
+  const int nblk = llmt_rmsnorm_bwd_nblocks((int)T, (int)H);
+  // the kernels write nblk x H fp32 partials only when a weight gradient is wanted (null otherwise)
+  at::Tensor part;
+  if (compute_dw) part = at::empty({(int64_t)nblk * H}, x.options().dtype(at::kFloat));
   check(llmt_rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), drp, dx.data_ptr(),
-                         part.data_ptr<float>(), dwp, dw_fp32, accumulate ? 1 : 0, (int)T, (int)H, cur_stream()),
+                         compute_dw ? part.data_ptr<float>() : nullptr, dwp, dw_fp32, accumulate ? 1 : 0, (int)T,
+                         (int)H, cur_stream()),
         "rmsnorm_bwd");
   return {dx, dw};
 }

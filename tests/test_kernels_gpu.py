@@ -52,6 +52,29 @@ def test_rmsnorm(H, residual):
         assert _rel(r.grad, rr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("H", [3072, 4096])
+def test_rmsnorm_bwd_frozen_weight(H):
+    """No weight gradient wanted (a frozen norm weight): the kernel writes no dW partials (it once wrote
+    nblocks x H of them into an H-float buffer) and dx is the same as with the weight gradient."""
+    torch.manual_seed(0)
+    T = 4099  # several blocks, a ragged last one
+    L = lib()
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    dy, dres = torch.randn_like(x), torch.randn_like(x)
+    rstd = L.rmsnorm_fwd(x, None, w, 1e-5)[2]
+    dx, dw = L.rmsnorm_bwd(dy, x, w, rstd, dres, None, False, True)
+    dx2, _ = L.rmsnorm_bwd(dy, x, w, rstd, dres, None, False, False)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx2)
+    xf, wf, dyf = x.float(), w.float(), dy.float()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    dn = dyf * wf
+    dx_ref = r * (dn - xf * r * (dn * xf * r).mean(-1, keepdim=True)) + dres.float()
+    assert _rel(dx, dx_ref) < 1e-2
+    assert _rel(dw, (dyf * (xf * r).bfloat16().float()).sum(0)) < 1e-2
+
+
 @pytest.mark.parametrize("I", [512, 14336])
 def test_swiglu(I):
     torch.manual_seed(0)
