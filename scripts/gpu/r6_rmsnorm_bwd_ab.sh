@@ -1,5 +1,5 @@
-# RMSNorm backward: one wave per row vs two waves per row (LLMT_RMSNORM_BWD_PAIR 0 / 1 / 2), kernel tests then
-# the interleaved A/B (benchmarks/ab/ab_rmsnorm_bwd.py) -> gpurun_out/r6_rmsnorm_bwd_ab.jsonl
+# RMSNorm backward A/B as run in round 6 (LLMT_RMSNORM_BWD_PAIR 0 / 1 / 2 selected the one-wave-per-row kernel and
+# two two-waves-per-row forms; only the winner is left, so the variable is now ignored) -> profiles/r6_rmsnorm_bwd_ab.jsonl
 set -eo pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "rmsnorm" > gpurun_out/r6_rms_tests.log 2>&1
