@@ -186,22 +186,26 @@ __global__ __launch_bounds__(256, NH <= 4 ? 4 : 2) void rmsnorm_bwd_kernel(
 }
 
 // Column reduction of the per-block dW partials: out[j] (+)= sum_b part[b][j].
-// 256 threads = 64 columns x 4 row groups (coalesced 256-byte rows), LDS combine of the 4 groups.
+// 256 threads = 16 columns x 16 row groups (64-byte row runs), LDS combine of the groups: H / 16 blocks (256 at
+// H = 4096) spread the 1024 partial rows over the chip (64 columns x 4 groups per block ran 64 blocks: 21 us a
+// call at 1024 partials, r6_llama8b_1gpu_mb4_final3_kernel_stats.md).
 template <typename OutT>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, OutT* __restrict__ out,
                                                      int nparts, int H, int accumulate) {
-  __shared__ float red[4][64];
-  const int cx = threadIdx.x & 63, gy = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + cx;
+  __shared__ float red[16][17];
+  const int cx = threadIdx.x & 15, gy = threadIdx.x >> 4;
+  const int j = blockIdx.x * 16 + cx;
   float s = 0.f;
   if (j < H) {
 #pragma unroll 4
-    for (int b = gy; b < nparts; b += 4) s += part[(int64_t)b * H + j];
+    for (int b = gy; b < nparts; b += 16) s += part[(int64_t)b * H + j];
   }
   red[gy][cx] = s;
   __syncthreads();
   if (gy == 0 && j < H) {
-    float t = red[0][cx] + red[1][cx] + red[2][cx] + red[3][cx];
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][cx];
     if (accumulate) t += (float)out[j];
     out[j] = (OutT)t;
   }
@@ -286,7 +290,7 @@ extern "C" hipError_t llmt_rmsnorm_bwd(const void* dy, const void* x, const void
     }
   }
   if (dw) {
-    const int g = (H + 63) / 64;
+    const int g = (H + 15) / 16;
     if (dw_is_fp32)
       colsum_kernel<float><<<g, 256, 0, stream>>>(dw_part, (float*)dw, T > 0 ? nblk : 0, H, accumulate);
     else
