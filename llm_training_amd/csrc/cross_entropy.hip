@@ -5,8 +5,9 @@
 // loss_parallel / log_softmax().gather() paths of DPO/ORPO (reference
 // src/llm_training/lms/dpo/dpo.py:73-114, lms/orpo/orpo.py:61-93).
 //
-// One 256-thread workgroup per row of bf16 logits [N, V_local] (the row is streamed in 16-byte
-// vectors). Pass 1: per-thread online max / sum-exp, block-reduced -> lse. Pass 2 (optional):
+// One 1024-thread workgroup per row of bf16 logits [N, V_local] holding the row in registers (ce_reg_kernel,
+// rows of up to 131072 logits in 16-byte chunks), else one 256-thread workgroup streaming the row in 16-byte
+// vectors (ce_kernel). Pass 1: max / sum-exp, block-reduced -> lse. Pass 2 (optional):
 // overwrite the row with coef * (softmax - onehot(label)), i.e. the gradient of
 //   coef * (lse - logit[label])
 // w.r.t. the logits, so the logits buffer doubles as the dlogits buffer (no extra [N, V] tensor).
@@ -130,6 +131,102 @@ __global__ __launch_bounds__(256) void ce_kernel(bf16* __restrict__ logits, int6
   }
 }
 
+// The same for rows of up to 1024 * NCH 16-byte chunks (V <= 131072 at NCH = 16) with V % 8 == 0 and aligned
+// rows: one 1024-thread workgroup per row holds the whole row in registers (NCH chunks per thread), so the row
+// is read from HBM once; the two-pass kernel above reads it again for the gradient, and with 8 rows of
+// 256 KB in flight per CU that second read misses the caches.
+template <int NCH>
+__global__ __launch_bounds__(1024) void ce_reg_kernel(bf16* __restrict__ logits, int64_t ld, int V,
+                                                      const int64_t* __restrict__ labels, int64_t vocab_start,
+                                                      int64_t ignore_index, const float* __restrict__ lse_in,
+                                                      float* __restrict__ lse_out, float* __restrict__ tgt_out,
+                                                      float* __restrict__ loss_out, const float* __restrict__ coef_row,
+                                                      const float* __restrict__ coef_scalar, int write_grad,
+                                                      int64_t vocab_total, int* __restrict__ err,
+                                                      float* __restrict__ rowsum_out) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  bf16* x = logits + row * ld;
+  bf16x8* xv = reinterpret_cast<bf16x8*>(x);
+  const int64_t lab = labels[row];
+  const bool valid = lab != ignore_index;
+  const int64_t lloc = lab - vocab_start;
+  const bool local_hit = valid && lloc >= 0 && lloc < V;
+  const int tid = threadIdx.x;
+  if (err && tid == 0 && valid && (lab < 0 || (vocab_total > 0 && lab >= vocab_total))) err[1] = 1;
+  const int V8 = V >> 3;
+  bf16x8 c[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int j = tid + 1024 * k;
+    if (j < V8) c[k] = xv[j];
+  }
+  float lse;
+  if (lse_in) {
+    lse = lse_in[row];
+  } else {
+    // the row is in registers: its max first, then the sum of exp against it (no online rescaling)
+    float m = -INFINITY, rsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      if (tid + 1024 * k < V8) {
+        float f[8];
+        unpack8(c[k], f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          m = fmaxf(m, f[i]);
+          rsum += f[i];
+        }
+      }
+    }
+    const float gm = block_max<16>(m, red);
+    float s = 0.f;
+    if (gm != -INFINITY) {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        if (tid + 1024 * k < V8) {
+          float f[8];
+          unpack8(c[k], f);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s += __expf(f[i] - gm);
+        }
+      }
+    }
+    const float gs = block_sum<16>(s, red);
+    lse = gm + __logf(gs);
+    if (rowsum_out) {
+      const float rs = block_sum<16>(rsum, red);
+      if (tid == 0) rowsum_out[row] = rs;
+    }
+  }
+  const float tgt = local_hit ? bf2f(x[lloc]) : 0.f;
+  if (tid == 0) {
+    if (lse_out) lse_out[row] = lse;
+    if (tgt_out) tgt_out[row] = tgt;
+    if (loss_out) loss_out[row] = valid ? (lse - tgt) : 0.f;
+  }
+  if (!write_grad) return;
+  __syncthreads();  // every thread has read x[lloc] before anyone overwrites it
+  float coef = valid ? 1.f : 0.f;
+  if (coef_row) coef *= coef_row[row];
+  if (coef_scalar) coef *= coef_scalar[0];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int j = tid + 1024 * k;
+    if (j < V8) {
+      float f[8];
+      unpack8(c[k], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float g = __expf(f[i] - lse);
+        if (local_hit && (int64_t)(j * 8 + i) == lloc) g -= 1.f;
+        f[i] = coef * g;
+      }
+      xv[j] = pack8(f);
+    }
+  }
+}
+
 }  // namespace llmt
 
 using namespace llmt;
@@ -141,7 +238,21 @@ extern "C" hipError_t llmt_cross_entropy(void* logits, int64_t N, int64_t ld, in
                                          float* rowsum_out, hipStream_t stream) {
   if (N == 0) return hipSuccess;
   const bool vec = (ld % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) & 15) == 0);
-  if (vec)
+  // rows of up to 131072 logits in 16-byte chunks: the one-pass kernel (8192 x 128256: 1.222 -> 0.920 ms,
+  // 8192 x 32064: 0.202 -> 0.156 ms against the two-pass one, profiles/r6_ce_ab.jsonl)
+  const bool reg_ok = vec && V % 8 == 0;
+  const int nch = (V / 8 + 1023) / 1024;
+#define CE_REG(NCH)                                                                                          \
+  ce_reg_kernel<NCH><<<(unsigned)N, 1024, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index,  \
+                                                      lse_in, lse_out, tgt_out, loss_out, coef_row, coef_scalar,  \
+                                                      write_grad, vocab_total, err, rowsum_out)
+  if (reg_ok && nch <= 4)
+    CE_REG(4);
+  else if (reg_ok && nch <= 8)
+    CE_REG(8);
+  else if (reg_ok && nch <= 16)
+    CE_REG(16);
+  else if (vec)
     ce_kernel<true><<<(unsigned)N, 256, 0, stream>>>((bf16*)logits, ld, V, labels, vocab_start, ignore_index, lse_in,
                                                      lse_out, tgt_out, loss_out, coef_row, coef_scalar, write_grad,
                                                      vocab_total, err, rowsum_out);
