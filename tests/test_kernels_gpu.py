@@ -231,7 +231,7 @@ def test_kernel_index_checks():
         check_kernel_errors()
 
 
-@pytest.mark.parametrize("V", [32064, 128256, 50257])
+@pytest.mark.parametrize("V", [32064, 128256, 50257, 152064])  # one-pass kernel up to 131072, two-pass above and for V % 8 != 0
 def test_cross_entropy(V):
     torch.manual_seed(0)
     N = 257
